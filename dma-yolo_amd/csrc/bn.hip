@@ -1,0 +1,328 @@
+// BatchNorm2d (train: batch statistics; eval: running statistics) fused with the activation,
+// NHWC.  Replaces nn.BatchNorm2d + nn.SiLU / nn.Hardswish of models/common.py:67-73 (Conv),
+// :1168-1180 (CoorAttention.bn1+act), :1281-1307 (SCConv k2/k3/k4 BN, no act).
+// BN semantics: torch batch_norm with eps/momentum from the module (utils/torch_utils.py:161-170
+// sets 1e-3 / 0.03): normalise with the biased batch variance, update running_var with the
+// unbiased one.  Batch sums arrive as per-row-block partials (written by the conv epilogue or by
+// bn_stats below) and are finalised in f64.
+#include "common.h"
+
+namespace {
+
+// -------- per-channel batch statistics from a stored activation (when no fused conv epilogue)
+template <typename T>
+__global__ void bn_stats_kernel(const T* __restrict__ z, long zps, long M, int C, int rows_per_block,
+                                float* __restrict__ psum, float* __restrict__ psq) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  __shared__ float s1[4][64], s2[4][64];
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(M, r0 + rows_per_block);
+    for (long m = r0 + ty; m < r1; m += 4) {
+      float v = to_f(z[m * zps + c]);
+      a += v;
+      b += v * v;
+    }
+  }
+  s1[ty][threadIdx.x & 63] = a;
+  s2[ty][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    const int l = threadIdx.x;
+    psum[(long)blockIdx.x * C + c] = s1[0][l] + s1[1][l] + s1[2][l] + s1[3][l];
+    psq[(long)blockIdx.x * C + c] = s2[0][l] + s2[1][l] + s2[2][l] + s2[3][l];
+  }
+}
+
+// -------- finalise: partial rows -> mean, invstd, scale, shift (+ running-stat update)
+__global__ void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int P, int C,
+                                   double count, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, long long* nbt, float momentum,
+                                   float eps, int update, float* __restrict__ mean, float* __restrict__ invstd,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x;
+  __shared__ double sa[256], sb[256];
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    a += (double)psum[(long)p * C + c];
+    b += (double)psq[(long)p * C + c];
+  }
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sa[threadIdx.x] += sa[threadIdx.x + s];
+      sb[threadIdx.x] += sb[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double mu = sa[0] / count;
+    double var = sb[0] / count - mu * mu;
+    if (var < 0) var = 0;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    mean[c] = (float)mu;
+    invstd[c] = is;
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    scale[c] = g * is;
+    shift[c] = bb - (float)mu * g * is;
+    if (update) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+      if (c == 0 && nbt) *nbt += 1;
+    }
+  }
+}
+
+// eval mode: scale/shift from running stats
+__global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                    float eps, int C, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = 1.f / sqrtf(rvar[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - rmean[c] * g * is;
+}
+
+// -------- y = act(z * scale + shift) (+ res)
+template <typename T, bool VEC>
+__global__ void bn_act_fwd_kernel(const T* __restrict__ z, long zps, const float* __restrict__ scale,
+                                  const float* __restrict__ shift, int act, const T* __restrict__ res, long rps,
+                                  T* __restrict__ y, long yps, long M, int C) {
+  constexpr int VW = Traits<T>::VW;
+  const int cv = VEC ? C / VW : C;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / cv;
+    const int c = (int)(i % cv) * (VEC ? VW : 1);
+    if (VEC) {
+      float f[VW], r[VW];
+      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c), f);
+      if (res) unpack<T>(*reinterpret_cast<const uint4*>(res + m * rps + c), r);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        f[j] = act_fwd(act, f[j] * scale[c + j] + shift[c + j]);
+        if (res) f[j] += r[j];
+      }
+      *reinterpret_cast<uint4*>(y + m * yps + c) = pack<T>(f);
+    } else {
+      float v = act_fwd(act, to_f(z[m * zps + c]) * scale[c] + shift[c]);
+      if (res) v += to_f(res[m * rps + c]);
+      y[m * yps + c] = from_f<T>(v);
+    }
+  }
+}
+
+// -------- backward reduce: per channel  sum(du), sum(du * xhat), du = dy * act'(u)
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* __restrict__ z, long zps, const T* __restrict__ dy, long dps,
+                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                     const float* __restrict__ mean, const float* __restrict__ invstd, int act,
+                                     long M, int C, int rows_per_block, float* __restrict__ pdb,
+                                     float* __restrict__ pdg) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  __shared__ float s1[4][64], s2[4][64];
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const float sc = scale[c], sh = shift[c], mu = mean[c], is = invstd[c];
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(M, r0 + rows_per_block);
+    for (long m = r0 + ty; m < r1; m += 4) {
+      const float zv = to_f(z[m * zps + c]);
+      const float du = to_f(dy[m * dps + c]) * act_grad(act, zv * sc + sh);
+      a += du;
+      b += du * (zv - mu) * is;
+    }
+  }
+  s1[ty][threadIdx.x & 63] = a;
+  s2[ty][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    const int l = threadIdx.x;
+    pdb[(long)blockIdx.x * C + c] = s1[0][l] + s1[1][l] + s1[2][l] + s1[3][l];
+    pdg[(long)blockIdx.x * C + c] = s2[0][l] + s2[1][l] + s2[2][l] + s2[3][l];
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdb, const float* __restrict__ pdg, int P, int C,
+                                       double count, const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ ca,
+                                       float* __restrict__ cb, float* __restrict__ cc) {
+  const int c = blockIdx.x;
+  __shared__ double sa[256], sb[256];
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    a += (double)pdb[(long)p * C + c];
+    b += (double)pdg[(long)p * C + c];
+  }
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sa[threadIdx.x] += sa[threadIdx.x + s];
+      sb[threadIdx.x] += sb[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float db = (float)sa[0], dg = (float)sb[0];
+    if (dbeta) dbeta[c] = db;
+    if (dgamma) dgamma[c] = dg;
+    const float g = gamma ? gamma[c] : 1.f;
+    const float k = g * invstd[c];
+    ca[c] = k;
+    cb[c] = (float)(-(double)k * sa[0] / count);
+    cc[c] = (float)(-(double)k * sb[0] / count);
+  }
+}
+
+// dz = ca*du + cb + cc*xhat   (train);  eval: cb = cc = 0, ca = scale
+template <typename T, bool VEC>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ z, long zps, const T* __restrict__ dy, long dps,
+                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                    const float* __restrict__ mean, const float* __restrict__ invstd, int act,
+                                    const float* __restrict__ ca, const float* __restrict__ cb,
+                                    const float* __restrict__ cc, T* __restrict__ dz, long dzps, long M, int C) {
+  constexpr int VW = Traits<T>::VW;
+  const int cv = VEC ? C / VW : C;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / cv;
+    const int c0 = (int)(i % cv) * (VEC ? VW : 1);
+    if (VEC) {
+      float zf[VW], gf[VW], o[VW];
+      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
+      unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const int c = c0 + j;
+        const float du = gf[j] * act_grad(act, zf[j] * scale[c] + shift[c]);
+        o[j] = ca[c] * du + cb[c] + cc[c] * (zf[j] - mean[c]) * invstd[c];
+      }
+      *reinterpret_cast<uint4*>(dz + m * dzps + c0) = pack<T>(o);
+    } else {
+      const int c = c0;
+      const float zv = to_f(z[m * zps + c]);
+      const float du = to_f(dy[m * dps + c]) * act_grad(act, zv * scale[c] + shift[c]);
+      dz[m * dzps + c] = from_f<T>(ca[c] * du + cb[c] + cc[c] * (zv - mean[c]) * invstd[c]);
+    }
+  }
+}
+
+inline bool vec_ok(int VW, int C, long s1, long s2, long s3, const void* p1, const void* p2, const void* p3) {
+  auto al = [](const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; };
+  return C % VW == 0 && s1 % VW == 0 && s2 % VW == 0 && s3 % VW == 0 && al(p1) && al(p2) && al(p3);
+}
+
+}  // namespace
+
+DMY_API int dmy_bn_partial_rows(long M) {
+  long p = (M + 255) / 256;
+  return (int)(p < 1024 ? (p < 1 ? 1 : p) : 1024);
+}
+
+DMY_API int dmy_bn_stats(int dtype, const void* z, long zps, long M, int C, float* psum, float* psq, void* stream) {
+  const int P = dmy_bn_partial_rows(M);
+  const int rpb = (int)((M + P - 1) / P);
+  dim3 grid(P, ceil_div(C, 64));
+  if (dtype) bn_stats_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)z, zps, M, C, rpb, psum, psq);
+  else bn_stats_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)z, zps, M, C, rpb, psum, psq);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
+                            const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                            int update, float* mean, float* invstd, float* scale, float* shift, void* stream) {
+  bn_finalize_kernel<<<C, 256, 0, (hipStream_t)stream>>>(psum, psq, P, C, count, gamma, beta, rmean, rvar, nbt,
+                                                         momentum, eps, update, mean, invstd, scale, shift);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_eval_coef(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                             int C, float* scale, float* shift, void* stream) {
+  bn_eval_coef_kernel<<<ceil_div(C, 256), 256, 0, (hipStream_t)stream>>>(gamma, beta, rmean, rvar, eps, C, scale, shift);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scale, const float* shift, int act,
+                           const void* res, long rps, void* y, long yps, long M, int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int VW = dtype ? 8 : 4;
+  const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res);
+  const long work = M * (vec ? C / VW : C);
+  const int grid = grid_cap(ceil_div(work, 256), 8192);
+  if (dtype) {
+    if (vec) bn_act_fwd_kernel<bf16, true><<<grid, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+    else bn_act_fwd_kernel<bf16, false><<<grid, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+  } else {
+    if (vec) bn_act_fwd_kernel<float, true><<<grid, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
+    else bn_act_fwd_kernel<float, false><<<grid, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
+  }
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
+                              const float* shift, const float* mean, const float* invstd, int act, long M, int C,
+                              float* pdb, float* pdg, void* stream) {
+  const int P = dmy_bn_partial_rows(M);
+  const int rpb = (int)((M + P - 1) / P);
+  dim3 grid(P, ceil_div(C, 64));
+  if (dtype)
+    bn_bwd_reduce_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
+  else
+    bn_bwd_reduce_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_bwd_finalize(const float* pdb, const float* pdg, int P, int C, double count, const float* gamma,
+                                const float* invstd, float* dgamma, float* dbeta, float* ca, float* cb, float* cc,
+                                void* stream) {
+  bn_bwd_finalize_kernel<<<C, 256, 0, (hipStream_t)stream>>>(pdb, pdg, P, C, count, gamma, invstd, dgamma, dbeta, ca,
+                                                             cb, cc);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
+                             const float* shift, const float* mean, const float* invstd, int act, const float* ca,
+                             const float* cb, const float* cc, void* dz, long dzps, long M, int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int VW = dtype ? 8 : 4;
+  const bool vec = vec_ok(VW, C, zps, dps, dzps, z, dy, dz);
+  const long work = M * (vec ? C / VW : C);
+  const int grid = grid_cap(ceil_div(work, 256), 8192);
+  if (dtype) {
+    if (vec) bn_bwd_apply_kernel<bf16, true><<<grid, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+    else bn_bwd_apply_kernel<bf16, false><<<grid, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+  } else {
+    if (vec) bn_bwd_apply_kernel<float, true><<<grid, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
+    else bn_bwd_apply_kernel<float, false><<<grid, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
+  }
+  return (int)hipGetLastError();
+}
+
+// out[c] (+)= sum_p part[p][c]   (bias gradients from bn_stats partials)
+__global__ void reduce_rows_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out, int acc) {
+  const int c = blockIdx.x;
+  __shared__ double s[256];
+  double a = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) a += (double)part[(long)p * C + c];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) s[threadIdx.x] += s[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[c] = (acc ? out[c] : 0.f) + (float)s[0];
+}
+
+DMY_API int dmy_reduce_rows(const float* part, int P, int C, float* out, int accumulate, void* stream) {
+  reduce_rows_kernel<<<C, 256, 0, (hipStream_t)stream>>>(part, P, C, out, accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,98 @@
+// Common device helpers for the DMA-YOLO gfx950 kernels.
+//
+// Storage convention (see DESIGN.md "Data layout"): every activation is NHWC with a
+// per-pixel stride `ps` (elements between consecutive pixels), so a channel slice of a
+// concat buffer is addressed by (base + c0, ps = Ctot).  Storage type T is float (parity
+// mode) or bf16 (throughput mode); all arithmetic and reductions are fp32 (f64 for BN
+// finalisation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+typedef __hip_bfloat16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+#define DEV __device__ __forceinline__
+
+template <typename T> struct Traits;
+template <> struct Traits<float> {
+  static constexpr int VW = 4;  // elements per 16-byte vector
+};
+template <> struct Traits<bf16> {
+  static constexpr int VW = 8;
+};
+
+DEV float to_f(float x) { return x; }
+DEV float to_f(bf16 x) { return __bfloat162float(x); }
+template <typename T> DEV T from_f(float x);
+template <> DEV float from_f<float>(float x) { return x; }
+template <> DEV bf16 from_f<bf16>(float x) { return __float2bfloat16(x); }
+
+// 16-byte vector <-> VW floats
+template <typename T> DEV void unpack(const uint4& v, float* f) {
+  const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+  for (int i = 0; i < Traits<T>::VW; ++i) f[i] = to_f(e[i]);
+}
+template <typename T> DEV uint4 pack(const float* f) {
+  uint4 v;
+  T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+  for (int i = 0; i < Traits<T>::VW; ++i) e[i] = from_f<T>(f[i]);
+  return v;
+}
+
+DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// Activation codes shared with the host (dmayolo/_lib.py ACT_*).
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_HARDSWISH = 2, ACT_SIGMOID = 3, ACT_GELU = 4 };
+
+DEV float act_fwd(int act, float u) {
+  switch (act) {
+    case ACT_SILU: return u / (1.0f + expf(-u));
+    case ACT_HARDSWISH: return u * fminf(fmaxf(u + 3.0f, 0.0f), 6.0f) / 6.0f;
+    case ACT_SIGMOID: return 1.0f / (1.0f + expf(-u));
+    case ACT_GELU: return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f));
+    default: return u;
+  }
+}
+// d act / d u at pre-activation u
+DEV float act_grad(int act, float u) {
+  switch (act) {
+    case ACT_SILU: {
+      float s = 1.0f / (1.0f + expf(-u));
+      return s * (1.0f + u * (1.0f - s));
+    }
+    case ACT_HARDSWISH:  // torch hardswish_backward: u<-3 -> 0, u<=3 -> u/3+0.5, else 1
+      return u < -3.0f ? 0.0f : (u <= 3.0f ? u / 3.0f + 0.5f : 1.0f);
+    case ACT_SIGMOID: {
+      float s = 1.0f / (1.0f + expf(-u));
+      return s * (1.0f - s);
+    }
+    case ACT_GELU: {
+      const float kA = 0.70710678118654752f, kB = 0.3989422804014327f;  // 1/sqrt2, 1/sqrt(2pi)
+      return 0.5f * (1.0f + erff(u * kA)) + u * kB * expf(-0.5f * u * u);
+    }
+    default: return 1.0f;
+  }
+}
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define HIP_LAUNCH_CHECK() return (int)hipGetLastError()
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+static inline int grid_cap(long blocks, int cap = 4096) { return (int)(blocks < cap ? (blocks < 1 ? 1 : blocks) : cap); }
+
+#define DMY_API extern "C" __attribute__((visibility("default")))

@@ -1,0 +1,107 @@
+"""ctypes binding of the gfx950 C-ABI library (include/dmayolo.h).
+
+The product path has NO fallback: if libdmayolo_hip.so is missing or a symbol is absent the
+import fails loudly.  All tensors are passed as raw device pointers + sizes + strides and every
+launch is stream-ordered on torch's current HIP stream.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libdmayolo_hip.so')
+
+P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_double
+
+# name -> argtypes (return type is int hipError_t unless listed in _RET)
+SIGNATURES = {
+    # conv.hip
+    'dmy_conv_fwd_partial_rows': [L, I],
+    'dmy_conv_fwd': [I, P, P, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
+    'dmy_conv_dgrad': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
+    'dmy_conv_wgrad': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
+    'dmy_conv_wprep': [I, P, P, P, I, I, I, I, P],
+    'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, P],
+    # bn.hip
+    'dmy_bn_partial_rows': [L],
+    'dmy_bn_stats': [I, P, L, L, I, P, P, P],
+    'dmy_bn_finalize': [P, P, I, I, D, P, P, P, P, P, F, F, I, P, P, P, P, P],
+    'dmy_bn_eval_coef': [P, P, P, P, F, I, P, P, P],
+    'dmy_bn_act_fwd': [I, P, L, P, P, I, P, L, P, L, L, I, P],
+    'dmy_bn_bwd_reduce': [I, P, L, P, L, P, P, P, P, I, L, I, P, P, P],
+    'dmy_bn_bwd_finalize': [P, P, I, I, D, P, P, P, P, P, P, P, P],
+    'dmy_bn_bwd_apply': [I, P, L, P, L, P, P, P, P, I, P, P, P, P, L, L, I, P],
+    'dmy_reduce_rows': [P, I, I, P, I, P],
+    # eltwise.hip
+    'dmy_maxpool_fwd': [I, P, L, P, L, P, I, I, I, I, I, P],
+    'dmy_maxpool_bwd': [I, P, L, P, P, L, I, I, I, I, I, I, P],
+    'dmy_avgpool_fwd': [I, P, L, P, I, I, I, I, I, P],
+    'dmy_avgpool_bwd': [I, P, P, L, I, I, I, I, I, I, P],
+    'dmy_resize_fwd': [I, P, L, P, L, F, I, I, I, I, I, I, P],
+    'dmy_resize_bwd': [I, P, L, P, L, I, I, I, I, I, I, P],
+    'dmy_slice_copy': [I, P, L, P, L, L, I, P, I, I, F, I, P],
+    'dmy_dot_partial_blocks': [L, I],
+    'dmy_dot_partial': [I, P, L, P, L, L, I, P, P],
+    'dmy_bifpn_wgrad': [P, I, I, P, F, P, P],
+    'dmy_scgate_fwd': [I, P, L, P, P, P, I, I, I, I, I, I, P],
+    'dmy_scgate_bwd': [I, P, L, P, P, P, P, P, I, I, I, I, I, I, P],
+    'dmy_ca_pool_fwd': [I, P, L, P, I, I, I, I, P],
+    'dmy_ca_pool_bwd': [I, P, P, L, I, I, I, I, I, P],
+    'dmy_ca_apply_fwd': [I, P, L, P, P, P, L, I, I, I, I, P],
+    'dmy_ca_apply_bwd': [I, P, L, P, P, P, L, P, L, P, P, I, I, I, I, P],
+    'dmy_nchw_to_nhwc': [I, I, P, P, I, I, I, I, F, P],
+    'dmy_nhwc_to_nchw_f32': [I, P, L, P, I, I, I, I, P],
+    'dmy_pointwise': [I, I, I, P, P, P, L, F, P],
+    'dmy_cast': [I, I, P, P, L, F, P],
+    # detect_loss.hip
+    'dmy_detect_decode': [I, P, L, L, L, I, I, I, I, I, F, P, P, L, L, P],
+    'dmy_build_targets': [P, I, P, I, I, I, F, P, P, P, P, P, P, P, P, P],
+    'dmy_yolo_loss_level': [I, P, L, L, L, L, I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P,
+                            I, P, P, P, P],
+    'dmy_yolo_loss_finalize': [P, I, F, F, F, F, P, P, P],
+    'dmy_loss_grad': [I, P, P, P, L, P],
+    # nms.hip
+    'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
+    'dmy_nms_sort': [P, L, P, I, P],
+    'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P],
+}
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise LibraryMissing(f'{LIB_PATH} not built: run `python -c "import __graft_entry__ as g; g.build()"` '
+                             '(the DMA-YOLO HIP path has no CPU fallback)')
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = stale build: fail loudly
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+    return lib
+
+
+lib = _load()
+
+
+def call(name, *args):
+    rc = getattr(lib, name)(*args)
+    if name.endswith(('partial_rows', 'partial_blocks')):
+        return rc
+    if rc != 0:
+        raise RuntimeError(f'{name} failed with hipError {rc}')
+    return rc
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU = 0, 1, 2, 3, 4

@@ -1,0 +1,450 @@
+"""Autograd Functions over the gfx950 C-ABI (dmayolo._lib).  Activations are NHWC
+(torch channels_last, logical NCHW shape) in the storage dtype (float32 parity / bfloat16
+throughput); master weights, BN statistics and reductions are fp32.
+
+Every forward/backward here launches hand-written HIP kernels; no ATen compute op sits on the
+hot path (torch is used for allocation and the current stream only).
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream, ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU  # noqa: F401
+
+DT = {torch.float32: 0, torch.bfloat16: 1}
+CL = torch.channels_last
+
+
+def dcode(t):
+    try:
+        return DT[t.dtype]
+    except KeyError:
+        raise TypeError(f'dmayolo kernels take float32 or bfloat16 activations, got {t.dtype}')
+
+
+def pixel_stride(t):
+    """Return (t', ps) with t' NHWC-addressable: addr(b,c,h,w) = b*H*W*ps + (h*W+w)*ps + c."""
+    N, C, H, W = t.shape
+    for attempt in range(2):
+        s = t.stride()
+        if C == 1 or s[1] == 1:
+            ps = s[3] if W > 1 else (s[2] if H > 1 else (s[0] if N > 1 else C))
+            if (W == 1 or s[3] == ps) and (H == 1 or s[2] == W * ps) and (N == 1 or s[0] == H * W * ps) and ps >= C:
+                return t, ps
+        t = t.contiguous(memory_format=CL)
+    raise AssertionError('layout')
+
+
+def new_act(N, C, H, W, like):
+    return torch.empty((N, C, H, W), dtype=like.dtype, device=like.device, memory_format=CL)
+
+
+def f32(n, dev):
+    return torch.empty(n, dtype=torch.float32, device=dev)
+
+
+# ------------------------------------------------------------------ convolution (+BN +act)
+
+class ConvSpec:
+    """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None)."""
+    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache')
+
+    def __init__(self, stride, pad, act, bn=None):
+        self.stride, self.pad, self.act, self.bn = int(stride), int(pad), int(act), bn
+        self.wcache = None
+
+
+def prep_weight(w, dtype, need_t):
+    K, C, KH, KW = w.shape
+    wc = w.detach().contiguous()
+    wf = torch.empty((K, KH * KW * C), dtype=dtype, device=w.device)
+    wt = torch.empty((C, KH * KW * K), dtype=dtype, device=w.device) if need_t else None
+    call('dmy_conv_wprep', DT[dtype], ptr(wc), ptr(wf), ptr(wt), K, C, KH, KW, stream())
+    return wf, wt
+
+
+def conv_out_hw(H, W, k, s, p):
+    return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+
+
+def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
+    N, C, H, W = x.shape
+    call('dmy_conv_fwd', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k,
+         s, p, OH, OW, yps, stream())
+
+
+class ConvBNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, res, spec):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        K, C2, k, _ = weight.shape
+        assert C2 == C, (C2, C)
+        s, p = spec.stride, spec.pad
+        OH, OW = conv_out_hw(H, W, k, s, p)
+        dev, dt = x.device, x.dtype
+        need_grad = any(ctx.needs_input_grad[:6])
+        if not need_grad and not torch.is_grad_enabled() and spec.wcache is not None and \
+                spec.wcache[0] == (weight.data_ptr(), weight._version, dt):
+            wf, wt = spec.wcache[1], None
+        else:
+            wf, wt = prep_weight(weight, dt, need_grad)
+            if not need_grad:
+                spec.wcache = ((weight.data_ptr(), weight._version, dt), wf)
+        M = N * OH * OW
+        z = new_act(N, K, OH, OW, x)
+        bn = spec.bn
+        train_bn = bn is not None and (bn.training or not bn.track_running_stats)
+        if res is not None:
+            res, rps = pixel_stride(res)
+        else:
+            rps = 0
+        if bn is not None:
+            scale, shift, mean, invstd = f32(K, dev), f32(K, dev), f32(K, dev), f32(K, dev)
+            if train_bn:
+                P = call('dmy_conv_fwd_partial_rows', M, K)
+                psum, psq = f32(P * K, dev), f32(P * K, dev)
+                _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, k, s, p, OH, OW)
+                upd = int(bn.training and bn.track_running_stats)
+                mom = bn.momentum if bn.momentum is not None else 0.0
+                call('dmy_bn_finalize', ptr(psum), ptr(psq), P, K, float(M), ptr(bn.weight), ptr(bn.bias),
+                     ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+                     ptr(bn.num_batches_tracked) if upd else None, float(mom), float(bn.eps), upd,
+                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
+            else:
+                _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, k, s, p, OH, OW)
+                call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
+                     float(bn.eps), K, ptr(scale), ptr(shift), stream())
+            y = new_act(N, K, OH, OW, x)
+            call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y), K,
+                 M, K, stream())
+            ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
+        else:
+            _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, k, s, p, OH, OW)
+            if spec.act != ACT_NONE or res is not None:
+                y = new_act(N, K, OH, OW, x)
+                one, zero = torch.ones(K, device=dev), torch.zeros(K, device=dev)
+                call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(one), ptr(zero), spec.act, ptr(res), rps, ptr(y), K,
+                     M, K, stream())
+            else:
+                y = z
+            ctx.save_for_backward(x, wt, z)
+        ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
+        ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        spec = ctx.spec
+        N, C, H, W, xps, K, k, s, p, OH, OW = ctx.geom
+        dy, dps = pixel_stride(dy.to(ctx.saved_tensors[2].dtype))
+        dev = dy.device
+        M = N * OH * OW
+        dt = dcode(dy)
+        dbias = dgamma = dbeta = None
+        if spec.bn is not None:
+            x, wt, z, scale, shift, mean, invstd, gamma = ctx.saved_tensors
+            dz = new_act(N, K, OH, OW, z)
+            ca, cb, cc = f32(K, dev), f32(K, dev), f32(K, dev)
+            if ctx.train_bn:
+                P = call('dmy_bn_partial_rows', M)
+                pdb, pdg = f32(P * K, dev), f32(P * K, dev)
+                call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
+                     spec.act, M, K, ptr(pdb), ptr(pdg), stream())
+                dgamma, dbeta = f32(K, dev), f32(K, dev)
+                call('dmy_bn_bwd_finalize', ptr(pdb), ptr(pdg), P, K, float(M), ptr(gamma), ptr(invstd), ptr(dgamma),
+                     ptr(dbeta), ptr(ca), ptr(cb), ptr(cc), stream())
+            else:
+                ca.copy_(scale)
+                cb.zero_()
+                cc.zero_()
+            call('dmy_bn_bwd_apply', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
+                 spec.act, ptr(ca), ptr(cb), ptr(cc), ptr(dz), K, M, K, stream())
+            dzps = K
+        else:
+            x, wt, z = ctx.saved_tensors
+            if spec.act != ACT_NONE:
+                dz = new_act(N, K, OH, OW, z)
+                zero = torch.zeros(K, device=dev)
+                one = torch.ones(K, device=dev)
+                call('dmy_bn_bwd_apply', dt, ptr(z), K, ptr(dy), dps, ptr(one), ptr(zero), ptr(zero), ptr(one),
+                     spec.act, ptr(one), ptr(zero), ptr(zero), ptr(dz), K, M, K, stream())
+                dzps = K
+            else:
+                dz, dzps = dy, dps
+            if ctx.has_bias:
+                P = call('dmy_bn_partial_rows', M)
+                ps_, pq_ = f32(P * K, dev), f32(P * K, dev)
+                call('dmy_bn_stats', dt, ptr(dz), dzps, M, K, ptr(ps_), ptr(pq_), stream())
+                dbias = f32(K, dev)
+                call('dmy_reduce_rows', ptr(ps_), P, K, ptr(dbias), 0, stream())
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = new_act(N, C, H, W, z)
+            call('dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(dx), 0, N, H, W, C, C, K, k, k, s, p, OH, OW, dzps,
+                 stream())
+        if ctx.needs_input_grad[1]:
+            dwo = f32(K * C * k * k, dev)
+            call('dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N, H, W, C, xps, K, k, k, s, p, OH, OW, dzps,
+                 stream())
+            dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
+            call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, k, k, stream())
+        dres = dy if ctx.has_res else None
+        return dx, dw, dbias, dgamma, dbeta, dres, None
+
+
+def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None):
+    spec = spec or ConvSpec(stride, pad, act, bn)
+    gamma = bn.weight if bn is not None else None
+    beta = bn.bias if bn is not None else None
+    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec)
+
+
+# ------------------------------------------------------------------ pooling / resize / concat
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, C, H, W, x)
+        arg = torch.empty((N, H, W, C), dtype=torch.uint8, device=x.device)
+        call('dmy_maxpool_fwd', dcode(x), ptr(x), xps, ptr(y), C, ptr(arg), N, H, W, C, k, stream())
+        ctx.save_for_backward(arg)
+        ctx.k, ctx.shape = k, (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy, dps = pixel_stride(dy)
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_maxpool_bwd', dcode(dy), ptr(dy), dps, ptr(arg), ptr(dx), C, 0, N, H, W, C, ctx.k, stream())
+        return dx, None
+
+
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, C, H // r, W // r, x)
+        call('dmy_avgpool_fwd', dcode(x), ptr(x), xps, ptr(y), N, H, W, C, r, stream())
+        ctx.r, ctx.shape = r, (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous(memory_format=CL)
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_avgpool_bwd', dcode(dy), ptr(dy), ptr(dx), C, 0, N, H, W, C, ctx.r, stream())
+        return dx, None
+
+
+class ResizeFn(torch.autograd.Function):
+    """nearest resize with ATen's index rule (F.interpolate(mode='nearest'), nn.Upsample)."""
+
+    @staticmethod
+    def forward(ctx, x, OH, OW):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, C, OH, OW, x)
+        call('dmy_resize_fwd', dcode(x), ptr(x), xps, ptr(y), C, 1.0, N, H, W, OH, OW, C, stream())
+        ctx.shape = (N, C, H, W, OH, OW)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W, OH, OW = ctx.shape
+        dy, dps = pixel_stride(dy)
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_resize_bwd', dcode(dy), ptr(dy), dps, ptr(dx), C, N, H, W, OH, OW, C, stream())
+        return dx, None, None
+
+
+class ConcatFn(torch.autograd.Function):
+    """cat(w_i/(sum w + eps) * x_i) along channels (w=None: plain Concat)."""
+
+    @staticmethod
+    def forward(ctx, w, eps, *xs):
+        xs = [pixel_stride(x) for x in xs]
+        N, _, H, W = xs[0][0].shape
+        Ct = sum(x.shape[1] for x, _ in xs)
+        y = new_act(N, Ct, H, W, xs[0][0])
+        c0 = 0
+        M = N * H * W
+        for i, (x, xps) in enumerate(xs):
+            C = x.shape[1]
+            call('dmy_slice_copy', dcode(x), ptr(x), xps, ctypes_off(y, c0), Ct, M, C, ptr(w), i,
+                 len(xs) if w is not None else 0, float(eps), 0, stream())
+            c0 += C
+        ctx.chans = [x.shape[1] for x, _ in xs]
+        ctx.eps = eps
+        if w is not None:
+            ctx.save_for_backward(w, *[x for x, _ in xs])
+        else:
+            ctx.save_for_backward()
+        ctx.has_w = w is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy, dps = pixel_stride(dy)
+        N, Ct, H, W = dy.shape
+        M = N * H * W
+        grads, c0 = [], 0
+        if not ctx.has_w:
+            for C in ctx.chans:
+                grads.append(dy[:, c0:c0 + C])
+                c0 += C
+            return (None, None, *grads)
+        w, *xs = ctx.saved_tensors
+        nb = call('dmy_dot_partial_blocks', M, max(ctx.chans))
+        part = torch.zeros((len(xs), nb), dtype=torch.float32, device=dy.device)
+        for i, (x, C) in enumerate(zip(xs, ctx.chans)):
+            x, xps = pixel_stride(x)
+            g = new_act(N, C, H, W, dy)
+            sl = dy[:, c0:c0 + C]
+            call('dmy_slice_copy', dcode(dy), ptr(sl), dps, ptr(g), C, M, C, ptr(w), i, len(xs), float(ctx.eps), 0,
+                 stream())
+            nbi = call('dmy_dot_partial_blocks', M, C)
+            call('dmy_dot_partial', dcode(dy), ptr(sl), dps, ptr(x), xps, M, C, ptr(part[i]), stream())
+            if nbi < nb:
+                part[i, nbi:].zero_()
+            grads.append(g)
+            c0 += C
+        dw = torch.empty_like(w)
+        call('dmy_bifpn_wgrad', ptr(part), nb, len(xs), ptr(w), float(ctx.eps), ptr(dw), stream())
+        return (dw, None, *grads)
+
+
+def ctypes_off(t, c0):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr() + c0 * t.element_size())
+
+
+# ------------------------------------------------------------------ SCConv gate / CoorAttention
+
+class SCGateFn(torch.autograd.Function):
+    """out = u3 * sigmoid(x + nearest(g))  (models/common.py:1311-1314)."""
+
+    @staticmethod
+    def forward(ctx, x, u3, g):
+        x, xps = pixel_stride(x)
+        u3 = u3.contiguous(memory_format=CL)
+        g = g.contiguous(memory_format=CL)
+        N, C, H, W = x.shape
+        GH, GW = g.shape[2:]
+        out = new_act(N, C, H, W, x)
+        call('dmy_scgate_fwd', dcode(x), ptr(x), xps, ptr(u3), ptr(g), ptr(out), N, H, W, C, GH, GW, stream())
+        ctx.save_for_backward(x, u3, g)
+        ctx.xps = xps
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, u3, g = ctx.saved_tensors
+        N, C, H, W = x.shape
+        GH, GW = g.shape[2:]
+        dout = dout.contiguous(memory_format=CL)
+        du3 = new_act(N, C, H, W, x)
+        dpre = new_act(N, C, H, W, x)
+        call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), N, H, W, C,
+             GH, GW, stream())
+        dg = new_act(N, C, GH, GW, x)
+        call('dmy_resize_bwd', dcode(x), ptr(dpre), C, ptr(dg), C, N, GH, GW, H, W, C, stream())
+        return dpre, du3, dg
+
+
+class CAPoolFn(torch.autograd.Function):
+    """[N,C,H,W] -> [N,C,H+W,1]: row means then column means (CoorAttention pool_h / pool_w + cat)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, C, H + W, 1, x)
+        call('dmy_ca_pool_fwd', dcode(x), ptr(x), xps, ptr(y), N, H, W, C, stream())
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous(memory_format=CL)
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_ca_pool_bwd', dcode(dy), ptr(dy), ptr(dx), C, 0, N, H, W, C, stream())
+        return dx
+
+
+class CAApplyFn(torch.autograd.Function):
+    """out = x * sigmoid(lw)[w] * sigmoid(lh)[h]; lh/lw are conv_h/conv_w logits over all H+W rows."""
+
+    @staticmethod
+    def forward(ctx, x, lh, lw):
+        x, xps = pixel_stride(x)
+        lh = lh.contiguous(memory_format=CL)
+        lw = lw.contiguous(memory_format=CL)
+        N, C, H, W = x.shape
+        out = new_act(N, C, H, W, x)
+        call('dmy_ca_apply_fwd', dcode(x), ptr(x), xps, ptr(lh), ptr(lw), ptr(out), C, N, H, W, C, stream())
+        ctx.save_for_backward(x, lh, lw)
+        ctx.xps = xps
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, lh, lw = ctx.saved_tensors
+        N, C, H, W = x.shape
+        dout, dps = pixel_stride(dout)
+        dx = new_act(N, C, H, W, x)
+        dlh = torch.empty_like(lh)
+        dlw = torch.empty_like(lw)
+        call('dmy_ca_apply_bwd', dcode(x), ptr(x), ctx.xps, ptr(lh), ptr(lw), ptr(dout), dps, ptr(dx), C, ptr(dlh),
+             ptr(dlw), N, H, W, C, stream())
+        return dx, dlh, dlw
+
+
+# ------------------------------------------------------------------ misc pointwise
+
+class AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a = a.contiguous(memory_format=CL) if a.dim() == 4 else a.contiguous()
+        b = b.contiguous(memory_format=CL) if b.dim() == 4 else b.contiguous()
+        y = torch.empty_like(a)
+        call('dmy_pointwise', dcode(a), 0, 0, ptr(a), ptr(b), ptr(y), a.numel(), 1.0, stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+class ToNHWC(torch.autograd.Function):
+    """NCHW float/uint8 image -> NHWC storage dtype (train.py:402 `/255` when uint8)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        N, C, H, W = x.shape
+        y = torch.empty((N, C, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        xc = x.contiguous()
+        if x.dtype == torch.uint8:
+            call('dmy_nchw_to_nhwc', DT[dtype], 0, ptr(xc), ptr(y), N, C, H, W, 1.0 / 255.0, stream())
+        else:
+            xf = xc if x.dtype == torch.float32 else xc.float()
+            call('dmy_nchw_to_nhwc', DT[dtype], 1, ptr(xf), ptr(y), N, C, H, W, 1.0, stream())
+        ctx.src_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.src_dtype == torch.uint8:
+            return None, None
+        dy, dps = pixel_stride(dy)
+        N, C, H, W = dy.shape
+        dx = torch.empty((N, C, H, W), dtype=torch.float32, device=dy.device)
+        call('dmy_nhwc_to_nchw_f32', dcode(dy), ptr(dy), dps, ptr(dx), N, C, H, W, stream())
+        return dx.to(ctx.src_dtype), None

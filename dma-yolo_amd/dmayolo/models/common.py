@@ -1,0 +1,278 @@
+"""Drop-in replacements for the reference's YAML modules (models/common.py, models/cspcm.py).
+
+Same class names, constructor signatures, parameter/buffer names (state_dict keys) and the
+attributes other reference code reads (`Conv.conv/.bn/.forward_fuse`, `AdConcat*.w`, real
+nn.BatchNorm2d / nn.Conv2d instances for optimizer grouping and initialize_weights).
+forward() runs the gfx950 kernels through dmayolo.functional; there is no CPU path.
+
+Activation tensors are NHWC (torch.channels_last) in the model's storage dtype.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import functional as Fn
+from ..functional import ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU
+
+__all__ = ['autopad', 'Conv', 'Bottleneck', 'C3', 'SPPF', 'SPPFCSPC', 'SCConv', 'CoorAttention', 'CA',
+           'CABottleneck', 'C3CA', 'Concat', 'AdConcat2', 'AdConcat3', 'Upsample', 'C3STR', 'SwinTransformerBlock',
+           'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath']
+
+
+def autopad(k, p=None):
+    """models/common.py:33-48."""
+    if p is None:
+        p = k // 2 if isinstance(k, int) else [x // 2 for x in k]
+    return p
+
+
+def act_code(m):
+    if m is None or isinstance(m, nn.Identity):
+        return ACT_NONE
+    if isinstance(m, nn.SiLU):
+        return ACT_SILU
+    if isinstance(m, nn.Hardswish):
+        return ACT_HARDSWISH
+    if isinstance(m, nn.Sigmoid):
+        return ACT_SIGMOID
+    if isinstance(m, nn.GELU):
+        return ACT_GELU
+    raise NotImplementedError(f'activation {type(m).__name__} has no gfx950 kernel')
+
+
+def _pad_int(p):
+    return p if isinstance(p, int) else p[0]
+
+
+def conv_forward(conv, bn, act, x, res=None):
+    """conv (nn.Conv2d, groups=1, dilation=1) -> optional BN -> act (+ residual) on the HIP path."""
+    assert conv.groups == 1 and conv.dilation in (1, (1, 1)), 'grouped/dilated conv not on the DMA-YOLO path'
+    s = conv.stride if isinstance(conv.stride, int) else conv.stride[0]
+    return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, _pad_int(conv.padding), act_code(act), res=res)
+
+
+class Conv(nn.Module):
+    """conv + BN + SiLU: models/cspcm.py:11-23 (YAML-level Conv) == models/common.py:50-77."""
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, act=True):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, c2, k, s, autopad(k, p), groups=g, bias=False)
+        self.bn = nn.BatchNorm2d(c2)
+        self.act = nn.SiLU() if act is True else (act if isinstance(act, nn.Module) else nn.Identity())
+
+    def forward(self, x, res=None):
+        return conv_forward(self.conv, self.bn, self.act, x, res)
+
+    def forward_fuse(self, x, res=None):
+        return conv_forward(self.conv, None, self.act, x, res)
+
+
+class Bottleneck(nn.Module):
+    """models/common.py:119-137; the residual add is fused into cv2's BN/act epilogue."""
+
+    def __init__(self, c1, c2, shortcut=True, g=1, e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_, c2, 3, 1, g=g)
+        self.add = shortcut and c1 == c2
+
+    def forward(self, x):
+        return self.cv2(self.cv1(x), res=x if self.add else None)
+
+
+class C3(nn.Module):
+    """models/common.py:159-182."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c1, c_, 1, 1)
+        self.cv3 = Conv(2 * c_, c2, 1)
+        self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, e=1.0) for _ in range(n)))
+
+    def forward(self, x):
+        return self.cv3(Fn.ConcatFn.apply(None, 0.0, self.m(self.cv1(x)), self.cv2(x)))
+
+
+class SPPF(nn.Module):
+    """models/common.py:243-258."""
+
+    def __init__(self, c1, c2, k=5):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_ * 4, c2, 1, 1)
+        self.m = nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2)
+
+    def forward(self, x):
+        k = self.m.kernel_size
+        x = self.cv1(x)
+        y1 = Fn.MaxPoolFn.apply(x, k)
+        y2 = Fn.MaxPoolFn.apply(y1, k)
+        return self.cv2(Fn.ConcatFn.apply(None, 0.0, x, y1, y2, Fn.MaxPoolFn.apply(y2, k)))
+
+
+class SPPFCSPC(nn.Module):
+    """models/common.py:1257-1276."""
+
+    def __init__(self, c1, c2, n=1, shortcut=False, g=1, e=0.5, k=5):
+        super().__init__()
+        c_ = int(2 * c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c1, c_, 1, 1)
+        self.cv3 = Conv(c_, c_, 3, 1)
+        self.cv4 = Conv(c_, c_, 1, 1)
+        self.m = nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2)
+        self.cv5 = Conv(4 * c_, c_, 1, 1)
+        self.cv6 = Conv(c_, c_, 3, 1)
+        self.cv7 = Conv(2 * c_, c2, 1, 1)
+
+    def forward(self, x):
+        k = self.m.kernel_size
+        x1 = self.cv4(self.cv3(self.cv1(x)))
+        x2 = Fn.MaxPoolFn.apply(x1, k)
+        x3 = Fn.MaxPoolFn.apply(x2, k)
+        y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, x1, x2, x3, Fn.MaxPoolFn.apply(x3, k))))
+        y2 = self.cv2(x)
+        return self.cv7(Fn.ConcatFn.apply(None, 0.0, y1, y2))
+
+
+class SCConv(nn.Module):
+    """Self-calibrated convolution, models/common.py:1279-1316: k4(k3(x) * sigmoid(x + up(k2(x))))."""
+
+    def __init__(self, c1, c2, stride, groups=1, dilation=1, pooling_r=4):
+        super().__init__()
+        self.k2 = nn.Sequential(nn.AvgPool2d(kernel_size=pooling_r, stride=pooling_r),
+                                nn.Conv2d(c1, c1, 3, 1, autopad(3, None), dilation=dilation, groups=groups,
+                                          bias=False),
+                                nn.BatchNorm2d(c1))
+        self.k3 = nn.Sequential(nn.Conv2d(c1, c1, 3, 1, autopad(3, None), dilation=dilation, groups=groups,
+                                          bias=False),
+                                nn.BatchNorm2d(c1))
+        self.k4 = nn.Sequential(nn.Conv2d(c1, c2, 3, stride, autopad(3, None), dilation=dilation, groups=groups,
+                                          bias=False),
+                                nn.BatchNorm2d(c2))
+
+    def forward(self, x):
+        r = self.k2[0].kernel_size
+        r = r if isinstance(r, int) else r[0]
+        g = conv_forward(self.k2[1], self.k2[2], None, Fn.AvgPoolFn.apply(x, r))
+        u3 = conv_forward(self.k3[0], self.k3[1], None, x)
+        return conv_forward(self.k4[0], self.k4[1], None, Fn.SCGateFn.apply(x, u3, g))
+
+
+class CoorAttention(nn.Module):
+    """Coordinate attention, models/common.py:1158-1207 (YAML token `CA`)."""
+
+    def __init__(self, c1, c2, reduction=32):
+        super().__init__()
+        self.pool_h = nn.AdaptiveAvgPool2d((None, 1))
+        self.pool_w = nn.AdaptiveAvgPool2d((1, None))
+        c_ = max(8, c1 // reduction)
+        self.conv1 = nn.Conv2d(c1, c_, kernel_size=1, stride=1, padding=0)
+        self.bn1 = nn.BatchNorm2d(c_)
+        self.act = nn.Hardswish()
+        self.conv_w = nn.Conv2d(c_, c2, kernel_size=1, stride=1, padding=0)
+        self.conv_h = nn.Conv2d(c_, c2, kernel_size=1, stride=1, padding=0)
+
+    def forward(self, x):
+        y = conv_forward(self.conv1, self.bn1, self.act, Fn.CAPoolFn.apply(x))   # [N, c_, H+W, 1]
+        lh = conv_forward(self.conv_h, None, None, y)                           # logits over all H+W rows
+        lw = conv_forward(self.conv_w, None, None, y)
+        return Fn.CAApplyFn.apply(x, lh, lw)
+
+
+CA = CoorAttention  # the north-star YAML's undefined `CA` token binds to CoorAttention
+
+
+class CABottleneck(nn.Module):
+    """models/common.py:1209-1227."""
+
+    def __init__(self, c1, c2, shortcut=True, g=1, e=0.5, reduction=32):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_, c2, 3, 1, g=g)
+        self.ca = CoorAttention(c2, c2, reduction)
+        self.add = shortcut and c1 == c2
+
+    def forward(self, x):
+        y = self.ca(self.cv2(self.cv1(x)))
+        return Fn.AddFn.apply(x, y) if self.add else y
+
+
+class C3CA(C3):
+    """models/common.py:1229-1235."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = nn.Sequential(*(CABottleneck(c_, c_, shortcut, g, e=1.0) for _ in range(n)))
+
+
+class Concat(nn.Module):
+    """models/common.py:656-664 (channel concat only: the YAML always passes dimension 1)."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def forward(self, x):
+        assert self.d == 1
+        return Fn.ConcatFn.apply(None, 0.0, *x)
+
+
+class AdConcat2(nn.Module):
+    """BiFPN weighted concat, models/common.py:994-1008."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+        self.w = nn.Parameter(torch.ones(2, dtype=torch.float32), requires_grad=True)
+        self.epsilon = 0.0001
+
+    def forward(self, x):
+        assert self.d == 1 and len(x) == 2
+        return Fn.ConcatFn.apply(self.w, self.epsilon, *x)
+
+
+class AdConcat3(AdConcat2):
+    """models/common.py:1010-1026."""
+
+    def __init__(self, dimension=1):
+        super().__init__(dimension)
+        self.w = nn.Parameter(torch.ones(3, dtype=torch.float32), requires_grad=True)
+
+    def forward(self, x):
+        assert self.d == 1 and len(x) == 3
+        return Fn.ConcatFn.apply(self.w, self.epsilon, *x)
+
+
+class Upsample(nn.Upsample):
+    """nn.Upsample(None, 2, 'nearest') as used by the YAML heads; nearest only."""
+
+    def forward(self, x):
+        assert self.mode == 'nearest'
+        H, W = x.shape[2:]
+        if self.size is not None:
+            OH, OW = (self.size, self.size) if isinstance(self.size, int) else self.size
+        else:
+            sf = self.scale_factor if isinstance(self.scale_factor, (tuple, list)) else (self.scale_factor,) * 2
+            OH, OW = int(math.floor(H * sf[0])), int(math.floor(W * sf[1]))
+        return Fn.ResizeFn.apply(x, OH, OW)
+
+
+# ------------------------------------------------------------------ Swin (C3STR) — layers in swin.py
+from .swin import SwinTransformerBlock, SwinTransformerLayer, WindowAttention, Mlp, DropPath  # noqa: E402
+
+
+class C3STR(C3):
+    """models/common.py:191-196: C3 whose bottleneck stack is a 3-layer Swin block (heads = c_ // 32)."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = SwinTransformerBlock(c_, c_, c_ // 32, n)

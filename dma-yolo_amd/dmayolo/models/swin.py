@@ -1,0 +1,85 @@
+"""Swin (C3STR) modules — models/common.py:97-117, 191-196, 386-654.  Kernels: csrc/swin.hip."""
+import torch
+import torch.nn as nn
+
+from .. import functional as Fn
+
+
+class DropPath(nn.Module):
+    """models/common.py:386-413 (stochastic depth, per-sample)."""
+
+    def __init__(self, drop_prob=None):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        raise NotImplementedError
+
+
+class Mlp(nn.Module):
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.drop1 = nn.Dropout(drop)
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop2 = nn.Dropout(drop)
+
+
+class WindowAttention(nn.Module):
+    def __init__(self, dim, window_size, num_heads, qkv_bias=True, attn_drop=0., proj_drop=0.):
+        super().__init__()
+        self.dim, self.window_size, self.num_heads = dim, window_size, num_heads
+        self.scale = (dim // num_heads) ** -0.5
+        ws = window_size[0]
+        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * ws - 1) * (2 * window_size[1] - 1),
+                                                                     num_heads))
+        r = torch.arange(ws).repeat_interleave(window_size[1])
+        c = torch.arange(window_size[1]).repeat(ws)
+        idx = (r[:, None] - r[None, :] + ws - 1) * (2 * window_size[1] - 1) + (c[:, None] - c[None, :] +
+                                                                               window_size[1] - 1)
+        self.register_buffer('relative_position_index', idx)
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
+
+
+class SwinTransformerLayer(nn.Module):
+    def __init__(self, c, num_heads, window_size=7, shift_size=0, mlp_ratio=4, qkv_bias=False, drop=0.,
+                 attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+        super().__init__()
+        if num_heads > 10:
+            drop_path = 0.1
+        self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
+        self.norm1 = norm_layer(c)
+        self.attn = WindowAttention(c, window_size=(window_size, window_size), num_heads=num_heads,
+                                    qkv_bias=qkv_bias, attn_drop=attn_drop, proj_drop=drop)
+        self.drop_path = DropPath(drop_path) if drop_path > 0. else nn.Identity()
+        self.norm2 = norm_layer(c)
+        self.mlp = Mlp(in_features=c, hidden_features=int(c * mlp_ratio), act_layer=act_layer, drop=drop)
+
+    def forward(self, x):
+        raise NotImplementedError('Swin kernels land in csrc/swin.hip')
+
+
+class SwinTransformerBlock(nn.Module):
+    def __init__(self, c1, c2, num_heads, num_layers, window_size=8):
+        super().__init__()
+        from .common import Conv
+        self.conv = Conv(c1, c2) if c1 != c2 else None
+        self.window_size = window_size
+        self.shift_size = window_size // 2
+        self.tr = nn.Sequential(*(SwinTransformerLayer(c2, num_heads=num_heads, window_size=window_size,
+                                                       shift_size=0 if (i % 2 == 0) else self.shift_size)
+                                  for i in range(num_layers)))
+
+    def forward(self, x):
+        if self.conv is not None:
+            x = self.conv(x)
+        return self.tr(x)
+
+

@@ -1,0 +1,265 @@
+"""Drop-in Model / parse_model / Detect (models/yolo.py:40-478) on the gfx950 kernels.
+
+Differences from the reference that do not change results:
+  * strides come from a shape-only walk of the parsed graph instead of a probe forward
+    (models/yolo.py:159-170); the probe's side effect on BN running stats is not reproduced
+    (parity is anchored on state_dict transfer);
+  * activations are NHWC in `Model.act_dtype` (float32 parity / bfloat16 throughput).
+"""
+import math
+from copy import deepcopy
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+
+from .. import functional as Fn
+from ..functional import call, ptr, stream, dcode
+from .common import *  # noqa: F401,F403  (the YAML namespace)
+from .common import Conv, Upsample, SCConv, autopad
+from ..utils.general import make_divisible
+from ..utils.torch_utils import initialize_weights, fuse_conv_and_bn
+
+
+class Detect(nn.Module):
+    """models/yolo.py:40-114."""
+    stride = None
+    onnx_dynamic = False
+
+    def __init__(self, nc=80, anchors=(), ch=(), inplace=True):
+        super().__init__()
+        self.nc = nc
+        self.no = nc + 5
+        self.nl = len(anchors)
+        self.na = len(anchors[0]) // 2
+        self.grid = [torch.zeros(1)] * self.nl
+        self.anchor_grid = [torch.zeros(1)] * self.nl
+        self.register_buffer('anchors', torch.tensor(anchors).float().view(self.nl, -1, 2))
+        self.m = nn.ModuleList(nn.Conv2d(x, self.no * self.na, 1) for x in ch)
+        self.inplace = inplace
+
+    def forward(self, x):
+        out = []
+        for i in range(self.nl):
+            y = Fn.conv_bn_act(x[i], self.m[i].weight, self.m[i].bias, None, 1, 0, Fn.ACT_NONE)
+            bs, _, ny, nx = y.shape
+            # NHWC [bs, ny, nx, na*no] -> [bs, na, ny, nx, no] view (no copy)
+            out.append(y.permute(0, 2, 3, 1).view(bs, ny, nx, self.na, self.no).permute(0, 3, 1, 2, 4))
+        if self.training:
+            return out
+        return self.decode(out), out
+
+    @torch.no_grad()
+    def decode(self, out):
+        bs = out[0].shape[0]
+        total = sum(self.na * p.shape[2] * p.shape[3] for p in out)
+        z = torch.empty((bs, total, self.no), dtype=torch.float32, device=out[0].device)
+        off = 0
+        anchors = self.anchors.float().contiguous()
+        for i, p in enumerate(out):
+            _, na, ny, nx, no = p.shape
+            s = p.stride()
+            call('dmy_detect_decode', dcode(p), ptr(p), s[0], s[2], s[3], bs, ny, nx, na, no, float(self.stride[i]),
+                 ptr(anchors[i]), ptr(z), off, total, stream())
+            off += na * ny * nx
+        return z
+
+    def _make_grid(self, nx=20, ny=20, i=0):
+        d = self.anchors[i].device
+        yv, xv = torch.meshgrid([torch.arange(ny, device=d), torch.arange(nx, device=d)], indexing='ij')
+        grid = torch.stack((xv, yv), 2).expand((1, self.na, ny, nx, 2)).float()
+        anchor_grid = (self.anchors[i].clone() * self.stride[i]).view((1, self.na, 1, 1, 2)).expand(
+            (1, self.na, ny, nx, 2)).float()
+        return grid, anchor_grid
+
+
+def check_anchor_order(m):
+    """utils/autoanchor.py:16-23."""
+    a = m.anchors.prod(-1).view(-1)
+    da = a[-1] - a[0]
+    ds = m.stride[-1] - m.stride[0]
+    if da.sign() != ds.sign():
+        m.anchors[:] = m.anchors.flip(0)
+
+
+def _out_hw(m, hw):
+    """Shape-only walk used for the stride probe (models/yolo.py:159-170)."""
+    if isinstance(m, nn.Sequential) and not isinstance(m[0], nn.AvgPool2d):
+        for mm in m:
+            hw = _out_hw(mm, hw)
+        return hw
+    if isinstance(m, Conv):
+        c = m.conv
+        k, s, p = c.kernel_size[0], c.stride[0], c.padding[0]
+        return ((hw[0] + 2 * p - k) // s + 1, (hw[1] + 2 * p - k) // s + 1)
+    if isinstance(m, SCConv):
+        s = m.k4[0].stride[0]
+        return ((hw[0] - 1) // s + 1, (hw[1] - 1) // s + 1)
+    if isinstance(m, nn.Upsample):
+        sf = m.scale_factor if isinstance(m.scale_factor, (int, float)) else m.scale_factor[0]
+        return (int(hw[0] * sf), int(hw[1] * sf))
+    return hw
+
+
+class Model(nn.Module):
+    """models/yolo.py:117-350."""
+
+    def __init__(self, cfg='yolov5s.yaml', ch=3, nc=None, anchors=None, act_dtype=torch.float32):
+        super().__init__()
+        if isinstance(cfg, dict):
+            self.yaml = deepcopy(cfg)
+        else:
+            import yaml
+            self.yaml_file = Path(cfg).name
+            with open(cfg, errors='ignore') as f:
+                self.yaml = yaml.safe_load(f)
+        ch = self.yaml['ch'] = self.yaml.get('ch', ch)
+        if nc and nc != self.yaml['nc']:
+            self.yaml['nc'] = nc
+        if anchors:
+            self.yaml['anchors'] = round(anchors)
+        self.model, self.save = parse_model(deepcopy(self.yaml), ch=[ch])
+        self.names = [str(i) for i in range(self.yaml['nc'])]
+        self.inplace = self.yaml.get('inplace', True)
+        self.act_dtype = act_dtype
+        m = self.model[-1]
+        if isinstance(m, Detect):
+            s = 256
+            m.inplace = self.inplace
+            hw = self._probe_hw(s)
+            m.stride = torch.tensor([s / h for h, _ in hw], dtype=torch.float32)
+            m.anchors /= m.stride.view(-1, 1, 1)
+            check_anchor_order(m)
+            self.stride = m.stride
+            self._initialize_biases()
+        initialize_weights(self)
+
+    def _probe_hw(self, s):
+        ys, hw = [], (s, s)
+        for m in self.model:
+            if m.f != -1:
+                hw = ys[m.f] if isinstance(m.f, int) else [hw if j == -1 else ys[j] for j in m.f]
+            if isinstance(m, Detect):
+                return hw
+            if isinstance(hw, list):
+                hw = hw[0]
+            hw = _out_hw(m, hw)
+            ys.append(hw)
+        raise AssertionError('no Detect layer')
+
+    def forward(self, x, augment=False, profile=False, visualize=False):
+        if augment:
+            raise NotImplementedError('test-time augmentation is outside the DMA-YOLO hot path')
+        return self._forward_once(x)
+
+    def to_input(self, x):
+        """uint8/float NCHW image batch -> NHWC act_dtype (train.py:402 `/255` for uint8)."""
+        if x.dtype == self.act_dtype and x.dim() == 4 and (x.shape[1] == 1 or x.stride(1) == 1):
+            return x
+        return Fn.ToNHWC.apply(x, self.act_dtype)
+
+    def _forward_once(self, x, profile=False, visualize=False):
+        x = self.to_input(x)
+        y = []
+        for m in self.model:
+            if m.f != -1:
+                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            x = m(x)
+            y.append(x if m.i in self.save else None)
+        return x
+
+    def _initialize_biases(self, cf=None):
+        """models/yolo.py:293-301."""
+        m = self.model[-1]
+        for mi, s in zip(m.m, m.stride):
+            b = mi.bias.view(m.na, -1)
+            b.data[:, 4] += math.log(8 / (640 / s) ** 2)
+            b.data[:, 5:] += math.log(0.6 / (m.nc - 0.999999)) if cf is None else torch.log(cf / cf.sum())
+            mi.bias = torch.nn.Parameter(b.view(-1), requires_grad=True)
+
+    def fuse(self):
+        """models/yolo.py:315-323: BN folded into YAML-level Conv layers only."""
+        for m in self.model:
+            if isinstance(m, Conv) and hasattr(m, 'bn'):
+                m.conv = fuse_conv_and_bn(m.conv, m.bn)
+                delattr(m, 'bn')
+                m.forward = m.forward_fuse
+        return self
+
+    def _apply(self, fn):
+        self = super()._apply(fn)
+        m = self.model[-1]
+        if isinstance(m, Detect):
+            m.stride = fn(m.stride)
+            m.grid = list(map(fn, m.grid))
+            if isinstance(m.anchor_grid, list):
+                m.anchor_grid = list(map(fn, m.anchor_grid))
+        return self
+
+    def info(self, verbose=False, img_size=640):
+        n_p = sum(x.numel() for x in self.parameters())
+        return n_p
+
+
+_CH_MODS = None
+
+
+def _namespace():
+    import types
+    from . import common as C
+    ns = {k: getattr(C, k) for k in C.__all__}
+    ns['Detect'] = Detect
+    ns['nn'] = types.SimpleNamespace(Upsample=Upsample, BatchNorm2d=nn.BatchNorm2d)
+    return ns
+
+
+def parse_model(d, ch):
+    """models/yolo.py:353-478 for the hot-path module set (eval of YAML names in this namespace)."""
+    from . import common as C
+    ns = _namespace()
+    anchors, nc, gd, gw = d['anchors'], d['nc'], d['depth_multiple'], d['width_multiple']
+    na = (len(anchors[0]) // 2) if isinstance(anchors, list) else anchors
+    no = na * (nc + 5)
+    ev = dict(ns, nc=nc, anchors=anchors)
+    chan_mods = (C.Conv, C.Bottleneck, C.SPPF, C.C3, C.C3STR, C.CoorAttention, C.CABottleneck, C.C3CA, C.SPPFCSPC,
+                 C.SCConv)
+    rep_mods = (C.C3, C.C3STR, C.C3CA)
+    layers, save, c2 = [], [], ch[-1]
+    for i, (f, n, m, args) in enumerate(d['backbone'] + d['head']):
+        m = eval(m, ev) if isinstance(m, str) else m
+        for j, a in enumerate(args):
+            try:
+                args[j] = eval(a, ev) if isinstance(a, str) else a
+            except NameError:
+                pass
+        n = n_ = max(round(n * gd), 1) if n > 1 else n
+        if m in chan_mods:
+            c1, c2 = ch[f], args[0]
+            if c2 != no:
+                c2 = make_divisible(c2 * gw, 8)
+            args = [c1, c2, *args[1:]]
+            if m in rep_mods:
+                args.insert(2, n)
+                n = 1
+        elif m is nn.BatchNorm2d:
+            args = [ch[f]]
+        elif m in (C.Concat, C.AdConcat2, C.AdConcat3):
+            c2 = sum(ch[x] for x in f)
+        elif m is Detect:
+            args.append([ch[x] for x in f])
+            if isinstance(args[1], int):
+                args[1] = [list(range(args[1] * 2))] * len(f)
+        elif m is Upsample:
+            c2 = ch[f]
+        else:
+            raise NotImplementedError(f'YAML module {m} is outside the DMA-YOLO hot path')
+        m_ = nn.Sequential(*(m(*args) for _ in range(n))) if n > 1 else m(*args)
+        t = str(m)[8:-2].replace('__main__.', '')
+        np_ = sum(x.numel() for x in m_.parameters())
+        m_.i, m_.f, m_.type, m_.np = i, f, t, np_
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        layers.append(m_)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    return nn.Sequential(*layers), sorted(save)

@@ -1,0 +1,144 @@
+"""Fused multi-tensor optimizers and EMA on gfx950 (csrc/optim.hip).
+
+FusedSGD / FusedAdam are torch.optim.Optimizer subclasses (so LambdaLR, param_groups, warmup
+writes to group['lr'] / group['momentum'] work exactly as in train.py:216-235, 408-422); each
+step() is one kernel launch per parameter group.  Semantics follow torch.optim.SGD(nesterov=True)
+and torch.optim.Adam (L2 weight decay, bias correction) as used by the reference.
+"""
+import ctypes
+
+import torch
+
+from ._lib import lib, stream, call
+
+lib.dmy_chunk_size.restype = ctypes.c_int
+lib.dmy_chunk_size.argtypes = []
+CHUNK = lib.dmy_chunk_size()
+_P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
+lib.dmy_sgd.argtypes = [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]
+lib.dmy_adam.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _P]
+lib.dmy_ema.argtypes = [_P, _P, _P, _P, _P, _I, _F, _P]
+for _f in (lib.dmy_sgd, lib.dmy_adam, lib.dmy_ema):
+    _f.restype = ctypes.c_int
+
+
+class _Table:
+    """Device-side pointer table + (tensor, chunk) map for a list of tensors."""
+
+    def __init__(self, lists, dev):
+        n = [t.numel() for t in lists[0]]
+        tid, off = [], []
+        for i, k in enumerate(n):
+            for o in range(0, k, CHUNK):
+                tid.append(i)
+                off.append(o)
+        self.nchunks = len(tid)
+        host = [torch.tensor([t.data_ptr() for t in L], dtype=torch.int64) for L in lists]
+        host += [torch.tensor(n, dtype=torch.int64), torch.tensor(tid, dtype=torch.int32),
+                 torch.tensor(off, dtype=torch.int64)]
+        self.dev = [h.to(dev, non_blocking=False) for h in host]
+
+    def p(self, i):
+        return ctypes.c_void_p(self.dev[i].data_ptr())
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f'{name} failed with hipError {rc}')
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, nesterov=False):
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for g in self.param_groups:
+            ps = [p for p in g['params'] if p.grad is not None]
+            if not ps:
+                continue
+            for p in ps:
+                assert p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
+            first = 'momentum_buffer' not in self.state[ps[0]]
+            bufs = []
+            for p in ps:
+                st = self.state[p]
+                if 'momentum_buffer' not in st:
+                    st['momentum_buffer'] = torch.empty_like(p)
+                bufs.append(st['momentum_buffer'])
+            tb = _Table([ps, [p.grad for p in ps], bufs], ps[0].device)
+            _check(lib.dmy_sgd(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.nchunks, float(g['lr']),
+                               float(g['momentum']), float(g['weight_decay']), int(g['nesterov']), int(first),
+                               stream()), 'dmy_sgd')
+        return None
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for g in self.param_groups:
+            ps = [p for p in g['params'] if p.grad is not None]
+            if not ps:
+                continue
+            ms, vs = [], []
+            for p in ps:
+                st = self.state[p]
+                if 'step' not in st:
+                    st['step'] = 0
+                    st['exp_avg'] = torch.zeros_like(p)
+                    st['exp_avg_sq'] = torch.zeros_like(p)
+                st['step'] += 1
+                ms.append(st['exp_avg'])
+                vs.append(st['exp_avg_sq'])
+            t = self.state[ps[0]]['step']
+            b1, b2 = g['betas']
+            bc1 = 1 - b1 ** t
+            bc2s = (1 - b2 ** t) ** 0.5
+            tb = _Table([ps, [p.grad for p in ps], ms, vs], ps[0].device)
+            _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
+                                float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
+                                float(bc1), float(bc2s), stream()), 'dmy_adam')
+        return None
+
+
+def ema_update(ema_tensors, model_tensors, d):
+    """e = d*e + (1-d)*m for every float tensor pair (utils/torch_utils.py:335-339)."""
+    es = [e for e in ema_tensors]
+    ms = [m.float() if m.dtype != torch.float32 else m for m in model_tensors]
+    for e in es:
+        assert e.dtype == torch.float32 and e.is_contiguous()
+    tb = _Table([es, [m.contiguous() for m in ms]], es[0].device)
+    _check(lib.dmy_ema(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.nchunks, float(d), stream()), 'dmy_ema')
+
+
+def param_groups(model):
+    """train.py:197-214 grouping: g0 BN weights (no decay), g1 weights + AdConcat.w (decay), g2 biases.
+    (relative_position_bias_table and other non-weight/bias params are NOT collected, as in the reference.)"""
+    import torch.nn as nn
+    from .models.common import AdConcat2, AdConcat3
+    g0, g1, g2 = [], [], []
+    for v in model.modules():
+        if hasattr(v, 'bias') and isinstance(v.bias, nn.Parameter):
+            g2.append(v.bias)
+        if isinstance(v, nn.BatchNorm2d):
+            g0.append(v.weight)
+        elif hasattr(v, 'weight') and isinstance(v.weight, nn.Parameter):
+            g1.append(v.weight)
+        elif isinstance(v, (AdConcat2, AdConcat3)) and isinstance(v.w, nn.Parameter):
+            g1.append(v.w)
+    return g0, g1, g2
+
+
+def build_optimizer(model, kind='sgd', lr0=0.01, momentum=0.937, weight_decay=5e-4):
+    """train.py:216-222 (Adam hard-codes lr=3e-4 for g0)."""
+    g0, g1, g2 = param_groups(model)
+    if kind == 'adam':
+        opt = FusedAdam(g0, lr=3e-4, betas=(momentum, 0.999))
+    else:
+        opt = FusedSGD(g0, lr=lr0, momentum=momentum, nesterov=True)
+    opt.add_param_group({'params': g1, 'weight_decay': weight_decay})
+    opt.add_param_group({'params': g2})
+    return opt

@@ -1,0 +1,89 @@
+"""utils/general.py counterparts on the hot path: make_divisible, box converters, and the
+batched gfx950 non_max_suppression (utils/general.py:633-725)."""
+import math
+
+import torch
+
+from ..functional import call, ptr, stream
+
+
+def make_divisible(x, divisor):
+    """utils/general.py:450-452."""
+    return math.ceil(x / divisor) * divisor
+
+
+def xywh2xyxy(x):
+    """utils/general.py:539-546."""
+    y = x.clone()
+    y[:, 0] = x[:, 0] - x[:, 2] / 2
+    y[:, 1] = x[:, 1] - x[:, 3] / 2
+    y[:, 2] = x[:, 0] + x[:, 2] / 2
+    y[:, 3] = x[:, 1] + x[:, 3] / 2
+    return y
+
+
+def xyxy2xywh(x):
+    """utils/general.py:529-536."""
+    y = x.clone()
+    y[:, 0] = (x[:, 0] + x[:, 2]) / 2
+    y[:, 1] = (x[:, 1] + x[:, 3]) / 2
+    y[:, 2] = x[:, 2] - x[:, 0]
+    y[:, 3] = x[:, 3] - x[:, 1]
+    return y
+
+
+def _pow2(n, lo=2048):
+    c = lo
+    while c < n:
+        c <<= 1
+    return c
+
+
+def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False,
+                        multi_label=False, labels=(), max_det=300):
+    """Drop-in for utils/general.py:633-725 (merge=False).  Returns a list of (k, 6) tensors
+    [xyxy, conf, cls] on the input device, rows in NMS keep order.
+
+    All per-image work runs in three HIP kernels (candidates, bitonic sort, greedy lazy-IoU scan);
+    the host reads two small count vectors (candidate counts to size the sort, keep counts to
+    slice the output) instead of the reference's per-image syncs.
+    """
+    assert 0 <= conf_thres <= 1 and 0 <= iou_thres <= 1
+    if labels is not None and len(labels) and any(len(l) for l in labels):
+        raise NotImplementedError('autolabel (labels=...) is outside the DMA-YOLO hot path')
+    pred = prediction.detach()
+    if pred.dtype != torch.float32:
+        pred = pred.float()
+    pred = pred.contiguous()
+    nimg, A, no = pred.shape
+    nc = no - 5
+    multi = bool(multi_label and nc > 1)
+    dev = pred.device
+    max_nms = 30000
+    cls_ok = None
+    if classes is not None:
+        cls_ok = torch.zeros(nc, dtype=torch.uint8, device=dev)
+        cls_ok[torch.tensor([c for c in classes if 0 <= c < nc], dtype=torch.long, device=dev)] = 1
+    cap0 = A * (nc if multi else 1)
+    counts = torch.zeros(nimg, dtype=torch.int32, device=dev)
+    # pass 1: count only (cap 0) to size the sort buffer
+    keys = torch.empty(1, dtype=torch.int64, device=dev)
+    call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), 0,
+         ptr(counts), stream())
+    nmax = int(counts.max()) if nimg else 0
+    out_list = [torch.zeros((0, 6), device=dev) for _ in range(nimg)]
+    if nmax == 0:
+        return out_list
+    cap = _pow2(min(nmax, cap0))
+    keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
+    counts.zero_()
+    call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), cap,
+         ptr(counts), stream())
+    call('dmy_nms_sort', ptr(keys), cap, ptr(counts), nimg, stream())
+    boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
+    out = torch.empty((nimg, max_det, 6), dtype=torch.float32, device=dev)
+    nkeep = torch.zeros(nimg, dtype=torch.int32, device=dev)
+    call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
+         ptr(keys), cap, ptr(counts), ptr(boxes), ptr(out), ptr(nkeep), stream())
+    nk = nkeep.tolist()
+    return [out[b, :nk[b]] for b in range(nimg)]

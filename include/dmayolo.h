@@ -1,0 +1,141 @@
+/* dmayolo.h — C ABI of the MI355X-native (gfx950) DMA-YOLO detection path.
+ *
+ * The reference (Yaling-Li/DMA-YOLO) is pure Python: its plugin boundary is the YAML module
+ * namespace that models/yolo.py:377 resolves with eval(name), plus ComputeLoss
+ * (utils/loss.py:135-218) and non_max_suppression (utils/general.py:633-725).  Every ATen kernel
+ * those Python entry points reach is replaced by one entry point below; the Python host side
+ * (dma-yolo_amd/dmayolo) binds them with ctypes.
+ *
+ * Conventions
+ *   dtype      0 = float32 storage (parity mode), 1 = bfloat16 storage (throughput mode)
+ *   layout     activations are NHWC; `*ps` is the pixel stride in elements (>= C), so a channel
+ *              slice of a concatenation buffer is (base + c0, ps = Ctot)
+ *   weights    fp32 master weights are OIHW (torch layout); conv kernels consume OHWI / IHWO copies
+ *   stream     hipStream_t passed as void*; every call is stream-ordered and never synchronises
+ *   return     0 on success, else the hipError_t of the launch.  *_partial_rows / *_blocks return sizes.
+ */
+#ifndef DMAYOLO_H
+#define DMAYOLO_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- convolution: replaces nn.Conv2d in models/cspcm.py:15 (YAML Conv), models/common.py:67 (Conv),
+ *      :1283-1304 (SCConv k2/k3/k4), :1172-1178 (CoorAttention conv1/conv_h/conv_w), models/yolo.py:63
+ *      (Detect.m), and nn.Linear (common.py:105-108, 483-484) as a 1x1 conv over tokens. */
+int dmy_conv_fwd_partial_rows(long M, int K);
+int dmy_conv_fwd(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, float* psum, float* psq,
+                 int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
+                 void* stream);
+int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
+                   long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
+int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
+                   int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
+int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int KH, int KW,
+                   void* stream);
+int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int KH, int KW, void* stream);
+
+/* ---- BatchNorm2d + activation: replaces nn.BatchNorm2d/nn.SiLU/nn.Hardswish in models/common.py:68-73,
+ *      1176-1180, 1284-1306 with utils/torch_utils.py:161-170 eps/momentum. act: 0 none 1 silu 2 hardswish
+ *      3 sigmoid 4 gelu(erf). */
+int dmy_bn_partial_rows(long M);
+int dmy_bn_stats(int dtype, const void* z, long zps, long M, int C, float* psum, float* psq, void* stream);
+int dmy_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
+                    const float* beta, float* running_mean, float* running_var, long long* num_batches_tracked,
+                    float momentum, float eps, int update, float* mean, float* invstd, float* scale, float* shift,
+                    void* stream);
+int dmy_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean, const float* running_var,
+                     float eps, int C, float* scale, float* shift, void* stream);
+int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scale, const float* shift, int act,
+                   const void* res, long rps, void* y, long yps, long M, int C, void* stream);
+int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
+                      const float* shift, const float* mean, const float* invstd, int act, long M, int C, float* pdb,
+                      float* pdg, void* stream);
+int dmy_bn_bwd_finalize(const float* pdb, const float* pdg, int P, int C, double count, const float* gamma,
+                        const float* invstd, float* dgamma, float* dbeta, float* ca, float* cb, float* cc,
+                        void* stream);
+int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
+                     const float* shift, const float* mean, const float* invstd, int act, const float* ca,
+                     const float* cb, const float* cc, void* dz, long dzps, long M, int C, void* stream);
+int dmy_reduce_rows(const float* part, int P, int C, float* out, int accumulate, void* stream);
+
+/* ---- memory-bound NHWC ops */
+/* nn.MaxPool2d(k, 1, k//2): SPPF common.py:250-258, SPPFCSPC :1266-1274 */
+int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yps, unsigned char* argmax, int N, int H, int W,
+                    int C, int k, void* stream);
+int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned char* argmax, void* dx, long dxps,
+                    int accumulate, int N, int H, int W, int C, int k, void* stream);
+/* nn.AvgPool2d(r, r): SCConv.k2[0] common.py:1282 */
+int dmy_avgpool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, int r, void* stream);
+int dmy_avgpool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C, int r,
+                    void* stream);
+/* nearest resize: nn.Upsample (yaml head), F.interpolate in SCConv common.py:1311 */
+int dmy_resize_fwd(int dtype, const void* x, long xps, void* y, long yps, float yscale, int N, int IH, int IW, int OH,
+                   int OW, int C, void* stream);
+int dmy_resize_bwd(int dtype, const void* dy, long dps, void* dx, long dxps, int N, int IH, int IW, int OH, int OW,
+                   int C, void* stream);
+/* torch.cat / AdConcat2/3 fast-normalised weights: common.py:656-664, 994-1026 */
+int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long dps, long M, int C, const float* w, int idx,
+                   int nw, float eps, int accumulate, void* stream);
+int dmy_dot_partial_blocks(long M, int C);
+int dmy_dot_partial(int dtype, const void* a, long aps, const void* b, long bps, long M, int C, float* part,
+                    void* stream);
+int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* w, float eps, float* dw, void* stream);
+/* SCConv gate k3(x) * sigmoid(x + up(k2(x))): common.py:1311-1314 */
+int dmy_scgate_fwd(int dtype, const void* x, long xps, const void* u3, const void* g, void* out, int N, int H, int W,
+                   int C, int GH, int GW, void* stream);
+int dmy_scgate_bwd(int dtype, const void* x, long xps, const void* u3, const void* g, const void* dout, void* du3,
+                   void* dpre, int N, int H, int W, int C, int GH, int GW, void* stream);
+/* CoorAttention pooling + re-weighting: common.py:1183-1207 */
+int dmy_ca_pool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, void* stream);
+int dmy_ca_pool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C,
+                    void* stream);
+int dmy_ca_apply_fwd(int dtype, const void* x, long xps, const void* lh, const void* lw, void* out, long ops, int N,
+                     int H, int W, int C, void* stream);
+int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh, const void* lw, const void* dout, long dps,
+                     void* dx, long dxps, void* dlh, void* dlw, int N, int H, int W, int C, void* stream);
+/* input normalisation imgs.float()/255 (train.py:402) + layout changes */
+int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, float scale,
+                     void* stream);
+int dmy_nhwc_to_nchw_f32(int dtype, const void* x, long xps, float* y, int N, int C, int H, int W, void* stream);
+int dmy_pointwise(int dtype, int op, int act, const void* a, const void* b, void* y, long n, float alpha,
+                  void* stream);
+int dmy_cast(int src_kind, int dst_kind, const void* x, void* y, long n, float scale, void* stream);
+
+/* ---- Detect decode (models/yolo.py:78-101) and ComputeLoss (utils/loss.py:167-276, metrics.py:192-235) */
+int dmy_detect_decode(int dtype, const void* y, long sb, long sh, long sw, int N, int H, int W, int na, int no,
+                      float stride, const float* anchors, float* z, long zoff, long ztotal, void* stream);
+int dmy_build_targets(const float* targets, int nt, const float* anchors, int na, int H, int W, float anchor_t,
+                      int* b, int* a, int* gj, int* gi, int* tcls, float* tbox, float* anch, int* count,
+                      void* stream);
+int dmy_yolo_loss_level(int dtype, const void* p, long sb, long sa, long sh, long sw, int N, int na, int H, int W,
+                        int no, int nc, float box_gain, float obj_gain, float cls_gain, float cls_pw, float obj_pw,
+                        float cp, float cn, float balance, float bs, const int* b, const int* a, const int* gj,
+                        const int* gi, const int* tcls, const float* tbox, const float* anch, const int* count,
+                        int cap, float* grad, float* tobj, float* acc3, void* stream);
+int dmy_yolo_loss_finalize(const float* acc, int nl, float box, float obj, float cls, float bs, float* loss,
+                           float* items, void* stream);
+int dmy_loss_grad(int dtype, const float* grad, const float* upstream, void* dp, long n, void* stream);
+
+/* ---- non_max_suppression (utils/general.py:633-725 -> torchvision.ops.nms at :708) */
+int dmy_nms_candidates(const float* pred, int nimg, int A, int no, float conf, int multi_label,
+                       const unsigned char* class_ok, unsigned long long* keys, long cap, int* counts, void* stream);
+int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, int nimg, void* stream);
+int dmy_nms_greedy(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det, int max_nms,
+                   const unsigned long long* keys, long cap, const int* counts, float* boxes, float* out, int* nkeep,
+                   void* stream);
+
+/* ---- optimizer step / EMA (train.py:216-222, 449-454; utils/torch_utils.py:329-339) */
+int dmy_chunk_size(void);
+int dmy_sgd(float* const* p, const float* const* g, float* const* m, const long* n, const int* tid, const long* off,
+            int nchunks, float lr, float momentum, float weight_decay, int nesterov, int first, void* stream);
+int dmy_adam(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n, const int* tid,
+             const long* off, int nchunks, float lr, float beta1, float beta2, float eps, float weight_decay,
+             float bias_corr1, float bias_corr2_sqrt, void* stream);
+int dmy_ema(float* const* ema, const float* const* src, const long* n, const int* tid, const long* off, int nchunks,
+            float decay, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

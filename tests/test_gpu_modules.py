@@ -1,0 +1,64 @@
+"""GPU parity: product HIP modules vs golden vectors from the reference (fp32 storage, tight
+tolerance) and vs the CPU oracle on fresh seeded inputs (fp32 and bf16 storage)."""
+import pytest
+import torch
+
+from golden_util import Fixture, golden_names
+from gpu_util import product_modules, run_case, rel_err
+from test_oracle_golden import MODULE_CASES, MODS as ORACLE_MODS, check_module_case
+
+pytestmark = pytest.mark.gpu
+
+# fp32 storage: the HIP path uses exact-fp32 MFMA; differences come from summation order only
+RTOL, ATOL = 2e-4, 2e-5
+GRAD_TOL = (1e-3, 1e-4)
+
+
+@pytest.mark.parametrize('name', MODULE_CASES)
+def test_module_vs_reference_golden_fp32(name):
+    fx, res = run_case(name, product_modules(), 'cuda')
+    check_module_case(fx, res, RTOL, ATOL, GRAD_TOL)
+
+
+@pytest.mark.parametrize('name', [n for n in MODULE_CASES if not n.startswith(('swin', 'c3str'))])
+def test_module_vs_oracle_bf16(name):
+    """bf16 storage (throughput mode): relative error bound 3e-2 on outputs and grads."""
+    fx, res = run_case(name, product_modules(), 'cuda', dtype=torch.bfloat16)
+    _, ref = run_case(name, ORACLE_MODS, 'cpu')
+    for a, b in zip(res['out'], ref['out']):
+        assert rel_err(a, b) < 3e-2, rel_err(a, b)
+    for a, b in zip(res['gin'], ref['gin']):
+        assert rel_err(a, b) < 6e-2, rel_err(a, b)
+    for k, b in ref['gp'].items():
+        assert rel_err(res['gp'][k], b) < 6e-2, (k, rel_err(res['gp'][k], b))
+
+
+@pytest.mark.parametrize('name,shape', [('conv_k3s2', (3, 16, 33, 21)), ('c3_1', (2, 16, 24, 40)),
+                                        ('scconv_sq', (2, 16, 44, 36)), ('sppfcspc', (1, 32, 17, 23)),
+                                        ('ca', (3, 32, 20, 9)), ('c3ca_sc', (1, 32, 16, 12))])
+def test_module_vs_oracle_new_shapes(name, shape):
+    """Same weights, new seeded inputs of other (ragged) shapes: HIP fp32 vs CPU oracle."""
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(7))
+    fx, res = run_case(name, product_modules(), 'cuda', inputs=[x])
+    _, ref = run_case(name, ORACLE_MODS, 'cpu', inputs=[x])
+    for a, b in zip(res['out'], ref['out']):
+        torch.testing.assert_close(a, b, rtol=RTOL, atol=ATOL)
+    for a, b in zip(res['gin'], ref['gin']):
+        torch.testing.assert_close(a, b, rtol=GRAD_TOL[0], atol=GRAD_TOL[1] * max(1, float(b.abs().max())))
+    for k, b in ref['gp'].items():
+        torch.testing.assert_close(res['gp'][k], b, rtol=GRAD_TOL[0], atol=GRAD_TOL[1] * max(1, float(b.abs().max())))
+
+
+def test_conv_fuse_gpu():
+    from dmayolo.models.common import Conv
+    from dmayolo.utils.torch_utils import fuse_conv_and_bn
+    from golden_util import load_sd
+    from oracle.nn import bn_defaults
+    fx = Fixture('conv_fuse')
+    m = bn_defaults(Conv(16, 32, 3, 1))
+    load_sd(m, fx.group('sd'))
+    m = m.cuda().eval()
+    m.conv = fuse_conv_and_bn(m.conv, m.bn)
+    with torch.no_grad():
+        y = m.forward_fuse(fx.t('in.0').cuda())
+    torch.testing.assert_close(y.float().cpu(), fx.t('eout.0'), rtol=RTOL, atol=ATOL)
