@@ -65,6 +65,14 @@ SIGNATURES = {
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
     'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P],
+    # swin.hip
+    'dmy_layernorm_fwd': [I, P, L, P, P, P, P, P, L, I, F, P],
+    'dmy_layernorm_bwd_blocks': [L],
+    'dmy_layernorm_bwd': [I, P, L, P, L, P, P, P, P, L, L, I, P, P, P],
+    'dmy_winattn_fwd': [I, P, P, P, I, I, I, I, I, I, F, P],
+    'dmy_winattn_bwd_groups': [I, I, I, I],
+    'dmy_winattn_bwd': [I, P, P, P, P, P, P, I, I, I, I, I, I, F, P],
+    'dmy_sample_scale': [I, P, P, P, L, L, P],
 }
 
 
@@ -89,7 +97,7 @@ lib = _load()
 
 def call(name, *args):
     rc = getattr(lib, name)(*args)
-    if name.endswith(('partial_rows', 'partial_blocks')):
+    if name.endswith(('partial_rows', 'partial_blocks', '_blocks', '_groups')):
         return rc
     if rc != 0:
         raise RuntimeError(f'{name} failed with hipError {rc}')

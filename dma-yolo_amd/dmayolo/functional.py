@@ -66,10 +66,39 @@ def conv_out_hw(H, W, k, s, p):
     return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
 
 
+class KernelTimer:
+    """Live per-launch timing of the implicit-GEMM conv kernels with HIP events on the launch
+    stream (bench.py roofline).  Off by default; zero overhead when disabled."""
+    enabled = False
+    records = []  # (kind, algorithmic_flops, start_event, end_event)
+
+    @classmethod
+    def run(cls, kind, flops, name, *args):
+        if not cls.enabled:
+            return call(name, *args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call(name, *args)
+        e1.record()
+        cls.records.append((kind, flops, e0, e1))
+
+    @classmethod
+    def summary(cls):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, fl, e0, e1 in cls.records:
+            d = out.setdefault(kind, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += fl
+            d[2] += e0.elapsed_time(e1) * 1e-3
+        cls.records = []
+        return {k: dict(launches=v[0], flops=v[1], seconds=v[2]) for k, v in out.items()}
+
+
 def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
     N, C, H, W = x.shape
-    call('dmy_conv_fwd', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k,
-         s, p, OH, OW, yps, stream())
+    KernelTimer.run('conv_fwd', 2.0 * N * OH * OW * K * C * k * k, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf),
+                    ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream())
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -178,15 +207,17 @@ class ConvBNActFn(torch.autograd.Function):
                 call('dmy_bn_stats', dt, ptr(dz), dzps, M, K, ptr(ps_), ptr(pq_), stream())
                 dbias = f32(K, dev)
                 call('dmy_reduce_rows', ptr(ps_), P, K, ptr(dbias), 0, stream())
+        if spec.bn is not None and ctx.has_bias and ctx.train_bn:
+            dbias = torch.zeros(K, dtype=torch.float32, device=dev)  # sum(dz) == 0 exactly behind train-mode BN
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = new_act(N, C, H, W, z)
-            call('dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(dx), 0, N, H, W, C, C, K, k, k, s, p, OH, OW, dzps,
-                 stream())
+            KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(dx), 0,
+                            N, H, W, C, C, K, k, k, s, p, OH, OW, dzps, stream())
         if ctx.needs_input_grad[1]:
             dwo = f32(K * C * k * k, dev)
-            call('dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N, H, W, C, xps, K, k, k, s, p, OH, OW, dzps,
-                 stream())
+            KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
+                            H, W, C, xps, K, k, k, s, p, OH, OW, dzps, stream())
             dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
             call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, k, k, stream())
         dres = dy if ctx.has_res else None
@@ -448,3 +479,89 @@ class ToNHWC(torch.autograd.Function):
         dx = torch.empty((N, C, H, W), dtype=torch.float32, device=dy.device)
         call('dmy_nhwc_to_nchw_f32', dcode(dy), ptr(dy), dps, ptr(dx), N, C, H, W, stream())
         return dx.to(ctx.src_dtype), None
+
+
+# ------------------------------------------------------------------ Swin pieces (csrc/swin.hip)
+
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm over channels of an NHWC activation (common.py:560, 565)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        M = N * H * W
+        y = new_act(N, C, H, W, x)
+        mean, rstd = f32(M, x.device), f32(M, x.device)
+        call('dmy_layernorm_fwd', dcode(x), ptr(x), xps, ptr(w), ptr(b), ptr(y), ptr(mean), ptr(rstd), M, C,
+             float(eps), stream())
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.xps = xps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        N, C, H, W = x.shape
+        M = N * H * W
+        dy, dps = pixel_stride(dy)
+        dx = new_act(N, C, H, W, x)
+        P = call('dmy_layernorm_bwd_blocks', M)
+        pdw, pdb = f32(P * C, x.device), f32(P * C, x.device)
+        call('dmy_layernorm_bwd', dcode(x), ptr(x), ctx.xps, ptr(dy), dps, ptr(w), ptr(mean), ptr(rstd), ptr(dx), C,
+             M, C, ptr(pdw), ptr(pdb), stream())
+        dw, db = f32(C, x.device), f32(C, x.device)
+        call('dmy_reduce_rows', ptr(pdw), P, C, ptr(dw), 0, stream())
+        call('dmy_reduce_rows', ptr(pdb), P, C, ptr(db), 0, stream())
+        return dx, dw, db, None
+
+
+class WinAttnFn(torch.autograd.Function):
+    """Shifted-window MHSA core (common.py:500-545 + 595-631): qkv [N,3C,H,W] NHWC -> [N,C,H,W]."""
+
+    @staticmethod
+    def forward(ctx, qkv, table, nh, shift, scale):
+        qkv = qkv.contiguous(memory_format=CL)
+        N, C3, H, W = qkv.shape
+        C = C3 // 3
+        out = torch.zeros((N, C, H, W), dtype=qkv.dtype, device=qkv.device, memory_format=CL)
+        tab = table.detach().float().contiguous()
+        call('dmy_winattn_fwd', dcode(qkv), ptr(qkv), ptr(tab), ptr(out), N, H, W, C, nh, shift, float(scale),
+             stream())
+        ctx.save_for_backward(qkv, tab)
+        ctx.cfg = (nh, shift, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, tab = ctx.saved_tensors
+        nh, shift, scale = ctx.cfg
+        N, C3, H, W = qkv.shape
+        dout = dout.contiguous(memory_format=CL)
+        dqkv = torch.zeros_like(qkv, memory_format=CL)
+        groups = call('dmy_winattn_bwd_groups', N, H, W, nh)
+        part = f32(groups * nh * 225, qkv.device)
+        dtab = torch.empty_like(tab)
+        call('dmy_winattn_bwd', dcode(qkv), ptr(qkv), ptr(dout), ptr(tab), ptr(dqkv), ptr(part), ptr(dtab), N, H, W,
+             C3 // 3, nh, shift, float(scale), stream())
+        return dqkv, dtab, None, None, None
+
+
+class SampleScaleFn(torch.autograd.Function):
+    """y = x * s[b] (DropPath with a pre-drawn per-sample keep mask, common.py:386-403)."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        x = x.contiguous(memory_format=CL)
+        y = torch.empty_like(x, memory_format=CL)
+        call('dmy_sample_scale', dcode(x), ptr(x), ptr(s), ptr(y), x.numel() // x.shape[0], x.numel(), stream())
+        ctx.save_for_backward(s)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (s,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=CL)
+        dx = torch.empty_like(dy, memory_format=CL)
+        call('dmy_sample_scale', dcode(dy), ptr(dy), ptr(s), ptr(dx), dy.numel() // dy.shape[0], dy.numel(), stream())
+        return dx, None

@@ -13,7 +13,12 @@ class DropPath(nn.Module):
         self.drop_prob = drop_prob
 
     def forward(self, x):
-        raise NotImplementedError
+        """Per-sample stochastic depth on the HIP path (the keep mask is drawn with torch's RNG)."""
+        if self.drop_prob == 0. or not self.training or not self.drop_prob:
+            return x
+        keep = 1 - self.drop_prob
+        s = (keep + torch.rand((x.shape[0],), dtype=torch.float32, device=x.device)).floor_().div_(keep)
+        return Fn.SampleScaleFn.apply(x, s)
 
 
 class Mlp(nn.Module):
@@ -63,7 +68,27 @@ class SwinTransformerLayer(nn.Module):
         self.mlp = Mlp(in_features=c, hidden_features=int(c * mlp_ratio), act_layer=act_layer, drop=drop)
 
     def forward(self, x):
-        raise NotImplementedError('Swin kernels land in csrc/swin.hip')
+        """common.py:595-637 on NHWC tokens: LN -> qkv -> shifted-window attention (pad/roll/partition
+        folded into the kernel's addressing) -> proj (+ residual) -> LN -> MLP(GELU) (+ residual)."""
+        c = x.shape[1]
+        a = self.attn
+        u = Fn.LayerNormFn.apply(x, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        qkv = Fn.conv_bn_act(u, a.qkv.weight.view(3 * c, c, 1, 1), a.qkv.bias, None, 1, 0, Fn.ACT_NONE)
+        o = Fn.WinAttnFn.apply(qkv, a.relative_position_bias_table, a.num_heads, self.shift_size, a.scale)
+        dp = isinstance(self.drop_path, DropPath) and self.training and self.drop_path.drop_prob
+        if dp:
+            x = Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias,
+                                                                None, 1, 0, Fn.ACT_NONE)))
+        else:
+            x = Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias, None, 1, 0, Fn.ACT_NONE, res=x)
+        m = self.mlp
+        u2 = Fn.LayerNormFn.apply(x, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        hd = m.fc1.weight.shape[0]
+        h = Fn.conv_bn_act(u2, m.fc1.weight.view(hd, c, 1, 1), m.fc1.bias, None, 1, 0, Fn.ACT_GELU)
+        if dp:
+            return Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias,
+                                                                   None, 1, 0, Fn.ACT_NONE)))
+        return Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0, Fn.ACT_NONE, res=x)
 
 
 class SwinTransformerBlock(nn.Module):

@@ -125,6 +125,20 @@ int dmy_nms_greedy(const float* pred, int nimg, int A, int no, float iou, int ag
                    const unsigned long long* keys, long cap, const int* counts, float* boxes, float* out, int* nkeep,
                    void* stream);
 
+/* ---- Swin / C3STR (models/common.py:452-654): LayerNorm, shifted-window attention core with the
+ *      reference's mask semantics, per-sample DropPath scale (common.py:386-403) */
+int dmy_layernorm_fwd(int dtype, const void* x, long xps, const float* w, const float* b, void* y, float* mean,
+                      float* rstd, long M, int C, float eps, void* stream);
+int dmy_layernorm_bwd_blocks(long M);
+int dmy_layernorm_bwd(int dtype, const void* x, long xps, const void* dy, long dps, const float* w, const float* mean,
+                      const float* rstd, void* dx, long dxps, long M, int C, float* pdw, float* pdb, void* stream);
+int dmy_winattn_fwd(int dtype, const void* qkv, const float* table, void* out, int B, int H, int W, int C, int nh,
+                    int shift, float scale, void* stream);
+int dmy_winattn_bwd_groups(int B, int H, int W, int nh);
+int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const float* table, void* dqkv, float* dtab_part,
+                    float* dtab, int B, int H, int W, int C, int nh, int shift, float scale, void* stream);
+int dmy_sample_scale(int dtype, const void* x, const float* scale, void* y, long per, long n, void* stream);
+
 /* ---- optimizer step / EMA (train.py:216-222, 449-454; utils/torch_utils.py:329-339) */
 int dmy_chunk_size(void);
 int dmy_sgd(float* const* p, const float* const* g, float* const* m, const long* n, const int* tid, const long* off,

@@ -8,7 +8,7 @@ import yaml
 
 from golden_util import Fixture
 
-YAMLS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests', 'configs')
+YAMLS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'dma-yolo_amd', 'dmayolo', 'configs')
 
 
 @pytest.mark.parametrize('name', ['model_v5s', 'model_dma'])

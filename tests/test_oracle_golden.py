@@ -37,7 +37,7 @@ def run_module_case(name, build=None, device='cpu', dtype=torch.float32):
     loss.backward()
     res = dict(out=[o.detach().float().cpu() for o in outs], gin=[x.grad.float().cpu() for x in ins],
                gp={k: p.grad.float().cpu() for k, p in mod.named_parameters() if p.grad is not None},
-               buf={k: v.float().cpu() for k, v in mod.state_dict().items() if 'running' in k})
+               buf={k: v.float().cpu().clone() for k, v in mod.state_dict().items() if 'running' in k})
     mod.load_state_dict({k: v for k, v in mod.state_dict().items()})
     load_sd(mod, fx.group('sd'))
     mod.eval()

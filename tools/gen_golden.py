@@ -41,7 +41,7 @@ torch.set_num_threads(8)
 
 
 def npy(t):
-    return t.detach().cpu().numpy()
+    return t.detach().cpu().numpy().copy()  # copy: never alias module buffers that are reloaded later
 
 
 def randomize_bn(mod, gen):
