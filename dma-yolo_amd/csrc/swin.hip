@@ -357,7 +357,7 @@ DMY_API int dmy_winattn_bwd_groups(int B, int H, int W, int nh) {
   return (int)groups;
 }
 
-// dqkv must be zero-initialised by the caller (padding tokens are never written)
+// every real pixel lies in exactly one window, so dqkv is fully written (padding tokens have no storage)
 DMY_API int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const float* table, void* dqkv,
                             float* dtab_part, float* dtab, int B, int H, int W, int C, int nh, int shift, float scale,
                             void* stream) {

@@ -524,7 +524,7 @@ class WinAttnFn(torch.autograd.Function):
         qkv = qkv.contiguous(memory_format=CL)
         N, C3, H, W = qkv.shape
         C = C3 // 3
-        out = torch.zeros((N, C, H, W), dtype=qkv.dtype, device=qkv.device, memory_format=CL)
+        out = torch.empty((N, C, H, W), dtype=qkv.dtype, device=qkv.device, memory_format=CL)  # every pixel is written
         tab = table.detach().float().contiguous()
         call('dmy_winattn_fwd', dcode(qkv), ptr(qkv), ptr(tab), ptr(out), N, H, W, C, nh, shift, float(scale),
              stream())
@@ -538,7 +538,7 @@ class WinAttnFn(torch.autograd.Function):
         nh, shift, scale = ctx.cfg
         N, C3, H, W = qkv.shape
         dout = dout.contiguous(memory_format=CL)
-        dqkv = torch.zeros_like(qkv, memory_format=CL)
+        dqkv = torch.empty_like(qkv, memory_format=CL)  # every pixel belongs to exactly one window
         groups = call('dmy_winattn_bwd_groups', N, H, W, nh)
         part = f32(groups * nh * 225, qkv.device)
         dtab = torch.empty_like(tab)

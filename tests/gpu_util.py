@@ -56,4 +56,6 @@ def run_case(name, mods, device, dtype=torch.float32, inputs=None, sd=None):
 
 def rel_err(a, b):
     """relative L2 error (robust to the few max-pool argmax swaps bf16 rounding causes)"""
-    return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-12))
+    # absolute floor: grads that are pure rounding noise in the reference (a bias feeding a
+    # train-mode BN has an exactly-zero gradient) must not count as 100 % error
+    return float((a.double() - b.double()).norm() / max(b.double().norm(), 1e-4 * b.numel() ** 0.5))
