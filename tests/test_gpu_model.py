@@ -37,7 +37,7 @@ def test_model_train_eval_fp32(name):
     names = [str(s) for s in fx.z['pnames']]
     got = torch.tensor([float(params[k].grad.norm()) if params[k].grad is not None else 0.0 for k in names],
                        dtype=torch.float64)
-    torch.testing.assert_close(got, gn, rtol=5e-3, atol=1e-6)
+    torch.testing.assert_close(got, gn, rtol=5e-3, atol=1e-5)  # zero-grad biases before BN: noise in the reference
     load_sd(m, fx.group('sd'))
     m.eval()
     with torch.no_grad():
