@@ -89,32 +89,170 @@ __global__ void bn_eval_coef_kernel(const float* gamma, const float* beta, const
   shift[c] = b - rmean[c] * g * is;
 }
 
+// Thread mapping shared by the vectorised kernels below: a block of 256 threads covers RB rows x
+// CV channel-vectors (CV = C / VW, RB = 256 / CV); each thread keeps ONE channel-vector for the
+// whole launch, so its per-channel coefficients live in registers and every access is a 16-B
+// vector.  Rows are grid-strided.
+struct RowMap {
+  int cv, rr, RB, CV;
+  DEV RowMap(int C, int VW) {
+    CV = C / VW;
+    RB = 256 / CV;
+    cv = threadIdx.x % CV;
+    rr = threadIdx.x / CV;
+  }
+  DEV bool active() const { return rr < RB; }
+};
+
 // -------- y = act(z * scale + shift) (+ res)
-template <typename T, bool VEC>
-__global__ void bn_act_fwd_kernel(const T* __restrict__ z, long zps, const float* __restrict__ scale,
+template <typename T>
+__global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, long zps, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int act, const T* __restrict__ res,
+                                                      long rps, T* __restrict__ y, long yps, long M, int C) {
+  constexpr int VW = Traits<T>::VW;
+  RowMap rm(C, VW);
+  if (!rm.active()) return;
+  const int c0 = rm.cv * VW;
+  float sc[VW], sh[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
+    float f[VW];
+    unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), f);
+    if (res) {
+      float r[VW];
+      unpack<T>(*reinterpret_cast<const uint4*>(res + m * rps + c0), r);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+    }
+    *reinterpret_cast<uint4*>(y + m * yps + c0) = pack<T>(f);
+  }
+}
+
+template <typename T>
+__global__ void bn_act_fwd_scalar(const T* __restrict__ z, long zps, const float* __restrict__ scale,
                                   const float* __restrict__ shift, int act, const T* __restrict__ res, long rps,
                                   T* __restrict__ y, long yps, long M, int C) {
-  constexpr int VW = Traits<T>::VW;
-  const int cv = VEC ? C / VW : C;
-  const long total = M * cv;
+  const long total = M * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / cv;
-    const int c = (int)(i % cv) * (VEC ? VW : 1);
-    if (VEC) {
-      float f[VW], r[VW];
-      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c), f);
-      if (res) unpack<T>(*reinterpret_cast<const uint4*>(res + m * rps + c), r);
+    const long m = i / C;
+    const int c = (int)(i % C);
+    float v = act_fwd(act, to_f(z[m * zps + c]) * scale[c] + shift[c]);
+    if (res) v += to_f(res[m * rps + c]);
+    y[m * yps + c] = from_f<T>(v);
+  }
+}
+
+// -------- backward reduce: per channel  sum(du), sum(du * xhat), du = dy * act'(u)
+// also used (dy = z, act none, scale 1, shift 0, mean 0, invstd 1) as plain column sums
+template <typename T, bool STATS>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z, long zps, const T* __restrict__ dy,
+                                                         long dps, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd, int act, long M, int C,
+                                                         float* __restrict__ pdb, float* __restrict__ pdg) {
+  constexpr int VW = Traits<T>::VW;
+  __shared__ float red[2][256 * VW];
+  RowMap rm(C, VW);
+  const int c0 = rm.cv * VW;
+  float a[VW], b[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  if (rm.active()) {
+    float sc[VW], sh[VW], mu[VW], is[VW];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      sc[j] = STATS ? 1.f : scale[c0 + j];
+      sh[j] = STATS ? 0.f : shift[c0 + j];
+      mu[j] = STATS ? 0.f : mean[c0 + j];
+      is[j] = STATS ? 1.f : invstd[c0 + j];
+    }
+    for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
+      float zf[VW], gf[VW];
+      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
+      unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
-        f[j] = act_fwd(act, f[j] * scale[c + j] + shift[c + j]);
-        if (res) f[j] += r[j];
+        if (STATS) {  // plain column sums of z and z^2 (batch statistics / bias gradients)
+          a[j] += zf[j];
+          b[j] += zf[j] * zf[j];
+        } else {
+          const float du = gf[j] * act_grad(act, zf[j] * sc[j] + sh[j]);
+          a[j] += du;
+          b[j] += du * (zf[j] - mu[j]) * is[j];
+        }
       }
-      *reinterpret_cast<uint4*>(y + m * yps + c) = pack<T>(f);
-    } else {
-      float v = act_fwd(act, to_f(z[m * zps + c]) * scale[c] + shift[c]);
-      if (res) v += to_f(res[m * rps + c]);
-      y[m * yps + c] = from_f<T>(v);
     }
+  }
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    red[0][threadIdx.x * VW + j] = a[j];
+    red[1][threadIdx.x * VW + j] = b[j];
+  }
+  __syncthreads();
+  // one thread per channel sums the RB row groups
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int cv = c / VW, j = c % VW;
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = 0; r < rm.RB; ++r) {
+      const int t = r * rm.CV + cv;
+      s1 += red[0][t * VW + j];
+      s2 += red[1][t * VW + j];
+    }
+    pdb[(long)blockIdx.x * C + c] = s1;
+    pdg[(long)blockIdx.x * C + c] = s2;
+  }
+}
+
+// dz = ca*du + cb + cc*xhat   (train);  eval: cb = cc = 0, ca = scale
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z, long zps, const T* __restrict__ dy,
+                                                        long dps, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int act,
+                                                        const float* __restrict__ ca, const float* __restrict__ cb,
+                                                        const float* __restrict__ cc, T* __restrict__ dz, long dzps,
+                                                        long M, int C) {
+  constexpr int VW = Traits<T>::VW;
+  RowMap rm(C, VW);
+  if (!rm.active()) return;
+  const int c0 = rm.cv * VW;
+  float sc[VW], sh[VW], k1[VW], k0[VW], k2[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    sc[j] = scale[c0 + j];
+    sh[j] = shift[c0 + j];
+    // dz = ca*du + cb + cc*(z - mean)*invstd = ca*du + k0 + k2*z
+    k1[j] = ca[c0 + j];
+    k2[j] = cc[c0 + j] * invstd[c0 + j];
+    k0[j] = cb[c0 + j] - k2[j] * mean[c0 + j];
+  }
+  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
+    float zf[VW], gf[VW], o[VW];
+    unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
+    unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) o[j] = k1[j] * (gf[j] * act_grad(act, zf[j] * sc[j] + sh[j])) + k0[j] + k2[j] * zf[j];
+    *reinterpret_cast<uint4*>(dz + m * dzps + c0) = pack<T>(o);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_scalar(const T* __restrict__ z, long zps, const T* __restrict__ dy, long dps,
+                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                    const float* __restrict__ mean, const float* __restrict__ invstd, int act,
+                                    const float* __restrict__ ca, const float* __restrict__ cb,
+                                    const float* __restrict__ cc, T* __restrict__ dz, long dzps, long M, int C) {
+  const long total = M * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / C;
+    const int c = (int)(i % C);
+    const float zv = to_f(z[m * zps + c]);
+    const float du = to_f(dy[m * dps + c]) * act_grad(act, zv * scale[c] + shift[c]);
+    dz[m * dzps + c] = from_f<T>(ca[c] * du + cb[c] + cc[c] * (zv - mean[c]) * invstd[c]);
   }
 }
 
@@ -183,36 +321,27 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdb, const floa
   }
 }
 
-// dz = ca*du + cb + cc*xhat   (train);  eval: cb = cc = 0, ca = scale
-template <typename T, bool VEC>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ z, long zps, const T* __restrict__ dy, long dps,
-                                    const float* __restrict__ scale, const float* __restrict__ shift,
-                                    const float* __restrict__ mean, const float* __restrict__ invstd, int act,
-                                    const float* __restrict__ ca, const float* __restrict__ cb,
-                                    const float* __restrict__ cc, T* __restrict__ dz, long dzps, long M, int C) {
-  constexpr int VW = Traits<T>::VW;
-  const int cv = VEC ? C / VW : C;
-  const long total = M * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / cv;
-    const int c0 = (int)(i % cv) * (VEC ? VW : 1);
-    if (VEC) {
-      float zf[VW], gf[VW], o[VW];
-      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
-      unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
-#pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const int c = c0 + j;
-        const float du = gf[j] * act_grad(act, zf[j] * scale[c] + shift[c]);
-        o[j] = ca[c] * du + cb[c] + cc[c] * (zf[j] - mean[c]) * invstd[c];
-      }
-      *reinterpret_cast<uint4*>(dz + m * dzps + c0) = pack<T>(o);
-    } else {
-      const int c = c0;
-      const float zv = to_f(z[m * zps + c]);
-      const float du = to_f(dy[m * dps + c]) * act_grad(act, zv * scale[c] + shift[c]);
-      dz[m * dzps + c] = from_f<T>(ca[c] * du + cb[c] + cc[c] * (zv - mean[c]) * invstd[c]);
+// two-stage column sums of [P][C] float partial pairs -> [S][C]
+__global__ void colsum2_kernel(const float* __restrict__ a, const float* __restrict__ b, long P, int C, int rows_per,
+                               float* __restrict__ oa, float* __restrict__ ob) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  __shared__ double s1[4][64], s2[4][64];
+  double x = 0.0, y = 0.0;
+  if (c < C) {
+    const long r0 = (long)blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+    for (long r = r0 + ty; r < r1; r += 4) {
+      x += a[r * C + c];
+      y += b[r * C + c];
     }
+  }
+  s1[ty][threadIdx.x & 63] = x;
+  s2[ty][threadIdx.x & 63] = y;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    const int l = threadIdx.x;
+    oa[(long)blockIdx.x * C + c] = (float)(s1[0][l] + s1[1][l] + s1[2][l] + s1[3][l]);
+    ob[(long)blockIdx.x * C + c] = (float)(s2[0][l] + s2[1][l] + s2[2][l] + s2[3][l]);
   }
 }
 
@@ -223,12 +352,25 @@ inline bool vec_ok(int VW, int C, long s1, long s2, long s3, const void* p1, con
 
 }  // namespace
 
+inline int vec_grid(long M, int C, int VW) {
+  const int RB = 256 / (C / VW);
+  return grid_cap(ceil_div(M, (long)RB * 8), 4096);
+}
+
 DMY_API int dmy_bn_partial_rows(long M) {
   long p = (M + 255) / 256;
   return (int)(p < 1024 ? (p < 1 ? 1 : p) : 1024);
 }
 
 DMY_API int dmy_bn_stats(int dtype, const void* z, long zps, long M, int C, float* psum, float* psq, void* stream) {
+  const int VW = dtype ? 8 : 4;
+  if (vec_ok(VW, C, zps, 0, 0, z, nullptr, nullptr) && C / VW <= 256) {
+    const int g = vec_grid(M, C, VW);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype) bn_bwd_reduce_vec<bf16, true><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq);
+    else bn_bwd_reduce_vec<float, true><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq);
+    return (int)hipGetLastError();
+  }
   const int P = dmy_bn_partial_rows(M);
   const int rpb = (int)((M + P - 1) / P);
   dim3 grid(P, ceil_div(C, 64));
@@ -251,33 +393,59 @@ DMY_API int dmy_bn_eval_coef(const float* gamma, const float* beta, const float*
   return (int)hipGetLastError();
 }
 
+
 DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scale, const float* shift, int act,
                            const void* res, long rps, void* y, long yps, long M, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int VW = dtype ? 8 : 4;
-  const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res);
-  const long work = M * (vec ? C / VW : C);
-  const int grid = grid_cap(ceil_div(work, 256), 8192);
-  if (dtype) {
-    if (vec) bn_act_fwd_kernel<bf16, true><<<grid, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
-    else bn_act_fwd_kernel<bf16, false><<<grid, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+  const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res) && C / VW <= 256;
+  if (vec) {
+    const int g = vec_grid(M, C, VW);
+    if (dtype) bn_act_fwd_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+    else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
   } else {
-    if (vec) bn_act_fwd_kernel<float, true><<<grid, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
-    else bn_act_fwd_kernel<float, false><<<grid, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
+    const int g = grid_cap(ceil_div(M * C, 256), 8192);
+    if (dtype) bn_act_fwd_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+    else bn_act_fwd_scalar<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
   }
   return (int)hipGetLastError();
+}
+
+// Partial rows written by dmy_bn_bwd_reduce / dmy_bn_stats for these exact arguments.
+DMY_API int dmy_bn_reduce_rows(int dtype, const void* z, long zps, const void* dy, long dps, long M, int C) {
+  const int VW = dtype ? 8 : 4;
+  if (vec_ok(VW, C, zps, dy ? dps : 0, 0, z, dy, nullptr) && C / VW <= 256) return vec_grid(M, C, VW);
+  return dmy_bn_partial_rows(M);
 }
 
 DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
                               const float* shift, const float* mean, const float* invstd, int act, long M, int C,
                               float* pdb, float* pdg, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int VW = dtype ? 8 : 4;
+  if (vec_ok(VW, C, zps, dps, 0, z, dy, nullptr) && C / VW <= 256) {
+    const int g = vec_grid(M, C, VW);
+    if (dtype) bn_bwd_reduce_vec<bf16, false><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg);
+    else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg);
+    return (int)hipGetLastError();
+  }
   const int P = dmy_bn_partial_rows(M);
   const int rpb = (int)((M + P - 1) / P);
   dim3 grid(P, ceil_div(C, 64));
   if (dtype)
-    bn_bwd_reduce_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
+    bn_bwd_reduce_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
   else
-    bn_bwd_reduce_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
+    bn_bwd_reduce_kernel<float><<<grid, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, rpb, pdb, pdg);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_colsum2_rows(long P) { return (int)(P < 256 ? P : 256); }
+
+DMY_API int dmy_colsum2(const float* a, const float* b, long P, int C, float* oa, float* ob, void* stream) {
+  const int S = dmy_colsum2_rows(P);
+  const int rows = (int)((P + S - 1) / S);
+  dim3 grid(S, ceil_div(C, 64));
+  colsum2_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a, b, P, C, rows, oa, ob);
   return (int)hipGetLastError();
 }
 
@@ -294,15 +462,14 @@ DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy,
                              const float* cb, const float* cc, void* dz, long dzps, long M, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int VW = dtype ? 8 : 4;
-  const bool vec = vec_ok(VW, C, zps, dps, dzps, z, dy, dz);
-  const long work = M * (vec ? C / VW : C);
-  const int grid = grid_cap(ceil_div(work, 256), 8192);
-  if (dtype) {
-    if (vec) bn_bwd_apply_kernel<bf16, true><<<grid, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
-    else bn_bwd_apply_kernel<bf16, false><<<grid, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+  if (vec_ok(VW, C, zps, dps, dzps, z, dy, dz) && C / VW <= 256) {
+    const int g = vec_grid(M, C, VW);
+    if (dtype) bn_bwd_apply_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+    else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
   } else {
-    if (vec) bn_bwd_apply_kernel<float, true><<<grid, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
-    else bn_bwd_apply_kernel<float, false><<<grid, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
+    const int g = grid_cap(ceil_div(M * C, 256), 8192);
+    if (dtype) bn_bwd_apply_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+    else bn_bwd_apply_scalar<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
   }
   return (int)hipGetLastError();
 }

@@ -463,27 +463,28 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const T* __restrict__ x,
   }
 }
 
-// OIHW fp32 master weights -> T OHWI (forward B operand) and T IHWO (data-grad B operand).
+// OIHW fp32 master weights -> T OHWI (forward B operand, input channels padded to Cp with zeros)
+// and T IHWO (data-grad B operand).
 template <typename T>
-__global__ void wprep_kernel(const float* __restrict__ w, T* __restrict__ wf, T* __restrict__ wt, int K, int C,
+__global__ void wprep_kernel(const float* __restrict__ w, T* __restrict__ wf, T* __restrict__ wt, int K, int C, int Cp,
                              int KH, int KW) {
-  const long total = (long)K * C * KH * KW;
+  const long total = (long)K * Cp * KH * KW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int kw = (int)(i % KW);
-    long t = i / KW;
-    int kh = (int)(t % KH);
-    t /= KH;
-    int c = (int)(t % C);
-    int k = (int)(t / C);
-    T v = from_f<T>(w[i]);
-    if (wf) wf[(((long)k * KH + kh) * KW + kw) * C + c] = v;
-    if (wt) wt[(((long)c * KH + kh) * KW + kw) * K + k] = v;
+    const int c = (int)(i % Cp);
+    long t = i / Cp;
+    const int kw = (int)(t % KW);
+    t /= KW;
+    const int kh = (int)(t % KH);
+    const int k = (int)(t / KH);
+    const float v = c < C ? w[(((long)k * C + c) * KH + kh) * KW + kw] : 0.f;
+    if (wf) wf[i] = from_f<T>(v);
+    if (wt && c < C) wt[(((long)c * KH + kh) * KW + kw) * K + k] = from_f<T>(v);
   }
 }
 
-// OHWI fp32 grad accumulator -> OIHW param-shaped gradient
-__global__ void wgrad_to_oihw_kernel(const float* __restrict__ src, float* __restrict__ dst, int K, int C, int KH,
-                                     int KW) {
+// OHWI fp32 grad accumulator (input channels padded to Cp) -> OIHW param-shaped gradient
+__global__ void wgrad_to_oihw_kernel(const float* __restrict__ src, float* __restrict__ dst, int K, int C, int Cp,
+                                     int KH, int KW) {
   const long total = (long)K * C * KH * KW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int kw = (int)(i % KW);
@@ -492,7 +493,7 @@ __global__ void wgrad_to_oihw_kernel(const float* __restrict__ src, float* __res
     t /= KH;
     int c = (int)(t % C);
     int k = (int)(t / C);
-    dst[i] = src[(((long)k * KH + kh) * KW + kw) * C + c];
+    dst[i] = src[(((long)k * KH + kh) * KW + kw) * Cp + c];
   }
 }
 
@@ -612,18 +613,19 @@ DMY_API int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_o
                : conv_wgrad_t<float>(x, dy, dw_ohwi, g, (hipStream_t)stream);
 }
 
-DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int KH, int KW,
-                           void* stream) {
-  const long total = (long)K * C * KH * KW;
+DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH,
+                           int KW, void* stream) {
+  const long total = (long)K * Cp * KH * KW;
   const int grid = grid_cap(ceil_div(total, 256), 1024);
-  if (dtype) wprep_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (bf16*)w_ohwi, (bf16*)w_ihwo, K, C, KH, KW);
-  else wprep_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (float*)w_ohwi, (float*)w_ihwo, K, C, KH, KW);
+  if (dtype) wprep_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (bf16*)w_ohwi, (bf16*)w_ihwo, K, C, Cp, KH, KW);
+  else wprep_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (float*)w_ohwi, (float*)w_ihwo, K, C, Cp, KH, KW);
   return (int)hipGetLastError();
 }
 
-DMY_API int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int KH, int KW, void* stream) {
+DMY_API int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int Cp, int KH, int KW,
+                                   void* stream) {
   const long total = (long)K * C * KH * KW;
   wgrad_to_oihw_kernel<<<grid_cap(ceil_div(total, 256), 1024), 256, 0, (hipStream_t)stream>>>(dw_ohwi, dw_oihw, K, C,
-                                                                                               KH, KW);
+                                                                                               Cp, KH, KW);
   return (int)hipGetLastError();
 }

@@ -408,17 +408,18 @@ __global__ void ca_apply_bwd_att_kernel(const T* __restrict__ x, long xps, const
 // ---------------------------------------------------------------- input normalisation / layout
 // NCHW (uint8 or fp32) -> NHWC T, times `scale` (1/255 for uint8 images, train.py:402)
 template <typename S, typename T>
-__global__ void nchw_to_nhwc_kernel(const S* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W,
+__global__ void nchw_to_nhwc_kernel(const S* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W, int Cp,
                                     float scale) {
-  const long total = (long)N * C * H * W;
+  // output pixel stride Cp >= C; channels [C, Cp) are written as zeros (stem vector padding)
+  const long total = (long)N * Cp * H * W;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    const int c = (int)(i % Cp);
+    long t = i / Cp;
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
     const int b = (int)(t / H);
-    y[i] = from_f<T>((float)x[(((long)b * C + c) * H + h) * W + w] * scale);
+    y[i] = from_f<T>(c < C ? (float)x[(((long)b * C + c) * H + h) * W + w] * scale : 0.f);
   }
 }
 
@@ -572,15 +573,15 @@ DMY_API int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh,
   DISPATCH_T(dtype, ca_apply_bwd_att_kernel<T><<<egrid((long)N * (H + W) * C), 256, 0, st>>>((const T*)x, xps, (const T*)lh, (const T*)lw, (const T*)dout, dps, (T*)dlh, (T*)dlw, N, H, W, C));
   return (int)hipGetLastError();
 }
-// src_kind: 0 = uint8, 1 = fp32, 2 = bf16
-DMY_API int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, float scale,
-                             void* stream) {
+// src_kind: 0 = uint8, 1 = fp32; output NHWC with pixel stride Cp >= C (zero-filled tail channels)
+DMY_API int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cp,
+                             float scale, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const long n = (long)N * C * H * W;
+  const long n = (long)N * Cp * H * W;
   if (src_kind == 0) {
-    DISPATCH_T(dtype, nchw_to_nhwc_kernel<uint8_t, T><<<egrid(n), 256, 0, st>>>((const uint8_t*)x, (T*)y, N, C, H, W, scale));
+    DISPATCH_T(dtype, nchw_to_nhwc_kernel<uint8_t, T><<<egrid(n), 256, 0, st>>>((const uint8_t*)x, (T*)y, N, C, H, W, Cp, scale));
   } else {
-    DISPATCH_T(dtype, nchw_to_nhwc_kernel<float, T><<<egrid(n), 256, 0, st>>>((const float*)x, (T*)y, N, C, H, W, scale));
+    DISPATCH_T(dtype, nchw_to_nhwc_kernel<float, T><<<egrid(n), 256, 0, st>>>((const float*)x, (T*)y, N, C, H, W, Cp, scale));
   }
   return (int)hipGetLastError();
 }

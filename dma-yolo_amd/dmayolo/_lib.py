@@ -21,8 +21,8 @@ SIGNATURES = {
     'dmy_conv_fwd': [I, P, P, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_dgrad': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_wgrad': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
-    'dmy_conv_wprep': [I, P, P, P, I, I, I, I, P],
-    'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, P],
+    'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
+    'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, I, P],
     # bn.hip
     'dmy_bn_partial_rows': [L],
     'dmy_bn_stats': [I, P, L, L, I, P, P, P],
@@ -33,6 +33,9 @@ SIGNATURES = {
     'dmy_bn_bwd_finalize': [P, P, I, I, D, P, P, P, P, P, P, P, P],
     'dmy_bn_bwd_apply': [I, P, L, P, L, P, P, P, P, I, P, P, P, P, L, L, I, P],
     'dmy_reduce_rows': [P, I, I, P, I, P],
+    'dmy_bn_reduce_rows': [I, P, L, P, L, L, I],
+    'dmy_colsum2_rows': [L],
+    'dmy_colsum2': [P, P, L, I, P, P, P],
     # eltwise.hip
     'dmy_maxpool_fwd': [I, P, L, P, L, P, I, I, I, I, I, P],
     'dmy_maxpool_bwd': [I, P, L, P, P, L, I, I, I, I, I, I, P],
@@ -50,7 +53,7 @@ SIGNATURES = {
     'dmy_ca_pool_bwd': [I, P, P, L, I, I, I, I, I, P],
     'dmy_ca_apply_fwd': [I, P, L, P, P, P, L, I, I, I, I, P],
     'dmy_ca_apply_bwd': [I, P, L, P, P, P, L, P, L, P, P, I, I, I, I, P],
-    'dmy_nchw_to_nhwc': [I, I, P, P, I, I, I, I, F, P],
+    'dmy_nchw_to_nhwc': [I, I, P, P, I, I, I, I, I, F, P],
     'dmy_nhwc_to_nchw_f32': [I, P, L, P, I, I, I, I, P],
     'dmy_pointwise': [I, I, I, P, P, P, L, F, P],
     'dmy_cast': [I, I, P, P, L, F, P],
@@ -97,7 +100,7 @@ lib = _load()
 
 def call(name, *args):
     rc = getattr(lib, name)(*args)
-    if name.endswith(('partial_rows', 'partial_blocks', '_blocks', '_groups')):
+    if name.endswith(('_rows', '_blocks', '_groups')):
         return rc
     if rc != 0:
         raise RuntimeError(f'{name} failed with hipError {rc}')

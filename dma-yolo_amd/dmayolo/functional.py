@@ -53,13 +53,23 @@ class ConvSpec:
         self.wcache = None
 
 
-def prep_weight(w, dtype, need_t):
+def prep_weight(w, dtype, need_t, Cp=None):
     K, C, KH, KW = w.shape
+    Cp = Cp or C
     wc = w.detach().contiguous()
-    wf = torch.empty((K, KH * KW * C), dtype=dtype, device=w.device)
+    wf = torch.empty((K, KH * KW * Cp), dtype=dtype, device=w.device)
     wt = torch.empty((C, KH * KW * K), dtype=dtype, device=w.device) if need_t else None
-    call('dmy_conv_wprep', DT[dtype], ptr(wc), ptr(wf), ptr(wt), K, C, KH, KW, stream())
+    call('dmy_conv_wprep', DT[dtype], ptr(wc), ptr(wf), ptr(wt), K, C, Cp, KH, KW, stream())
     return wf, wt
+
+
+VW = {torch.float32: 4, torch.bfloat16: 8}
+
+
+def zero_padded_channels(x):
+    """Channel count the storage of `x` is zero-padded to (set by ToNHWC for the 3-channel stem)."""
+    cp = getattr(x, '_dmy_cpad', 0)
+    return cp if cp and cp % VW[x.dtype] == 0 else 0
 
 
 def conv_out_hw(H, W, k, s, p):
@@ -104,10 +114,13 @@ def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, res, spec):
+        cpad = zero_padded_channels(x)
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
         K, C2, k, _ = weight.shape
         assert C2 == C, (C2, C)
+        # stem: read the zero-padded storage as Cp channels (16-byte vectors) with zero weights
+        Cp = cpad if (cpad and C % VW[x.dtype] and xps >= cpad) else C
         s, p = spec.stride, spec.pad
         OH, OW = conv_out_hw(H, W, k, s, p)
         dev, dt = x.device, x.dtype
@@ -116,9 +129,11 @@ class ConvBNActFn(torch.autograd.Function):
                 spec.wcache[0] == (weight.data_ptr(), weight._version, dt):
             wf, wt = spec.wcache[1], None
         else:
-            wf, wt = prep_weight(weight, dt, need_grad)
+            wf, wt = prep_weight(weight, dt, need_grad and Cp == C, Cp)
             if not need_grad:
                 spec.wcache = ((weight.data_ptr(), weight._version, dt), wf)
+        if Cp != C:
+            x = x.as_strided((N, Cp, H, W), x.stride())
         M = N * OH * OW
         z = new_act(N, K, OH, OW, x)
         bn = spec.bn
@@ -133,6 +148,11 @@ class ConvBNActFn(torch.autograd.Function):
                 P = call('dmy_conv_fwd_partial_rows', M, K)
                 psum, psq = f32(P * K, dev), f32(P * K, dev)
                 _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, k, s, p, OH, OW)
+                if P > 256:  # two-stage column reduction of the epilogue partials
+                    S = call('dmy_colsum2_rows', P)
+                    ps2, pq2 = f32(S * K, dev), f32(S * K, dev)
+                    call('dmy_colsum2', ptr(psum), ptr(psq), P, K, ptr(ps2), ptr(pq2), stream())
+                    psum, psq, P = ps2, pq2, S
                 upd = int(bn.training and bn.track_running_stats)
                 mom = bn.momentum if bn.momentum is not None else 0.0
                 call('dmy_bn_finalize', ptr(psum), ptr(psq), P, K, float(M), ptr(bn.weight), ptr(bn.bias),
@@ -159,6 +179,7 @@ class ConvBNActFn(torch.autograd.Function):
             ctx.save_for_backward(x, wt, z)
         ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
+        ctx.cp = Cp
         ctx.has_bias = bias is not None
         return y
 
@@ -176,7 +197,7 @@ class ConvBNActFn(torch.autograd.Function):
             dz = new_act(N, K, OH, OW, z)
             ca, cb, cc = f32(K, dev), f32(K, dev), f32(K, dev)
             if ctx.train_bn:
-                P = call('dmy_bn_partial_rows', M)
+                P = call('dmy_bn_reduce_rows', dt, ptr(z), K, ptr(dy), dps, M, K)
                 pdb, pdg = f32(P * K, dev), f32(P * K, dev)
                 call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
                      spec.act, M, K, ptr(pdb), ptr(pdg), stream())
@@ -202,7 +223,7 @@ class ConvBNActFn(torch.autograd.Function):
             else:
                 dz, dzps = dy, dps
             if ctx.has_bias:
-                P = call('dmy_bn_partial_rows', M)
+                P = call('dmy_bn_reduce_rows', dt, ptr(dz), dzps, None, 0, M, K)
                 ps_, pq_ = f32(P * K, dev), f32(P * K, dev)
                 call('dmy_bn_stats', dt, ptr(dz), dzps, M, K, ptr(ps_), ptr(pq_), stream())
                 dbias = f32(K, dev)
@@ -210,16 +231,19 @@ class ConvBNActFn(torch.autograd.Function):
         if spec.bn is not None and ctx.has_bias and ctx.train_bn:
             dbias = torch.zeros(K, dtype=torch.float32, device=dev)  # sum(dz) == 0 exactly behind train-mode BN
         dx = dw = None
+        Cp = ctx.cp
         if ctx.needs_input_grad[0]:
+            if Cp != C:
+                raise NotImplementedError('input gradient of a channel-padded stem conv')
             dx = new_act(N, C, H, W, z)
             KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(dx), 0,
                             N, H, W, C, C, K, k, k, s, p, OH, OW, dzps, stream())
         if ctx.needs_input_grad[1]:
-            dwo = f32(K * C * k * k, dev)
+            dwo = f32(K * Cp * k * k, dev)
             KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
-                            H, W, C, xps, K, k, k, s, p, OH, OW, dzps, stream())
+                            H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream())
             dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
-            call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, k, k, stream())
+            call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
         dres = dy if ctx.has_res else None
         return dx, dw, dbias, dgamma, dbeta, dres, None
 
@@ -455,20 +479,23 @@ class AddFn(torch.autograd.Function):
 
 
 class ToNHWC(torch.autograd.Function):
-    """NCHW float/uint8 image -> NHWC storage dtype (train.py:402 `/255` when uint8)."""
+    """NCHW float/uint8 image -> NHWC storage dtype (train.py:402 `/255` when uint8).  The pixel
+    stride is rounded up to a 16-byte vector with zero channels so the stem conv stays vectorised."""
 
     @staticmethod
     def forward(ctx, x, dtype):
         N, C, H, W = x.shape
-        y = torch.empty((N, C, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        Cp = -(-C // VW[dtype]) * VW[dtype]
+        buf = torch.empty((N, Cp, H, W), dtype=dtype, device=x.device, memory_format=CL)
         xc = x.contiguous()
         if x.dtype == torch.uint8:
-            call('dmy_nchw_to_nhwc', DT[dtype], 0, ptr(xc), ptr(y), N, C, H, W, 1.0 / 255.0, stream())
+            call('dmy_nchw_to_nhwc', DT[dtype], 0, ptr(xc), ptr(buf), N, C, H, W, Cp, 1.0 / 255.0, stream())
         else:
             xf = xc if x.dtype == torch.float32 else xc.float()
-            call('dmy_nchw_to_nhwc', DT[dtype], 1, ptr(xf), ptr(y), N, C, H, W, 1.0, stream())
+            call('dmy_nchw_to_nhwc', DT[dtype], 1, ptr(xf), ptr(buf), N, C, H, W, Cp, 1.0, stream())
         ctx.src_dtype = x.dtype
-        return y
+        ctx.mark_non_differentiable(buf) if x.dtype == torch.uint8 else None
+        return buf[:, :C] if Cp != C else buf
 
     @staticmethod
     def backward(ctx, dy):

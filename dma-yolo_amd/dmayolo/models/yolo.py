@@ -156,7 +156,9 @@ class Model(nn.Module):
         """uint8/float NCHW image batch -> NHWC act_dtype (train.py:402 `/255` for uint8)."""
         if x.dtype == self.act_dtype and x.dim() == 4 and (x.shape[1] == 1 or x.stride(1) == 1):
             return x
-        return Fn.ToNHWC.apply(x, self.act_dtype)
+        y = Fn.ToNHWC.apply(x, self.act_dtype)
+        y._dmy_cpad = -(-x.shape[1] // Fn.VW[self.act_dtype]) * Fn.VW[self.act_dtype]  # zero-padded channels
+        return y
 
     def _forward_once(self, x, profile=False, visualize=False):
         x = self.to_input(x)

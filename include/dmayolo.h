@@ -31,9 +31,10 @@ int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int 
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
                    int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
-int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int KH, int KW,
+/* Cp >= C: input channels zero-padded to a full 16-byte vector (the 3-channel stem, yaml:15) */
+int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH, int KW,
                    void* stream);
-int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int KH, int KW, void* stream);
+int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int Cp, int KH, int KW, void* stream);
 
 /* ---- BatchNorm2d + activation: replaces nn.BatchNorm2d/nn.SiLU/nn.Hardswish in models/common.py:68-73,
  *      1176-1180, 1284-1306 with utils/torch_utils.py:161-170 eps/momentum. act: 0 none 1 silu 2 hardswish
@@ -58,6 +59,9 @@ int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy, long dp
                      const float* shift, const float* mean, const float* invstd, int act, const float* ca,
                      const float* cb, const float* cc, void* dz, long dzps, long M, int C, void* stream);
 int dmy_reduce_rows(const float* part, int P, int C, float* out, int accumulate, void* stream);
+int dmy_bn_reduce_rows(int dtype, const void* z, long zps, const void* dy, long dps, long M, int C);
+int dmy_colsum2_rows(long P);
+int dmy_colsum2(const float* a, const float* b, long P, int C, float* oa, float* ob, void* stream);
 
 /* ---- memory-bound NHWC ops */
 /* nn.MaxPool2d(k, 1, k//2): SPPF common.py:250-258, SPPFCSPC :1266-1274 */
@@ -95,7 +99,7 @@ int dmy_ca_apply_fwd(int dtype, const void* x, long xps, const void* lh, const v
 int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh, const void* lw, const void* dout, long dps,
                      void* dx, long dxps, void* dlh, void* dlw, int N, int H, int W, int C, void* stream);
 /* input normalisation imgs.float()/255 (train.py:402) + layout changes */
-int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, float scale,
+int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cp, float scale,
                      void* stream);
 int dmy_nhwc_to_nchw_f32(int dtype, const void* x, long xps, float* y, int N, int C, int H, int W, void* stream);
 int dmy_pointwise(int dtype, int op, int act, const void* a, const void* b, void* y, long n, float alpha,
