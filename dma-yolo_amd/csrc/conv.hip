@@ -6,57 +6,119 @@
 //   and nn.Linear in the Swin layers (:452-545, 97-117) as 1x1 convs over tokens.
 //
 // One GEMM core, three operand loaders:
-//   fwd  : C[m=(b,oh,ow)][n=cout]      = sum_k A[m][k=(kh,kw,ci)]   * W[n][k]          (W = OHWI)
-//   dgrad: C[m=(b,ih,iw)][n=ci]        = sum_k dY[m'(m,kh,kw)][co]  * Wt[n][k=(kh,kw,co)] (Wt = IHWO)
-//   wgrad: C[m=cout][n=(kh,kw,ci)]     = sum_pix dY[pix][m] * X[pix shifted][ci]        (split-K over pixels)
-// Tiles are staged global -> registers -> LDS ([row][k] with k contiguous, rows padded so the
-// MFMA fragment reads are bank-conflict free), double-buffered with one barrier per K-step.
+//   fwd  : C[m=(b,oh,ow)][n=cout]  = sum_k A[m][k=(kh,kw,ci)]  * W[n][k]            W  = OHWI
+//   dgrad: C[m=(b,ih,iw)][n=ci]    = sum_k dY[m'(m,kh,kw)][co] * Wt[n][k=(kh,kw,co)] Wt = IHWO
+//          stride-2 layers are split into the 4 output-parity classes so only live taps are
+//          multiplied (sub-pixel decomposition; 4x less MFMA work for 3x3/s2).
+//   wgrad: C[m=cout][n=(kh,kw,ci)] = sum_pix dY[pix][m] * X[pix shifted][ci]       split-K over pixels
+// Staging: global -> registers -> LDS, two stages, one barrier per BK-deep step (BK = 64 bf16 / 32 f32).
+//   "m-major" tiles ([row][k], k contiguous, 16-B row pad => conflict-free ds_read_b128 fragments);
+//   "k-major" tiles ([k][row], as loaded from NHWC; wgrad) are read with ds_read_b64_tr_b16, the
+//   16-B chunks XOR-swizzled per k-row so the transposed reads are bank-conflict free.
+// Epilogues go through LDS so every global store / atomic is a 16-B vector or a 256-B wave segment.
 // MFMA: bf16 -> v_mfma_f32_16x16x32_bf16, f32 -> v_mfma_f32_16x16x4_f32 (exact fp32, parity mode).
+// Block ids are remapped so consecutive tiles sharing an A panel land on one XCD (L2 reuse).
 #include "common.h"
 
 namespace {
 
-constexpr int BK = 32;
 constexpr int NT = 256;  // 4 waves, 2x2 over the block tile
 
-template <typename T> struct LdsCfg;
-template <> struct LdsCfg<bf16> { static constexpr int RS = BK + 8; };   // 80-B rows: conflict-free b128 reads
-template <> struct LdsCfg<float> { static constexpr int RS = BK + 4; };  // 144-B rows
-
-template <typename T, int BM, int BN> struct Tile {
-  static constexpr int RS = LdsCfg<T>::RS;
-  static constexpr int VW = Traits<T>::VW;
-  static constexpr int STAGE = (BM + BN) * RS;  // elements per pipeline stage
-  static constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 fragments per wave
+template <typename T> struct Cfg;
+template <> struct Cfg<bf16> {
+  static constexpr int BK = 64, PADM = 8, PADK = 0;  // m-major rows 144 B; k-major rows unpadded (swizzled)
+};
+template <> struct Cfg<float> {
+  static constexpr int BK = 32, PADM = 4, PADK = 16;
 };
 
-// ---------------------------------------------------------------- MFMA over one staged K-step
-template <int BM, int BN>
-DEV void mma_step(const bf16* As, const bf16* Bs, f32x4 (&acc)[BM / 32][BN / 32], int wm, int wn, int lane) {
-  constexpr int RS = LdsCfg<bf16>::RS, TM = BM / 32, TN = BN / 32;
-  bf16x8 a[TM], b[TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-    a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * (BM / 2) + i * 16 + (lane & 15)) * RS + 8 * (lane >> 4));
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-    b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * (BN / 2) + j * 16 + (lane & 15)) * RS + 8 * (lane >> 4));
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+template <typename T, int BM, int BN, bool AK, bool BKM> struct Tile {
+  static constexpr int BK = Cfg<T>::BK, VW = Traits<T>::VW;
+  static constexpr int RSM = BK + Cfg<T>::PADM;  // m-major row stride (elements)
+  static constexpr int A_ELEMS = AK ? BK * (BM + Cfg<T>::PADK) : BM * RSM;
+  static constexpr int B_ELEMS = BKM ? BK * (BN + Cfg<T>::PADK) : BN * RSM;
+  static constexpr int STAGE = A_ELEMS + B_ELEMS;
+  static constexpr int TM = BM / 32, TN = BN / 32;
+  static constexpr int STAGE_BYTES = 2 * STAGE * (int)sizeof(T);
+  static constexpr int CT_BYTES = BM * (BN + 8) * 4;  // C tile (largest epilogue use, fp32 worst case)
+  static constexpr int LDS_BYTES = STAGE_BYTES > CT_BYTES ? STAGE_BYTES : CT_BYTES;
+};
+
+// ---------------------------------------------------------------- LDS placement helpers
+// k-major tile [k][ROW] with ROW = BM (or BN) elements; bf16 16-B chunks XOR-swizzled per k-row
+template <typename T, int ROW> DEV int kmaj_off(int k, int row) {
+  if constexpr (sizeof(T) == 2) {
+    constexpr int RB = ROW * 2;  // bytes per k-row
+    const int c = row >> 3, w = row & 7;
+    int key;
+    if constexpr (RB >= 256) key = 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+    else key = 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+    return k * ROW + (((c ^ key) & (ROW / 8 - 1)) << 3) + w;
+  } else {
+    return k * (ROW + Cfg<float>::PADK) + row;
+  }
 }
 
-template <int BM, int BN>
-DEV void mma_step(const float* As, const float* Bs, f32x4 (&acc)[BM / 32][BN / 32], int wm, int wn, int lane) {
-  constexpr int RS = LdsCfg<float>::RS, TM = BM / 32, TN = BN / 32;
+// ---------------------------------------------------------------- fragment reads + MFMA
+// bf16: A frag lane l = A[m0 + (l&15)][8(l>>4) .. +8)
+template <int RSM> DEV bf16x8 frag_m(const bf16* base, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(base + (r0 + (lane & 15)) * RSM + k0 + 8 * (lane >> 4));
+}
+template <int ROW> DEV bf16x8 frag_k(const bf16* base, int r0, int k0, int lane) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3;
+  const bf16* a0 = base + kmaj_off<bf16, ROW>(k0 + 8 * g + q, r0 + 4 * p);
+  const bf16* a1 = base + kmaj_off<bf16, ROW>(k0 + 8 * g + 4 + q, r0 + 4 * p);
+  s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+  s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a1));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int BM, int BN, bool AK, bool BKM>
+DEV void mma_step(const bf16* As, const bf16* Bs, f32x4 (&acc)[BM / 32][BN / 32], int wm, int wn, int lane) {
+  using TT = Tile<bf16, BM, BN, AK, BKM>;
+  constexpr int TM = TT::TM, TN = TT::TN;
 #pragma unroll
-  for (int kk = 0; kk < BK / 4; ++kk) {
+  for (int ks = 0; ks < TT::BK; ks += 32) {
+    bf16x8 a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r0 = wm * (BM / 2) + i * 16;
+      a[i] = AK ? frag_k<BM>(As, r0, ks, lane) : frag_m<TT::RSM>(As, r0, ks, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r0 = wn * (BN / 2) + j * 16;
+      b[j] = BKM ? frag_k<BN>(Bs, r0, ks, lane) : frag_m<TT::RSM>(Bs, r0, ks, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKM>
+DEV void mma_step(const float* As, const float* Bs, f32x4 (&acc)[BM / 32][BN / 32], int wm, int wn, int lane) {
+  using TT = Tile<float, BM, BN, AK, BKM>;
+  constexpr int TM = TT::TM, TN = TT::TN;
+#pragma unroll
+  for (int kk = 0; kk < TT::BK / 4; ++kk) {
+    const int k = 4 * kk + (lane >> 4);
     float a[TM], b[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = As[(wm * (BM / 2) + i * 16 + (lane & 15)) * RS + 4 * kk + (lane >> 4)];
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * (BM / 2) + i * 16 + (lane & 15);
+      a[i] = AK ? As[kmaj_off<float, BM>(k, r)] : As[r * TT::RSM + k];
+    }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) b[j] = Bs[(wn * (BN / 2) + j * 16 + (lane & 15)) * RS + 4 * kk + (lane >> 4)];
+    for (int j = 0; j < TN; ++j) {
+      const int r = wn * (BN / 2) + j * 16 + (lane & 15);
+      b[j] = BKM ? Bs[kmaj_off<float, BN>(k, r)] : Bs[r * TT::RSM + k];
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -64,12 +126,12 @@ DEV void mma_step(const float* As, const float* Bs, f32x4 (&acc)[BM / 32][BN / 3
   }
 }
 
-// ---------------------------------------------------------------- generic pipelined main loop
-// Loader contract:  load(kt, ra, rb) issues global loads for K-tile kt into registers;
-//                   store(As, Bs, ra, rb) writes them into one LDS stage.
-template <typename T, int BM, int BN, class L>
+// ---------------------------------------------------------------- pipelined main loop
+// Loader contract: load(kt, ra, rb) issues the global loads of K-tile kt into registers;
+//                  store(As, Bs, ra, rb) writes them into one LDS stage.
+template <typename T, int BM, int BN, bool AK, bool BKM, class L>
 DEV void mainloop(L& ld, int kt0, int kt1, T* lds, f32x4 (&acc)[BM / 32][BN / 32]) {
-  using TT = Tile<T, BM, BN>;
+  using TT = Tile<T, BM, BN, AK, BKM>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   uint4 ra[L::CA], rb[L::CB];
@@ -78,55 +140,70 @@ DEV void mainloop(L& ld, int kt0, int kt1, T* lds, f32x4 (&acc)[BM / 32][BN / 32
   int buf = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     T* As = lds + buf * TT::STAGE;
-    T* Bs = As + BM * TT::RS;
+    T* Bs = As + TT::A_ELEMS;
     ld.store(As, Bs, ra, rb);
     __syncthreads();
     if (kt + 1 < kt1) ld.load(kt + 1, ra, rb);
-    mma_step<BM, BN>(As, Bs, acc, wm, wn, lane);
+    mma_step<BM, BN, AK, BKM>(As, Bs, acc, wm, wn, lane);
     buf ^= 1;
   }
 }
 
-// row-major [row][k] vector store into LDS
-template <typename T, int RS> DEV void st_vec(T* base, int row, int col, const uint4& v) {
-  *reinterpret_cast<uint4*>(base + row * RS + col) = v;
+template <typename T, int RSM> DEV void st_m(T* base, int row, int col, const uint4& v) {
+  *reinterpret_cast<uint4*>(base + row * RSM + col) = v;
 }
-// transposed store: element e of the vector goes to [row0+e][col]
-template <typename T, int RS> DEV void st_tr(T* base, int row0, int col, const uint4& v) {
-  const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-  for (int i = 0; i < Traits<T>::VW; ++i) base[(row0 + i) * RS + col] = e[i];
+template <typename T, int ROW> DEV void st_k(T* base, int k, int row0, const uint4& v) {
+  *reinterpret_cast<uint4*>(base + kmaj_off<T, ROW>(k, row0)) = v;
 }
 
 struct Geom {
-  int N, H, W, C;      // input activation (forward sense)
+  int N, H, W, C;       // input activation (forward sense)
   int K, KH, KW, S, P;  // out channels, kernel, stride, pad
   int OH, OW;           // output spatial
   long xps, yps;        // pixel strides of x and y (elements)
 };
 
-// ---------------------------------------------------------------- forward loader
+// parity class of a stride-2 data-grad (blockIdx.y): output pixels with (ih%2, iw%2) == (a, b)
+struct Parity {
+  int a, b;      // parities
+  int kh0, kw0;  // first live tap ( (a + P) & 1 )
+  int nkh, nkw;  // live taps per dim
+  int Hc, Wc;    // pixels of this class per image (rows / cols)
+};
+DEV Parity parity_class(const Geom& g, int cls) {
+  Parity q;
+  q.a = cls >> 1;
+  q.b = cls & 1;
+  q.kh0 = (q.a + g.P) & 1;
+  q.kw0 = (q.b + g.P) & 1;
+  q.nkh = (g.KH - q.kh0 + 1) / 2;
+  q.nkw = (g.KW - q.kw0 + 1) / 2;
+  q.Hc = (g.H - q.a + 1) / 2;
+  q.Wc = (g.W - q.b + 1) / 2;
+  return q;
+}
+
+// ---------------------------------------------------------------- forward loader (m-major A and B)
 template <typename T, int BM, int BN, bool VEC, bool P1> struct FwdLoader {
-  using TT = Tile<T, BM, BN>;
-  static constexpr int VW = TT::VW, KV = BK / VW, RPP = NT / KV;  // rows per pass
+  using TT = Tile<T, BM, BN, false, false>;
+  static constexpr int BK = TT::BK, VW = TT::VW, KV = BK / VW, RPP = NT / KV;
   static constexpr int CA = BM / RPP, CB = BN / RPP;
   const T* x; const T* w; Geom g; long M; int Ktot;
-  int kc, r0;
+  int kc, r0, n0;
   long abase[CA]; int ih0[CA], iw0[CA]; bool aval[CA];
-  int n0;
   DEV FwdLoader(const T* x_, const T* w_, const Geom& g_, long M_, long m0, int n0_) : x(x_), w(w_), g(g_), M(M_), n0(n0_) {
     Ktot = g.KH * g.KW * g.C;
     kc = threadIdx.x % KV;
     r0 = threadIdx.x / KV;
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      long m = m0 + r0 + i * RPP;
+      const long m = m0 + r0 + i * RPP;
       aval[i] = m < M;
-      long mm = aval[i] ? m : 0;
-      int ow = (int)(mm % g.OW);
-      long t = mm / g.OW;
-      int oh = (int)(t % g.OH);
-      int b = (int)(t / g.OH);
+      const long mm = aval[i] ? m : 0;
+      const int ow = (int)(mm % g.OW);
+      const long t = mm / g.OW;
+      const int oh = (int)(t % g.OH);
+      const int b = (int)(t / g.OH);
       if (P1) { abase[i] = mm * g.xps; ih0[i] = 0; iw0[i] = 0; }
       else { abase[i] = (long)b * g.H * g.W * g.xps; ih0[i] = oh * g.S - g.P; iw0[i] = ow * g.S - g.P; }
     }
@@ -134,13 +211,20 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct FwdLoader {
   DEV T ld_a1(int i, int k) const {
     if (!aval[i] || k >= Ktot) return from_f<T>(0.f);
     if (P1) return x[abase[i] + k];
-    int ci = k % g.C, t = k / g.C, kw = t % g.KW, kh = t / g.KW;
-    int ih = ih0[i] + kh, iw = iw0[i] + kw;
+    const int ci = k % g.C, t = k / g.C, kw = t % g.KW, kh = t / g.KW;
+    const int ih = ih0[i] + kh, iw = iw0[i] + kw;
     if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return from_f<T>(0.f);
     return x[abase[i] + ((long)ih * g.W + iw) * g.xps + ci];
   }
   DEV void load(int kt, uint4* ra, uint4* rb) const {
     const int k = kt * BK + kc * VW;
+    int ci = 0, kh = 0, kw = 0;
+    if (!P1) {
+      ci = k % g.C;
+      const int t = k / g.C;
+      kw = t % g.KW;
+      kh = t / g.KW;
+    }
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
       if (VEC) {
@@ -148,8 +232,7 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct FwdLoader {
         if (aval[i] && k < Ktot) {
           if (P1) v = *reinterpret_cast<const uint4*>(x + abase[i] + k);
           else {
-            int ci = k % g.C, t = k / g.C, kw = t % g.KW, kh = t / g.KW;
-            int ih = ih0[i] + kh, iw = iw0[i] + kw;
+            const int ih = ih0[i] + kh, iw = iw0[i] + kw;
             if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
               v = *reinterpret_cast<const uint4*>(x + abase[i] + ((long)ih * g.W + iw) * g.xps + ci);
           }
@@ -163,7 +246,7 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct FwdLoader {
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      int n = n0 + r0 + i * RPP;
+      const int n = n0 + r0 + i * RPP;
       if (VEC) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (n < g.K && k < Ktot) v = *reinterpret_cast<const uint4*>(w + (long)n * Ktot + k);
@@ -177,49 +260,74 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct FwdLoader {
   }
   DEV void store(T* As, T* Bs, const uint4* ra, const uint4* rb) const {
 #pragma unroll
-    for (int i = 0; i < CA; ++i) st_vec<T, TT::RS>(As, r0 + i * RPP, kc * VW, ra[i]);
+    for (int i = 0; i < CA; ++i) st_m<T, TT::RSM>(As, r0 + i * RPP, kc * VW, ra[i]);
 #pragma unroll
-    for (int i = 0; i < CB; ++i) st_vec<T, TT::RS>(Bs, r0 + i * RPP, kc * VW, rb[i]);
+    for (int i = 0; i < CB; ++i) st_m<T, TT::RSM>(Bs, r0 + i * RPP, kc * VW, rb[i]);
   }
 };
 
-// ---------------------------------------------------------------- data-grad loader
-// A[m=(b,ih,iw)][k=(kh,kw,co)] = dy[b, (ih+P-kh)/S, (iw+P-kw)/S, co] when divisible and in range.
-template <typename T, int BM, int BN, bool VEC, bool P1> struct DgradLoader {
-  using TT = Tile<T, BM, BN>;
-  static constexpr int VW = TT::VW, KV = BK / VW, RPP = NT / KV;
+// ---------------------------------------------------------------- data-grad loader (m-major)
+// S2: stride-2 parity class; m enumerates the class pixels, k = (live kh, live kw, co)
+template <typename T, int BM, int BN, bool VEC, bool P1, bool S2> struct DgradLoader {
+  using TT = Tile<T, BM, BN, false, false>;
+  static constexpr int BK = TT::BK, VW = TT::VW, KV = BK / VW, RPP = NT / KV;
   static constexpr int CA = BM / RPP, CB = BN / RPP;
-  const T* dy; const T* wt; Geom g; long M; int Ktot;
-  int kc, r0, n0;
+  const T* dy; const T* wt; Geom g; Parity q; long M; int Ktot, kc, r0, n0;
   long abase[CA]; int ih[CA], iw[CA]; bool aval[CA];
-  DEV DgradLoader(const T* dy_, const T* wt_, const Geom& g_, long M_, long m0, int n0_) : dy(dy_), wt(wt_), g(g_), M(M_), n0(n0_) {
-    Ktot = g.KH * g.KW * g.K;
+  DEV DgradLoader(const T* dy_, const T* wt_, const Geom& g_, const Parity& q_, long M_, long m0, int n0_)
+      : dy(dy_), wt(wt_), g(g_), q(q_), M(M_), n0(n0_) {
+    Ktot = S2 ? q.nkh * q.nkw * g.K : g.KH * g.KW * g.K;
     kc = threadIdx.x % KV;
     r0 = threadIdx.x / KV;
+    const int Hm = S2 ? q.Hc : g.H, Wm = S2 ? q.Wc : g.W;
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      long m = m0 + r0 + i * RPP;
+      const long m = m0 + r0 + i * RPP;
       aval[i] = m < M;
-      long mm = aval[i] ? m : 0;
-      iw[i] = (int)(mm % g.W);
-      long t = mm / g.W;
-      ih[i] = (int)(t % g.H);
-      int b = (int)(t / g.H);
+      const long mm = aval[i] ? m : 0;
+      const int x_ = (int)(mm % Wm);
+      const long t = mm / Wm;
+      const int y_ = (int)(t % Hm);
+      const int b = (int)(t / Hm);
+      ih[i] = S2 ? 2 * y_ + q.a : y_;
+      iw[i] = S2 ? 2 * x_ + q.b : x_;
       abase[i] = P1 ? mm * g.yps : (long)b * g.OH * g.OW * g.yps;
     }
+  }
+  // tap index t (row-major over the (live) taps) -> kernel (kh, kw)
+  DEV void tap(int t, int& kh, int& kw) const {
+    if (S2) { kh = q.kh0 + 2 * (t / q.nkw); kw = q.kw0 + 2 * (t % q.nkw); }
+    else { kh = t / g.KW; kw = t % g.KW; }
+  }
+  DEV bool src(int i, int kh, int kw, long& off) const {
+    const int hn = ih[i] + g.P - kh, wn = iw[i] + g.P - kw;
+    if (hn < 0 || wn < 0) return false;
+    if (!S2 && g.S > 1 && ((hn % g.S) || (wn % g.S))) return false;
+    const int oh = S2 ? (hn >> 1) : hn / g.S, ow = S2 ? (wn >> 1) : wn / g.S;
+    if (oh >= g.OH || ow >= g.OW) return false;
+    off = abase[i] + ((long)oh * g.OW + ow) * g.yps;
+    return true;
   }
   DEV T ld_a1(int i, int k) const {
     if (!aval[i] || k >= Ktot) return from_f<T>(0.f);
     if (P1) return dy[abase[i] + k];
-    int co = k % g.K, t = k / g.K, kw = t % g.KW, kh = t / g.KW;
-    int hn = ih[i] + g.P - kh, wn = iw[i] + g.P - kw;
-    if (hn < 0 || wn < 0 || hn % g.S || wn % g.S) return from_f<T>(0.f);
-    int oh = hn / g.S, ow = wn / g.S;
-    if (oh >= g.OH || ow >= g.OW) return from_f<T>(0.f);
-    return dy[abase[i] + ((long)oh * g.OW + ow) * g.yps + co];
+    int kh, kw;
+    tap(k / g.K, kh, kw);
+    long off;
+    return src(i, kh, kw, off) ? dy[off + k % g.K] : from_f<T>(0.f);
+  }
+  DEV T ld_b1(int n, int k) const {
+    if (n >= g.C || k >= Ktot) return from_f<T>(0.f);
+    if (!S2) return wt[(long)n * Ktot + k];
+    int kh, kw;
+    tap(k / g.K, kh, kw);
+    return wt[(((long)n * g.KH + kh) * g.KW + kw) * g.K + k % g.K];
   }
   DEV void load(int kt, uint4* ra, uint4* rb) const {
     const int k = kt * BK + kc * VW;
+    const int co = k % g.K;
+    int kh = 0, kw = 0;
+    if (!P1) tap(k / g.K, kh, kw);
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
       if (VEC) {
@@ -227,13 +335,8 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct DgradLoader {
         if (aval[i] && k < Ktot) {
           if (P1) v = *reinterpret_cast<const uint4*>(dy + abase[i] + k);
           else {
-            int co = k % g.K, t = k / g.K, kw = t % g.KW, kh = t / g.KW;
-            int hn = ih[i] + g.P - kh, wn = iw[i] + g.P - kw;
-            if (hn >= 0 && wn >= 0 && (hn % g.S) == 0 && (wn % g.S) == 0) {
-              int oh = hn / g.S, ow = wn / g.S;
-              if (oh < g.OH && ow < g.OW)
-                v = *reinterpret_cast<const uint4*>(dy + abase[i] + ((long)oh * g.OW + ow) * g.yps + co);
-            }
+            long off;
+            if (src(i, kh, kw, off)) v = *reinterpret_cast<const uint4*>(dy + off + co);
           }
         }
         ra[i] = v;
@@ -245,56 +348,70 @@ template <typename T, int BM, int BN, bool VEC, bool P1> struct DgradLoader {
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      int n = n0 + r0 + i * RPP;
+      const int n = n0 + r0 + i * RPP;
       if (VEC) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (n < g.C && k < Ktot) v = *reinterpret_cast<const uint4*>(wt + (long)n * Ktot + k);
+        if (n < g.C && k < Ktot) {
+          const long wo = S2 ? (((long)n * g.KH + kh) * g.KW + kw) * g.K + co : (long)n * Ktot + k;
+          v = *reinterpret_cast<const uint4*>(wt + wo);
+        }
         rb[i] = v;
       } else {
         T* e = reinterpret_cast<T*>(&rb[i]);
 #pragma unroll
-        for (int j = 0; j < VW; ++j) e[j] = (n < g.C && k + j < Ktot) ? wt[(long)n * Ktot + k + j] : from_f<T>(0.f);
+        for (int j = 0; j < VW; ++j) e[j] = ld_b1(n, k + j);
       }
     }
   }
   DEV void store(T* As, T* Bs, const uint4* ra, const uint4* rb) const {
 #pragma unroll
-    for (int i = 0; i < CA; ++i) st_vec<T, TT::RS>(As, r0 + i * RPP, kc * VW, ra[i]);
+    for (int i = 0; i < CA; ++i) st_m<T, TT::RSM>(As, r0 + i * RPP, kc * VW, ra[i]);
 #pragma unroll
-    for (int i = 0; i < CB; ++i) st_vec<T, TT::RS>(Bs, r0 + i * RPP, kc * VW, rb[i]);
+    for (int i = 0; i < CB; ++i) st_m<T, TT::RSM>(Bs, r0 + i * RPP, kc * VW, rb[i]);
   }
 };
 
-// ---------------------------------------------------------------- weight-grad loader
-// GEMM over pixels: A[m=co][pix] = dy[pix][co]; B[n=(kh,kw,ci)][pix] = x[pix shifted by (kh,kw)][ci].
-// Global loads are coalesced along channels; the LDS stores transpose into [row][pix].
+// ---------------------------------------------------------------- weight-grad loader (k-major A and B)
+// A[k=pix][m=co] = dy[pix][co];  B[k=pix][n=(kh,kw,ci)] = x[pix shifted by (kh,kw)][ci]
 template <typename T, int BM, int BN, bool VECA, bool VECB> struct WgradLoader {
-  using TT = Tile<T, BM, BN>;
-  static constexpr int VW = TT::VW;
+  using TT = Tile<T, BM, BN, true, true>;
+  static constexpr int BK = TT::BK, VW = TT::VW;
   static constexpr int AV = BM / VW, BV = BN / VW;  // vectors per pixel row
   static constexpr int CA = BK * AV / NT, CB = BK * BV / NT;
   const T* x; const T* dy; Geom g; long NP; int Ntot, m0, n0;
+  // the n -> (kh, kw, ci) decomposition is fixed per thread across K-steps
+  int b_kh[CB], b_kw[CB], b_ci[CB];
+  bool b_ok[CB];
   DEV WgradLoader(const T* x_, const T* dy_, const Geom& g_, int m0_, int n0_) : x(x_), dy(dy_), g(g_), m0(m0_), n0(n0_) {
     NP = (long)g.N * g.OH * g.OW;
     Ntot = g.KH * g.KW * g.C;
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int n = n0 + (c % BV) * VW;
+      b_ok[i] = n < Ntot;
+      b_ci[i] = n % g.C;
+      const int u = n / g.C;
+      b_kw[i] = u % g.KW;
+      b_kh[i] = u / g.KW;
+    }
   }
   DEV T ld_b1(long pix, int n) const {
     if (pix >= NP || n >= Ntot) return from_f<T>(0.f);
-    int ow = (int)(pix % g.OW);
-    long t = pix / g.OW;
-    int oh = (int)(t % g.OH), b = (int)(t / g.OH);
-    int ci = n % g.C, u = n / g.C, kw = u % g.KW, kh = u / g.KW;
-    int ih = oh * g.S - g.P + kh, iw = ow * g.S - g.P + kw;
+    const int ow = (int)(pix % g.OW);
+    const long t = pix / g.OW;
+    const int oh = (int)(t % g.OH), b = (int)(t / g.OH);
+    const int ci = n % g.C, u = n / g.C, kw = u % g.KW, kh = u / g.KW;
+    const int ih = oh * g.S - g.P + kh, iw = ow * g.S - g.P + kw;
     if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return from_f<T>(0.f);
     return x[(((long)b * g.H + ih) * g.W + iw) * g.xps + ci];
   }
   DEV void load(int kt, uint4* ra, uint4* rb) const {
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      int c = threadIdx.x + i * NT;
-      int pl = c / AV, cv = c % AV;
-      long pix = (long)kt * BK + pl;
-      int co = m0 + cv * VW;
+      const int c = threadIdx.x + i * NT;
+      const long pix = (long)kt * BK + c / AV;
+      const int co = m0 + (c % AV) * VW;
       if (VECA) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (pix < NP && co < g.K) v = *reinterpret_cast<const uint4*>(dy + pix * g.yps + co);
@@ -307,24 +424,22 @@ template <typename T, int BM, int BN, bool VECA, bool VECB> struct WgradLoader {
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      int c = threadIdx.x + i * NT;
-      int pl = c / BV, nv = c % BV;
-      long pix = (long)kt * BK + pl;
-      int n = n0 + nv * VW;
+      const int c = threadIdx.x + i * NT;
+      const long pix = (long)kt * BK + c / BV;
       if (VECB) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (pix < NP && n < Ntot) {
-          int ow = (int)(pix % g.OW);
-          long t = pix / g.OW;
-          int oh = (int)(t % g.OH), b = (int)(t / g.OH);
-          int ci = n % g.C, u = n / g.C, kw = u % g.KW, kh = u / g.KW;
-          int ih = oh * g.S - g.P + kh, iw = ow * g.S - g.P + kw;
+        if (pix < NP && b_ok[i]) {
+          const int ow = (int)(pix % g.OW);
+          const long t = pix / g.OW;
+          const int oh = (int)(t % g.OH), b = (int)(t / g.OH);
+          const int ih = oh * g.S - g.P + b_kh[i], iw = ow * g.S - g.P + b_kw[i];
           if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-            v = *reinterpret_cast<const uint4*>(x + (((long)b * g.H + ih) * g.W + iw) * g.xps + ci);
+            v = *reinterpret_cast<const uint4*>(x + (((long)b * g.H + ih) * g.W + iw) * g.xps + b_ci[i]);
         }
         rb[i] = v;
       } else {
         T* e = reinterpret_cast<T*>(&rb[i]);
+        const int n = n0 + (c % BV) * VW;
 #pragma unroll
         for (int j = 0; j < VW; ++j) e[j] = ld_b1(pix, n + j);
       }
@@ -333,133 +448,213 @@ template <typename T, int BM, int BN, bool VECA, bool VECB> struct WgradLoader {
   DEV void store(T* As, T* Bs, const uint4* ra, const uint4* rb) const {
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      int c = threadIdx.x + i * NT;
-      st_tr<T, TT::RS>(As, (c % AV) * VW, c / AV, ra[i]);
+      const int c = threadIdx.x + i * NT;
+      st_k<T, BM>(As, c / AV, (c % AV) * VW, ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      int c = threadIdx.x + i * NT;
-      st_tr<T, TT::RS>(Bs, (c % BV) * VW, c / BV, rb[i]);
+      const int c = threadIdx.x + i * NT;
+      st_k<T, BN>(Bs, c / BV, (c % BV) * VW, rb[i]);
     }
   }
 };
+
+// ---------------------------------------------------------------- XCD-aware tile order
+// Linear block id -> logical tile id such that each XCD (block id mod 8 under round-robin
+// dispatch) walks a contiguous range of logical tiles; n-tiles of one m-panel are adjacent.
+// Speed only: any placement is correct.  Bijective for every grid size.
+DEV int xcd_remap(int id, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = id % 8, loc = id / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+template <int BM, int BN> DEV void zero_acc(f32x4 (&acc)[BM / 32][BN / 32]) {
+#pragma unroll
+  for (int i = 0; i < BM / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < BN / 32; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Write the accumulator tile (+bias) as T into LDS [BM][BN+8] (row-major) and return per-column
+// sums / sums of squares of the fp32 values (rows < M) for the BN statistics.
+template <typename T, int BM, int BN>
+DEV void acc_to_lds(const f32x4 (&acc)[BM / 32][BN / 32], T* ct, const float* bias, int n0, int K, long m0, long M,
+                    float* s1, float* s2) {
+  constexpr int RS = BN + 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+#pragma unroll
+  for (int j = 0; j < BN / 32; ++j) {
+    const int c = wn * (BN / 2) + j * 16 + (lane & 15);
+    const float bv = (bias != nullptr && n0 + c < K) ? bias[n0 + c] : 0.f;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
+        const float v = acc[i][j][r] + bv;
+        ct[row * RS + c] = from_f<T>(v);
+        if (m0 + row < M) {
+          a += v;
+          b += v * v;
+        }
+      }
+    s1[j] = a;
+    s2[j] = b;
+  }
+}
 
 // ---------------------------------------------------------------- kernels
 template <typename T, int BM, int BN, bool VEC, bool P1>
 __global__ void __launch_bounds__(NT) conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                       const float* __restrict__ bias, T* __restrict__ y,
-                                                      float* __restrict__ psum, float* __restrict__ psq, Geom g) {
-  using TT = Tile<T, BM, BN>;
-  __shared__ __attribute__((aligned(16))) T lds[2 * TT::STAGE];
+                                                      float* __restrict__ psum, float* __restrict__ psq, Geom g,
+                                                      int gm, int gn) {
+  using TT = Tile<T, BM, BN, false, false>;
+  __shared__ __attribute__((aligned(16))) char smem[TT::LDS_BYTES];
+  T* lds = reinterpret_cast<T*>(smem);
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
   const long M = (long)g.N * g.OH * g.OW;
-  const long m0 = (long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
   FwdLoader<T, BM, BN, VEC, P1> ld(x, w, g, M, m0, n0);
   f32x4 acc[TT::TM][TT::TN];
-#pragma unroll
-  for (int i = 0; i < TT::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TT::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
-  mainloop<T, BM, BN>(ld, 0, nk, lds, acc);
-
+  zero_acc<BM, BN>(acc);
+  const int nk = (g.KH * g.KW * g.C + TT::BK - 1) / TT::BK;
+  mainloop<T, BM, BN, false, false>(ld, 0, nk, lds, acc);
+  __syncthreads();
+  float s1[TT::TN], s2[TT::TN];
+  acc_to_lds<T, BM, BN>(acc, lds, bias, n0, g.K, m0, M, s1, s2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  if (psum != nullptr) {
 #pragma unroll
-  for (int j = 0; j < TT::TN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-    const float bv = (bias != nullptr && n < g.K) ? bias[n] : 0.f;
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < TT::TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
-        float v = acc[i][j][r] + bv;
-        if (m < M && n < g.K) {
-          y[m * g.yps + n] = from_f<T>(v);
-          s1 += v;
-          s2 += v * v;
-        }
+    for (int j = 0; j < TT::TN; ++j) {
+      float a = s1[j], b = s2[j];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+      if (lane < 16 && n < g.K) {
+        const long row = (long)tm * 2 + wm;
+        psum[row * g.K + n] = a;
+        psq[row * g.K + n] = b;
       }
     }
-    if (psum != nullptr) {
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 16 && n < g.K) {
-        const long row = (long)blockIdx.x * 2 + wm;
-        psum[row * g.K + n] = s1;
-        psq[row * g.K + n] = s2;
-      }
+  }
+  __syncthreads();
+  // coalesced 16-B stores of the staged tile
+  constexpr int VW = TT::VW, RS = BN + 8, CPR = BN / VW;
+  const bool vec = (g.yps % VW) == 0 && (g.K % VW) == 0 && ((((uintptr_t)y) & 15) == 0);
+  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+    const int row = e / CPR, cv = e % CPR;
+    const long m = m0 + row;
+    const int n = n0 + cv * VW;
+    if (m >= M || n >= g.K) continue;
+    const T* src = lds + row * RS + cv * VW;
+    if (vec && n + VW <= g.K) {
+      *reinterpret_cast<uint4*>(y + m * g.yps + n) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      for (int j = 0; j < VW && n + j < g.K; ++j) y[m * g.yps + n + j] = src[j];
     }
   }
 }
 
-template <typename T, int BM, int BN, bool VEC, bool P1>
+template <typename T, int BM, int BN, bool VEC, bool P1, bool S2>
 __global__ void __launch_bounds__(NT) conv_dgrad_kernel(const T* __restrict__ dy, const T* __restrict__ wt,
-                                                        T* __restrict__ dx, int accumulate, Geom g) {
-  using TT = Tile<T, BM, BN>;
-  __shared__ __attribute__((aligned(16))) T lds[2 * TT::STAGE];
-  const long M = (long)g.N * g.H * g.W;
-  const long m0 = (long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  DgradLoader<T, BM, BN, VEC, P1> ld(dy, wt, g, M, m0, n0);
+                                                        T* __restrict__ dx, int accumulate, Geom g, int gm, int gn) {
+  using TT = Tile<T, BM, BN, false, false>;
+  __shared__ __attribute__((aligned(16))) char smem[TT::LDS_BYTES];
+  T* lds = reinterpret_cast<T*>(smem);
+  const Parity q = parity_class(g, S2 ? (int)blockIdx.y : 0);
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = S2 ? (long)g.N * q.Hc * q.Wc : (long)g.N * g.H * g.W;
+  const long m0 = (long)tm * BM;
+  if (m0 >= M) return;  // a parity class can be smaller than the grid's M extent (block-uniform exit)
+  const int n0 = tn * BN;
+  DgradLoader<T, BM, BN, VEC, P1, S2> ld(dy, wt, g, q, M, m0, n0);
   f32x4 acc[TT::TM][TT::TN];
+  zero_acc<BM, BN>(acc);
+  const int Ktot = S2 ? q.nkh * q.nkw * g.K : g.KH * g.KW * g.K;
+  const int nk = (Ktot + TT::BK - 1) / TT::BK;
+  mainloop<T, BM, BN, false, false>(ld, 0, nk, lds, acc);
+  __syncthreads();
+  float s1[TT::TN], s2[TT::TN];
+  acc_to_lds<T, BM, BN>(acc, lds, nullptr, n0, g.C, m0, M, s1, s2);
+  __syncthreads();
+  constexpr int VW = TT::VW, RS = BN + 8, CPR = BN / VW;
+  const bool vec = (g.xps % VW) == 0 && (g.C % VW) == 0 && ((((uintptr_t)dx) & 15) == 0);
+  const int Wm = S2 ? q.Wc : g.W, Hm = S2 ? q.Hc : g.H;
+  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+    const int row = e / CPR, cv = e % CPR;
+    const long m = m0 + row;
+    const int n = n0 + cv * VW;
+    if (m >= M || n >= g.C) continue;
+    long pix = m;
+    if (S2) {
+      const int xx = (int)(m % Wm);
+      const long t = m / Wm;
+      const int yy = (int)(t % Hm), b = (int)(t / Hm);
+      pix = ((long)b * g.H + 2 * yy + q.a) * g.W + 2 * xx + q.b;
+    }
+    const T* src = lds + row * RS + cv * VW;
+    T* dst = dx + pix * g.xps + n;
+    if (vec && n + VW <= g.C) {
+      if (accumulate) {
+        float a[VW], b[VW];
+        unpack<T>(*reinterpret_cast<const uint4*>(src), a);
+        unpack<T>(*reinterpret_cast<const uint4*>(dst), b);
 #pragma unroll
-  for (int i = 0; i < TT::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TT::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (g.KH * g.KW * g.K + BK - 1) / BK;
-  mainloop<T, BM, BN>(ld, 0, nk, lds, acc);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
-#pragma unroll
-  for (int j = 0; j < TT::TN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < TT::TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
-        if (m < M && n < g.C) {
-          T* p = dx + m * g.xps + n;
-          float v = acc[i][j][r];
-          if (accumulate) v += to_f(*p);
-          *p = from_f<T>(v);
-        }
+        for (int j = 0; j < VW; ++j) a[j] += b[j];
+        *reinterpret_cast<uint4*>(dst) = pack<T>(a);
+      } else {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
       }
+    } else {
+      for (int j = 0; j < VW && n + j < g.C; ++j)
+        dst[j] = accumulate ? from_f<T>(to_f(src[j]) + to_f(dst[j])) : src[j];
+    }
   }
 }
 
 template <typename T, int BM, int BN, bool VECA, bool VECB>
 __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                        float* __restrict__ dw, int kt_per_split, Geom g) {
-  using TT = Tile<T, BM, BN>;
-  __shared__ __attribute__((aligned(16))) T lds[2 * TT::STAGE];
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+                                                        float* __restrict__ dw, int kt_per_split, Geom g, int gm,
+                                                        int gn) {
+  using TT = Tile<T, BM, BN, true, true>;
+  __shared__ __attribute__((aligned(16))) char smem[TT::LDS_BYTES];
+  T* lds = reinterpret_cast<T*>(smem);
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const int m0 = tm * BM, n0 = tn * BN;
   WgradLoader<T, BM, BN, VECA, VECB> ld(x, dy, g, m0, n0);
   const long NP = (long)g.N * g.OH * g.OW;
-  const int nk = (int)((NP + BK - 1) / BK);
-  const int kt0 = blockIdx.z * kt_per_split;
+  const int nk = (int)((NP + TT::BK - 1) / TT::BK);
+  const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(nk, kt0 + kt_per_split);
   f32x4 acc[TT::TM][TT::TN];
+  zero_acc<BM, BN>(acc);
+  mainloop<T, BM, BN, true, true>(ld, kt0, kt1, lds, acc);
+  __syncthreads();
+  // stage the fp32 partial tile in LDS, then atomics in contiguous 256-B wave segments
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int RS = BN + 4;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
 #pragma unroll
   for (int i = 0; i < TT::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TT::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mainloop<T, BM, BN>(ld, kt0, kt1, lds, acc);
+    for (int j = 0; j < TT::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r) * RS + wn * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
-#pragma unroll
-  for (int j = 0; j < TT::TN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < TT::TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
-        if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, acc[i][j][r]);
-      }
+  for (int e = threadIdx.x; e < BM * BN; e += NT) {
+    const int row = e / BN, c = e % BN;
+    const int m = m0 + row, n = n0 + c;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
   }
 }
 
@@ -514,33 +709,40 @@ template <typename T, int BM, int BN>
 int launch_fwd(const T* x, const T* w, const float* b, T* y, float* ps, float* pq, const Geom& g, hipStream_t st) {
   constexpr int VW = Traits<T>::VW;
   const long M = (long)g.N * g.OH * g.OW;
-  dim3 grid(ceil_div(M, BM), ceil_div(g.K, BN));
+  const int gm = ceil_div(M, BM), gn = ceil_div(g.K, BN);
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
   const bool vec = g.C % VW == 0 && g.xps % VW == 0 && aligned16(x);
-  if (vec && p1) conv_fwd_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g);
-  else if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g);
-  else if (p1) conv_fwd_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g);
-  else conv_fwd_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g);
+  const unsigned grid = (unsigned)gm * gn;
+  if (vec && p1) conv_fwd_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
+  else if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
+  else if (p1) conv_fwd_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
+  else conv_fwd_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
   return (int)hipGetLastError();
 }
 
 template <typename T, int BM, int BN>
 int launch_dgrad(const T* dy, const T* wt, T* dx, int acc, const Geom& g, hipStream_t st) {
   constexpr int VW = Traits<T>::VW;
-  const long M = (long)g.N * g.H * g.W;
-  dim3 grid(ceil_div(M, BM), ceil_div(g.C, BN));
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
+  const bool s2 = g.S == 2;
+  const long M = s2 ? (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2) : (long)g.N * g.H * g.W;
+  const int gm = ceil_div(M, BM), gn = ceil_div(g.C, BN);
   const bool vec = g.K % VW == 0 && g.yps % VW == 0 && aligned16(dy);
-  if (vec && p1) conv_dgrad_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g);
-  else if (vec) conv_dgrad_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g);
-  else if (p1) conv_dgrad_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g);
-  else conv_dgrad_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g);
+  const dim3 grid((unsigned)gm * gn, s2 ? 4 : 1);
+  if (s2) {
+    if (vec) conv_dgrad_kernel<T, BM, BN, true, false, true><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
+    else conv_dgrad_kernel<T, BM, BN, false, false, true><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
+  } else if (vec && p1) conv_dgrad_kernel<T, BM, BN, true, true, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
+  else if (vec) conv_dgrad_kernel<T, BM, BN, true, false, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
+  else if (p1) conv_dgrad_kernel<T, BM, BN, false, true, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
+  else conv_dgrad_kernel<T, BM, BN, false, false, false><<<grid, NT, 0, st>>>(dy, wt, dx, acc, g, gm, gn);
   return (int)hipGetLastError();
 }
 
 template <typename T, int BM, int BN>
 int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t st) {
   constexpr int VW = Traits<T>::VW;
+  constexpr int BK = Cfg<T>::BK;
   const long NP = (long)g.N * g.OH * g.OW;
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, BM), gn = ceil_div(Ntot, BN);
@@ -551,16 +753,16 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
   if (splits > maxs) splits = maxs;
-  int per = ceil_div(nk, splits);
+  const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
-  dim3 grid(gm, gn, splits);
+  const dim3 grid((unsigned)gm * gn, splits);
   const bool va = g.K % VW == 0 && g.yps % VW == 0 && aligned16(dy);
   const bool vb = g.C % VW == 0 && g.xps % VW == 0 && aligned16(x);
   (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
-  if (va && vb) conv_wgrad_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g);
-  else if (va) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g);
-  else if (vb) conv_wgrad_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g);
-  else conv_wgrad_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g);
+  if (va && vb) conv_wgrad_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  else if (va) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  else if (vb) conv_wgrad_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  else conv_wgrad_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
   return (int)hipGetLastError();
 }
 
@@ -573,7 +775,7 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
 }
 template <typename T>
 int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st) {
-  const long M = (long)g.N * g.H * g.W;
+  const long M = (long)g.N * g.H * g.W / (g.S == 2 ? 4 : 1);
   if (big_tile(M, g.C)) return launch_dgrad<T, 128, 128>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
   return launch_dgrad<T, 64, 64>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
 }
@@ -602,6 +804,7 @@ DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
                            void* stream) {
   Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
   if ((long)N * H * W == 0 || C == 0) return 0;
+  if (S > 2) return (int)hipErrorInvalidValue;
   return dtype ? conv_dgrad_t<bf16>(dy, wt, dx, accumulate, g, (hipStream_t)stream)
                : conv_dgrad_t<float>(dy, wt, dx, accumulate, g, (hipStream_t)stream);
 }

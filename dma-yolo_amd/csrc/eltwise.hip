@@ -410,16 +410,24 @@ __global__ void ca_apply_bwd_att_kernel(const T* __restrict__ x, long xps, const
 template <typename S, typename T>
 __global__ void nchw_to_nhwc_kernel(const S* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W, int Cp,
                                     float scale) {
-  // output pixel stride Cp >= C; channels [C, Cp) are written as zeros (stem vector padding)
-  const long total = (long)N * Cp * H * W;
+  // one thread per pixel: C plane reads (coalesced across threads along w), Cp contiguous writes
+  // (16-B vectors when Cp*sizeof(T) is a multiple of 16); channels [C, Cp) are zero (stem padding)
+  const long HW = (long)H * W, total = (long)N * HW;
+  constexpr int VW = Traits<T>::VW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % Cp);
-    long t = i / Cp;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
-    y[i] = from_f<T>(c < C ? (float)x[(((long)b * C + c) * H + h) * W + w] * scale : 0.f);
+    const long b = i / HW, r = i % HW;
+    const S* src = x + b * C * HW + r;
+    T* dst = y + i * Cp;
+    for (int c0 = 0; c0 < Cp; c0 += VW) {
+      float f[VW];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] = (c0 + j < C) ? (float)src[(long)(c0 + j) * HW] * scale : 0.f;
+      if (c0 + VW <= Cp) {
+        *reinterpret_cast<uint4*>(dst + c0) = pack<T>(f);
+      } else {
+        for (int j = 0; c0 + j < Cp; ++j) dst[c0 + j] = from_f<T>(f[j]);
+      }
+    }
   }
 }
 
@@ -577,7 +585,7 @@ DMY_API int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh,
 DMY_API int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cp,
                              float scale, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const long n = (long)N * Cp * H * W;
+  const long n = (long)N * H * W;
   if (src_kind == 0) {
     DISPATCH_T(dtype, nchw_to_nhwc_kernel<uint8_t, T><<<egrid(n), 256, 0, st>>>((const uint8_t*)x, (T*)y, N, C, H, W, Cp, scale));
   } else {
