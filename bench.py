@@ -42,6 +42,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-detect', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--layer-report', action='store_true', help='per-conv-shape timing table on stderr')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='process-group backend (nccl = RCCL; gloo only to rehearse several ranks on one GPU)')
     return ap.parse_args()
 
 
@@ -53,6 +56,22 @@ def build(cfg, dtype, device):
     m = Model(os.path.join(CDIR, yml), nc=nc, act_dtype=dtype).to(device)
     m.hyp = scaled_hyp(HYP_VISDRONE, nc, img)
     return m
+
+
+def train_step(net, model, compute_loss, opt, ema, imgs, tg, world):
+    """One iteration of train.py:400-454 on a staged batch: forward (DDP-wrapped `net` when world > 1),
+    loss * WORLD_SIZE (train.py:440; DDP averages, so the applied gradient is the sum over ranks),
+    backward (RCCL bucketed all-reduce overlapped by DDP), optimizer step, rank-0 EMA."""
+    pred = net(imgs)
+    loss, _ = compute_loss(pred, tg)
+    if world > 1:
+        loss = loss * world
+    loss.backward()
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    if ema is not None:
+        ema.update(model)
+    return loss
 
 
 def cpu_baseline(cfg, seconds):
@@ -95,10 +114,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = torch.cuda.device_count()
+    dev_idx = local % max(ndev, 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    device = torch.device('cuda', local)
+        torch.cuda.set_device(dev_idx)
+        if a.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_idx))
+        else:
+            dist.init_process_group('gloo')
+    device = torch.device('cuda', dev_idx)
     cfg = list(CONFIGS[a.config])
     if a.batch:
         cfg[3] = a.batch
@@ -119,21 +143,12 @@ def main():
     ema = ModelEMA(model) if rank == 0 else None
     net = model
     if world > 1:
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local)
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev_idx], output_device=dev_idx)
     imgs = images(bs, img, seed=1 + rank, device=device)
     tg = targets(bs, nc, seed=1 + rank, device=device)
 
     def step():
-        pred = net(imgs)
-        loss, items = compute_loss(pred, tg)
-        if world > 1:
-            loss = loss * world
-        loss.backward()
-        opt.step()
-        opt.zero_grad(set_to_none=True)
-        if ema is not None:
-            ema.update(model)
-        return loss
+        return train_step(net, model, compute_loss, opt, ema, imgs, tg, world)
 
     model.train()
     for _ in range(a.warmup):
@@ -151,12 +166,20 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     KernelTimer.enabled = False
-    ks = KernelTimer.summary()
+    detail = {} if a.layer_report else None
+    ks = KernelTimer.summary(detail)
+    if detail and rank == 0:
+        tot = sum(v[2] for v in detail.values())
+        print('kind        N    C    H    W    K  k s  launches  ms/step  TFLOP/s  share', file=sys.stderr)
+        for (kind, tag), v in sorted(detail.items(), key=lambda kv: -kv[1][2]):
+            print('%-10s %s %6d %8.3f %8.1f %6.3f' % (kind, ' '.join('%4d' % t for t in tag), v[0],
+                  v[2] * 1e3 / a.steps, v[1] / v[2] / 1e12, v[2] / tot), file=sys.stderr)
     if world > 1:
         t = torch.tensor([el], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     assert torch.isfinite(loss).all(), 'non-finite loss'
+    peak_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30
     ips = world * bs * a.steps / el
 
     # dominant kernel family by time -> roofline
@@ -165,7 +188,7 @@ def main():
     achieved = d['flops'] / d['launches'] / (d['seconds'] / d['launches']) / 1e12
     roof = dict(bound='mfma', kernel=f'dmy_{dom} (implicit-GEMM, all launches of the timed region)',
                 achieved=round(achieved, 2), peak=PEAK[dtype], unit='TFLOP/s', frac=round(achieved / PEAK[dtype], 4),
-                traffic=None, launches=d['launches'],
+                traffic=None, launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
                 kernels={k: dict(launches=v['launches'], ms=round(v['seconds'] * 1e3 / a.steps, 3),
                                  tflops=round(v['flops'] / v['seconds'] / 1e12, 2)) for k, v in ks.items()},
                 conv_share_of_step=round(sum(v['seconds'] for v in ks.values()) / el, 3))
@@ -212,7 +235,7 @@ def main():
             'data': 'synthetic (uint8 images seed 1, 50 VisDrone-like targets/img; random-init weights)',
             'config': {'workload': f'{yml} train @{img} nc={nc}', 'model': yml, 'global_batch': bs * world,
                        'img': img, 'parallelism': f'dp{world}'},
-            'roofline': roof, 'cpu_baseline': cpu, **extra,
+            'roofline': roof, 'cpu_baseline': cpu, 'peak_hbm_gib': round(peak_gb, 1), **extra,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

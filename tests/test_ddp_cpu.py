@@ -1,0 +1,102 @@
+"""CPU, world_size 2 over gloo: the data-parallel training step of bench.py (train.py:400-454 +
+DDP at train.py:326) shards images by rank and applies the SUM of the per-rank gradients
+(loss * WORLD_SIZE, DDP averaging, train.py:440).  The model here is the CPU oracle: the
+product modules need the GPU; what is checked is the sharding / exchange / step logic that
+bench.py runs over RCCL on the GPU box."""
+import os
+import socket
+import sys
+import tempfile
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = os.path.join(ROOT, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5n.yaml')
+IMG, BS, NC = 64, 2, 10
+
+
+def _setup():
+    for p in (ROOT, os.path.join(ROOT, 'dma-yolo_amd')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _model():
+    from oracle import nn as onn
+    torch.manual_seed(0)
+    with open(CFG) as f:
+        d = yaml.safe_load(f)
+    return onn.bn_defaults(onn.Model(d, nc=NC)).train()
+
+
+def _loss_fn(model):
+    from oracle.loss import compute_loss
+    from dmayolo.synthetic import HYP_SCRATCH, scaled_hyp
+    det = model.model[-1]
+    anchors = det.anchors / det.stride.view(-1, 1, 1)
+    hyp = scaled_hyp(HYP_SCRATCH, NC, IMG)
+    return lambda p, t: compute_loss(p, t, anchors, hyp, NC)
+
+
+def _batch(rank):
+    from dmayolo.synthetic import images, targets
+    return images(BS, IMG, seed=1 + rank).float() / 255, targets(BS, NC, per_image=6, seed=1 + rank)
+
+
+def _worker(rank, world, port, out):
+    _setup()
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import bench
+    model = _model()
+    net = torch.nn.parallel.DistributedDataParallel(model)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+    x, t = _batch(rank)
+    loss = bench.train_step(net, model, _loss_fn(model), opt, None, x, t, world)
+    assert torch.isfinite(loss).all()
+    if rank == 0:
+        torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def test_ddp_world2_applies_sum_of_rank_gradients():
+    _setup()
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, 'rank0.pt')
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    # expected: one process, per-shard forward (BN batch stats per rank, no SyncBN), grads summed
+    model = _model()
+    lf = _loss_fn(model)
+    grads = None
+    for r in range(world):
+        x, t = _batch(r)
+        model.zero_grad(set_to_none=True)
+        loss, _ = lf(model(x), t)
+        loss.backward()
+        g = [p.grad.clone() for p in model.parameters()]
+        grads = g if grads is None else [a + b for a, b in zip(grads, g)]
+    ref = _model()
+    opt = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+    for p, g in zip(ref.parameters(), grads):
+        p.grad = g
+    opt.step()
+    exp = dict(ref.named_parameters())
+    n = 0
+    for k, v in got.items():
+        if k in exp:
+            torch.testing.assert_close(v, exp[k].detach(), rtol=1e-4, atol=1e-6)
+            n += 1
+    assert n == len(exp)
