@@ -4,115 +4,177 @@
 //   BiFPN weights (Concat :656-664, AdConcat2/3 :994-1026), SCConv gate (:1311-1314),
 //   CoorAttention pooling / re-weighting (:1183-1207), input normalisation (train.py:402).
 #include "common.h"
+#include <initializer_list>
 
 namespace {
 
 inline bool al16(const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; }
 
+// NV = elements per thread: the 16-byte vector width (channels % VW == 0, 16-B aligned bases and
+// pixel strides) or 1 (scalar fallback).  All math per element in fp32, identical in both forms.
+template <typename T, int NV> DEV void ldv(const T* p, float* f) {
+  if constexpr (NV == Traits<T>::VW) unpack<T>(*reinterpret_cast<const uint4*>(p), f);
+  else
+#pragma unroll
+    for (int j = 0; j < NV; ++j) f[j] = to_f(p[j]);
+}
+template <typename T, int NV> DEV void stv(T* p, const float* f) {
+  if constexpr (NV == Traits<T>::VW) *reinterpret_cast<uint4*>(p) = pack<T>(f);
+  else
+#pragma unroll
+    for (int j = 0; j < NV; ++j) p[j] = from_f<T>(f[j]);
+}
+// decompose a vector index over [N][H][W][C/NV] -> (b, h, w, c)
+DEV void vidx(long i, int H, int W, int CV, int NV, int& b, int& h, int& w, int& c) {
+  c = (int)(i % CV) * NV;
+  long t = i / CV;
+  w = (int)(t % W);
+  t /= W;
+  h = (int)(t % H);
+  b = (int)(t / H);
+}
+
 // ---------------------------------------------------------------- max-pool (k odd, stride 1, pad k/2)
 // Writes the first-max window offset (row-major scan, like ATen's CPU kernel) for the backward.
-template <typename T>
+template <typename T, int NV>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps,
                                    uint8_t* __restrict__ arg, int N, int H, int W, int C, int k) {
-  const long total = (long)N * H * W * C;
+  const int CV = C / NV;
+  const long total = (long)N * H * W * CV;
   const int p = k / 2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
-    float best = -INFINITY;
-    int bi = 0;
+    int b, h, w, c;
+    vidx(i, H, W, CV, NV, b, h, w, c);
+    float best[NV];
+    int bi[NV];
+    bool nan[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) { best[j] = -INFINITY; bi[j] = 0; nan[j] = false; }
     for (int dh = 0; dh < k; ++dh) {
       const int hh = h - p + dh;
       if (hh < 0 || hh >= H) continue;
       for (int dw = 0; dw < k; ++dw) {
         const int ww = w - p + dw;
         if (ww < 0 || ww >= W) continue;
-        const float v = to_f(x[(((long)b * H + hh) * W + ww) * xps + c]);
-        if (v > best || isnan(v)) {
-          best = v;
-          bi = dh * k + dw;
-          if (isnan(v)) { dh = k; break; }
+        float v[NV];
+        ldv<T, NV>(x + (((long)b * H + hh) * W + ww) * xps + c, v);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          if (!nan[j] && (v[j] > best[j] || isnan(v[j]))) {
+            best[j] = v[j];
+            bi[j] = dh * k + dw;
+            nan[j] = isnan(v[j]);
+          }
         }
       }
     }
     const long pix = ((long)b * H + h) * W + w;
-    y[pix * yps + c] = from_f<T>(best);
-    arg[pix * C + c] = (uint8_t)bi;
+    stv<T, NV>(y + pix * yps + c, best);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) arg[pix * C + c + j] = (uint8_t)bi[j];
   }
 }
 
 // dx[p] = sum of dy[q] over windows q whose argmax is p (gather: deterministic, no atomics)
-template <typename T>
+template <typename T, int NV>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, long dps, const uint8_t* __restrict__ arg,
                                    T* __restrict__ dx, long dxps, int accumulate, int N, int H, int W, int C, int k) {
-  const long total = (long)N * H * W * C;
+  const int CV = C / NV;
+  const long total = (long)N * H * W * CV;
   const int p = k / 2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
-    float s = 0.f;
+    int b, h, w, c;
+    vidx(i, H, W, CV, NV, b, h, w, c);
+    float s[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] = 0.f;
     for (int oh = h - p; oh <= h + p; ++oh) {
       if (oh < 0 || oh >= H) continue;
       for (int ow = w - p; ow <= w + p; ++ow) {
         if (ow < 0 || ow >= W) continue;
         const long q = ((long)b * H + oh) * W + ow;
-        const int a = arg[q * C + c];
-        if (a == (h - oh + p) * k + (w - ow + p)) s += to_f(dy[q * dps + c]);
+        const int want = (h - oh + p) * k + (w - ow + p);
+        uint8_t a[NV];
+        if constexpr (NV == 8) *reinterpret_cast<uint2*>(a) = *reinterpret_cast<const uint2*>(arg + q * C + c);
+        else if constexpr (NV == 4) *reinterpret_cast<uint32_t*>(a) = *reinterpret_cast<const uint32_t*>(arg + q * C + c);
+        else
+#pragma unroll
+          for (int j = 0; j < NV; ++j) a[j] = arg[q * C + c + j];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) any |= a[j] == want;
+        if (!any) continue;
+        float d[NV];
+        ldv<T, NV>(dy + q * dps + c, d);
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+          if (a[j] == want) s[j] += d[j];
       }
     }
     T* o = dx + (((long)b * H + h) * W + w) * dxps + c;
-    if (accumulate) s += to_f(*o);
-    *o = from_f<T>(s);
+    if (accumulate) {
+      float d[NV];
+      ldv<T, NV>(o, d);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) s[j] += d[j];
+    }
+    stv<T, NV>(o, s);
   }
 }
 
 // ---------------------------------------------------------------- avg-pool r x r, stride r, floor mode
-template <typename T>
+template <typename T, int NV>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, int N, int H, int W, int C,
                                    int r) {
-  const int OH = H / r, OW = W / r;
-  const long total = (long)N * OH * OW * C;
+  const int OH = H / r, OW = W / r, CV = C / NV;
+  const long total = (long)N * OH * OW * CV;
   const float inv = 1.0f / (r * r);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int ow = (int)(t % OW);
-    t /= OW;
-    const int oh = (int)(t % OH);
-    const int b = (int)(t / OH);
-    float s = 0.f;
+    int b, oh, ow, c;
+    vidx(i, OH, OW, CV, NV, b, oh, ow, c);
+    float s[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] = 0.f;
     for (int dh = 0; dh < r; ++dh)
-      for (int dw = 0; dw < r; ++dw) s += to_f(x[(((long)b * H + oh * r + dh) * W + ow * r + dw) * xps + c]);
-    y[i] = from_f<T>(s * inv);
+      for (int dw = 0; dw < r; ++dw) {
+        float v[NV];
+        ldv<T, NV>(x + (((long)b * H + oh * r + dh) * W + ow * r + dw) * xps + c, v);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) s[j] += v[j];
+      }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] *= inv;
+    stv<T, NV>(y + (((long)b * OH + oh) * OW + ow) * C + c, s);
   }
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, long dxps, int accumulate, int N,
                                    int H, int W, int C, int r) {
-  const int OH = H / r, OW = W / r;
-  const long total = (long)N * H * W * C;
+  const int OH = H / r, OW = W / r, CV = C / NV;
+  const long total = (long)N * H * W * CV;
   const float inv = 1.0f / (r * r);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
+    int b, h, w, c;
+    vidx(i, H, W, CV, NV, b, h, w, c);
     const int oh = h / r, ow = w / r;
-    float v = (oh < OH && ow < OW) ? to_f(dy[(((long)b * OH + oh) * OW + ow) * C + c]) * inv : 0.f;
+    float v[NV];
+    if (oh < OH && ow < OW) {
+      ldv<T, NV>(dy + (((long)b * OH + oh) * OW + ow) * C + c, v);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] *= inv;
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] = 0.f;
+    }
     T* o = dx + (((long)b * H + h) * W + w) * dxps + c;
-    if (accumulate) v += to_f(*o);
-    *o = from_f<T>(v);
+    if (accumulate) {
+      float d[NV];
+      ldv<T, NV>(o, d);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += d[j];
+    }
+    stv<T, NV>(o, v);
   }
 }
 
@@ -125,43 +187,51 @@ DEV int nearest_src(int d, int in, int out) {
   return s < in - 1 ? s : in - 1;
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ void resize_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps, float yscale,
                                   int N, int IH, int IW, int OH, int OW, int C) {
-  const long total = (long)N * OH * OW * C;
+  const int CV = C / NV;
+  const long total = (long)N * OH * OW * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int ow = (int)(t % OW);
-    t /= OW;
-    const int oh = (int)(t % OH);
-    const int b = (int)(t / OH);
+    int b, oh, ow, c;
+    vidx(i, OH, OW, CV, NV, b, oh, ow, c);
     const int ih = nearest_src(oh, IH, OH), iw = nearest_src(ow, IW, OW);
-    y[(((long)b * OH + oh) * OW + ow) * yps + c] = from_f<T>(yscale * to_f(x[(((long)b * IH + ih) * IW + iw) * xps + c]));
+    float v[NV];
+    ldv<T, NV>(x + (((long)b * IH + ih) * IW + iw) * xps + c, v);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] *= yscale;
+    stv<T, NV>(y + (((long)b * OH + oh) * OW + ow) * yps + c, v);
   }
 }
 
 // dx[ih,iw] = sum over dst (oh,ow) mapping to it; preimages are contiguous ranges
-template <typename T>
+template <typename T, int NV>
 __global__ void resize_bwd_kernel(const T* __restrict__ dy, long dps, T* __restrict__ dx, long dxps, int N, int IH,
                                   int IW, int OH, int OW, int C) {
-  const long total = (long)N * IH * IW * C;
+  const int CV = C / NV;
+  const long total = (long)N * IH * IW * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int iw = (int)(t % IW);
-    t /= IW;
-    const int ih = (int)(t % IH);
-    const int b = (int)(t / IH);
-    const int h0 = max(0, (int)((long)ih * OH / IH) - 2), h1 = min(OH - 1, (int)((long)(ih + 1) * OH / IH) + 2);
-    const int w0 = max(0, (int)((long)iw * OW / IW) - 2), w1 = min(OW - 1, (int)((long)(iw + 1) * OW / IW) + 2);
-    float s = 0.f;
+    int b, ih, iw, c;
+    vidx(i, IH, IW, CV, NV, b, ih, iw, c);
+    int h0, h1, w0, w1;
+    if (OH == 2 * IH) { h0 = 2 * ih; h1 = h0 + 1; }
+    else { h0 = max(0, (int)((long)ih * OH / IH) - 2); h1 = min(OH - 1, (int)((long)(ih + 1) * OH / IH) + 2); }
+    if (OW == 2 * IW) { w0 = 2 * iw; w1 = w0 + 1; }
+    else { w0 = max(0, (int)((long)iw * OW / IW) - 2); w1 = min(OW - 1, (int)((long)(iw + 1) * OW / IW) + 2); }
+    float s[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] = 0.f;
     for (int oh = h0; oh <= h1; ++oh) {
       if (nearest_src(oh, IH, OH) != ih) continue;
       for (int ow = w0; ow <= w1; ++ow)
-        if (nearest_src(ow, IW, OW) == iw) s += to_f(dy[(((long)b * OH + oh) * OW + ow) * dps + c]);
+        if (nearest_src(ow, IW, OW) == iw) {
+          float v[NV];
+          ldv<T, NV>(dy + (((long)b * OH + oh) * OW + ow) * dps + c, v);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) s[j] += v[j];
+        }
     }
-    dx[(((long)b * IH + ih) * IW + iw) * dxps + c] = from_f<T>(s);
+    stv<T, NV>(dx + (((long)b * IH + ih) * IW + iw) * dxps + c, s);
   }
 }
 
@@ -206,15 +276,20 @@ __global__ void slice_copy_kernel(const T* __restrict__ src, long sps, T* __rest
 }
 
 // per-block partial of sum(a*b) over a [M][C] slice pair
-template <typename T>
+template <typename T, int NV>
 __global__ void dot_partial_kernel(const T* __restrict__ a, long aps, const T* __restrict__ b, long bps, long M,
                                    int C, float* __restrict__ part) {
-  const long total = M * C;
+  const int CV = C / NV;
+  const long total = M * CV;
   float s = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / C;
-    const int c = (int)(i % C);
-    s += to_f(a[m * aps + c]) * to_f(b[m * bps + c]);
+    const long m = i / CV;
+    const int c = (int)(i % CV) * NV;
+    float av[NV], bv[NV];
+    ldv<T, NV>(a + m * aps + c, av);
+    ldv<T, NV>(b + m * bps + c, bv);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s += av[j] * bv[j];
   }
   __shared__ float red[4];
   s = wave_sum(s);
@@ -245,46 +320,57 @@ __global__ void bifpn_wgrad_kernel(const float* __restrict__ part, int nblk, int
 
 // ---------------------------------------------------------------- SCConv gate
 // out = u3 * sigmoid(x + nearest(g))   with g the k2 branch at the pooled resolution
-template <typename T>
+// torch computes sigmoid(add(identity, y_)) in storage precision, then mul: reproduced per element.
+template <typename T, int NV>
 __global__ void scgate_fwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ u3, const T* __restrict__ g,
                                   T* __restrict__ out, int N, int H, int W, int C, int GH, int GW) {
-  const long total = (long)N * H * W * C;
+  const int CV = C / NV;
+  const long total = (long)N * H * W * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
+    int b, h, w, c;
+    vidx(i, H, W, CV, NV, b, h, w, c);
     const long pix = ((long)b * H + h) * W + w;
     const int gh = nearest_src(h, GH, H), gw = nearest_src(w, GW, W);
-    const float gv = to_f(g[(((long)b * GH + gh) * GW + gw) * C + c]);
-    // torch: sigmoid(add(identity, y_)) computed in storage precision, then mul
-    const float s = sigmoidf_(to_f(from_f<T>(to_f(x[pix * xps + c]) + gv)));
-    out[pix * C + c] = from_f<T>(to_f(u3[pix * C + c]) * to_f(from_f<T>(s)));
+    float xv[NV], gv[NV], uv[NV];
+    ldv<T, NV>(x + pix * xps + c, xv);
+    ldv<T, NV>(g + (((long)b * GH + gh) * GW + gw) * C + c, gv);
+    ldv<T, NV>(u3 + pix * C + c, uv);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float sg = sigmoidf_(to_f(from_f<T>(xv[j] + gv[j])));
+      uv[j] = uv[j] * to_f(from_f<T>(sg));
+    }
+    stv<T, NV>(out + pix * C + c, uv);
   }
 }
 
-// d u3 = dout * s ;  dpre = dout * u3 * s(1-s)  (-> dx contribution, written to dpre)
-template <typename T>
+// d u3 = dout * s ;  dpre = dout * u3 * s(1-s)  (-> dx contribution, written or accumulated into dpre)
+template <typename T, int NV>
 __global__ void scgate_bwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ u3, const T* __restrict__ g,
-                                  const T* __restrict__ dout, T* __restrict__ du3, T* __restrict__ dpre, int N, int H,
-                                  int W, int C, int GH, int GW) {
-  const long total = (long)N * H * W * C;
+                                  const T* __restrict__ dout, T* __restrict__ du3, T* __restrict__ dpre, long dpps,
+                                  int accumulate, int N, int H, int W, int C, int GH, int GW) {
+  const int CV = C / NV;
+  const long total = (long)N * H * W * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
+    int b, h, w, c;
+    vidx(i, H, W, CV, NV, b, h, w, c);
     const long pix = ((long)b * H + h) * W + w;
     const int gh = nearest_src(h, GH, H), gw = nearest_src(w, GW, W);
-    const float gv = to_f(g[(((long)b * GH + gh) * GW + gw) * C + c]);
-    const float s = sigmoidf_(to_f(from_f<T>(to_f(x[pix * xps + c]) + gv)));
-    const float d = to_f(dout[pix * C + c]);
-    du3[pix * C + c] = from_f<T>(d * s);
-    dpre[pix * C + c] = from_f<T>(d * to_f(u3[pix * C + c]) * s * (1.f - s));
+    float xv[NV], gv[NV], uv[NV], dv[NV], pv[NV];
+    ldv<T, NV>(x + pix * xps + c, xv);
+    ldv<T, NV>(g + (((long)b * GH + gh) * GW + gw) * C + c, gv);
+    ldv<T, NV>(u3 + pix * C + c, uv);
+    ldv<T, NV>(dout + pix * C + c, dv);
+    if (accumulate) ldv<T, NV>(dpre + pix * dpps + c, pv);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float sg = sigmoidf_(to_f(from_f<T>(xv[j] + gv[j])));
+      const float dp = dv[j] * uv[j] * sg * (1.f - sg);
+      pv[j] = accumulate ? pv[j] + dp : dp;
+      uv[j] = dv[j] * sg;
+    }
+    stv<T, NV>(du3 + pix * C + c, uv);
+    stv<T, NV>(dpre + pix * dpps + c, pv);
   }
 }
 
@@ -483,40 +569,71 @@ inline int egrid(long n) { return grid_cap(ceil_div(n, 256), 8192); }
     __VA_ARGS__;                       \
   }
 
+// T = storage type; NV = 16-byte vector width when `vec` holds, else 1 (scalar)
+#define DISPATCH_TV(dtype, vec, ...)                \
+  if (dtype) {                                      \
+    using T = bf16;                                 \
+    if (vec) { constexpr int NV = 8; __VA_ARGS__; } \
+    else { constexpr int NV = 1; __VA_ARGS__; }     \
+  } else {                                          \
+    using T = float;                                \
+    if (vec) { constexpr int NV = 4; __VA_ARGS__; } \
+    else { constexpr int NV = 1; __VA_ARGS__; }     \
+  }
+
+namespace {
+// all channel counts / pixel strides multiples of the 16-B vector and all bases 16-B aligned
+inline bool vec_ok(int dtype, std::initializer_list<long> ns, std::initializer_list<const void*> ps) {
+  const long VW = dtype ? 8 : 4;
+  for (long n : ns)
+    if (n % VW) return false;
+  for (const void* p : ps)
+    if (!al16(p)) return false;
+  return true;
+}
+inline long vw_of(int dtype, bool vec) { return vec ? (dtype ? 8 : 4) : 1; }
+}  // namespace
+
 DMY_API int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yps, unsigned char* arg, int N, int H,
                             int W, int C, int k, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, maxpool_fwd_kernel<T><<<egrid((long)N * H * W * C), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, arg, N, H, W, C, k));
+  const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
+  DISPATCH_TV(dtype, v, maxpool_fwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, arg, N, H, W, C, k));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned char* arg, void* dx, long dxps,
                             int accumulate, int N, int H, int W, int C, int k, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, maxpool_bwd_kernel<T><<<egrid((long)N * H * W * C), 256, 0, st>>>((const T*)dy, dps, arg, (T*)dx, dxps, accumulate, N, H, W, C, k));
+  const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
+  DISPATCH_TV(dtype, v, maxpool_bwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)dy, dps, arg, (T*)dx, dxps, accumulate, N, H, W, C, k));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_avgpool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, int r,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, avgpool_fwd_kernel<T><<<egrid((long)N * (H / r) * (W / r) * C), 256, 0, st>>>((const T*)x, xps, (T*)y, N, H, W, C, r));
+  const bool v = vec_ok(dtype, {C, xps}, {x, y});
+  DISPATCH_TV(dtype, v, avgpool_fwd_kernel<T, NV><<<egrid((long)N * (H / r) * (W / r) * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, N, H, W, C, r));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_avgpool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C,
                             int r, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, avgpool_bwd_kernel<T><<<egrid((long)N * H * W * C), 256, 0, st>>>((const T*)dy, (T*)dx, dxps, accumulate, N, H, W, C, r));
+  const bool v = vec_ok(dtype, {C, dxps}, {dy, dx});
+  DISPATCH_TV(dtype, v, avgpool_bwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)dy, (T*)dx, dxps, accumulate, N, H, W, C, r));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_resize_fwd(int dtype, const void* x, long xps, void* y, long yps, float yscale, int N, int IH, int IW,
                            int OH, int OW, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, resize_fwd_kernel<T><<<egrid((long)N * OH * OW * C), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, yscale, N, IH, IW, OH, OW, C));
+  const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
+  DISPATCH_TV(dtype, v, resize_fwd_kernel<T, NV><<<egrid((long)N * OH * OW * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, yscale, N, IH, IW, OH, OW, C));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_resize_bwd(int dtype, const void* dy, long dps, void* dx, long dxps, int N, int IH, int IW, int OH,
                            int OW, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, resize_bwd_kernel<T><<<egrid((long)N * IH * IW * C), 256, 0, st>>>((const T*)dy, dps, (T*)dx, dxps, N, IH, IW, OH, OW, C));
+  const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
+  DISPATCH_TV(dtype, v, resize_bwd_kernel<T, NV><<<egrid((long)N * IH * IW * C / NV), 256, 0, st>>>((const T*)dy, dps, (T*)dx, dxps, N, IH, IW, OH, OW, C));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long dps, long M, int C, const float* wv,
@@ -532,12 +649,13 @@ DMY_API int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long
   }
   return (int)hipGetLastError();
 }
-DMY_API int dmy_dot_partial_blocks(long M, int C) { return grid_cap(ceil_div(M * C, 256 * 8), 512); }
+DMY_API int dmy_dot_partial_blocks(long M, int C) { return grid_cap(ceil_div(M * C, 256 * 64), 2048); }
 DMY_API int dmy_dot_partial(int dtype, const void* a, long aps, const void* b, long bps, long M, int C, float* part,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int nb = dmy_dot_partial_blocks(M, C);
-  DISPATCH_T(dtype, dot_partial_kernel<T><<<nb, 256, 0, st>>>((const T*)a, aps, (const T*)b, bps, M, C, part));
+  const bool v = vec_ok(dtype, {C, aps, bps}, {a, b});
+  DISPATCH_TV(dtype, v, dot_partial_kernel<T, NV><<<nb, 256, 0, st>>>((const T*)a, aps, (const T*)b, bps, M, C, part));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* wv, float eps, float* dw, void* stream) {
@@ -547,13 +665,16 @@ DMY_API int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* wv
 DMY_API int dmy_scgate_fwd(int dtype, const void* x, long xps, const void* u3, const void* g, void* out, int N, int H,
                            int W, int C, int GH, int GW, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, scgate_fwd_kernel<T><<<egrid((long)N * H * W * C), 256, 0, st>>>((const T*)x, xps, (const T*)u3, (const T*)g, (T*)out, N, H, W, C, GH, GW));
+  const bool v = vec_ok(dtype, {C, xps}, {x, u3, g, out});
+  DISPATCH_TV(dtype, v, scgate_fwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (const T*)u3, (const T*)g, (T*)out, N, H, W, C, GH, GW));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_scgate_bwd(int dtype, const void* x, long xps, const void* u3, const void* g, const void* dout,
-                           void* du3, void* dpre, int N, int H, int W, int C, int GH, int GW, void* stream) {
+                           void* du3, void* dpre, long dpps, int accumulate, int N, int H, int W, int C, int GH, int GW,
+                           void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, scgate_bwd_kernel<T><<<egrid((long)N * H * W * C), 256, 0, st>>>((const T*)x, xps, (const T*)u3, (const T*)g, (const T*)dout, (T*)du3, (T*)dpre, N, H, W, C, GH, GW));
+  const bool v = vec_ok(dtype, {C, xps, dpps}, {x, u3, g, dout, du3, dpre});
+  DISPATCH_TV(dtype, v, scgate_bwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (const T*)u3, (const T*)g, (const T*)dout, (T*)du3, (T*)dpre, dpps, accumulate, N, H, W, C, GH, GW));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_ca_pool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, void* stream) {

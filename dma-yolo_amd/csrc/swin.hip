@@ -105,6 +105,143 @@ __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __rest
   }
 }
 
+// Vectorised LayerNorm: a row of C channels is held by L lanes (16-B vectors, L = pow2 >= C/VW),
+// 64/L rows per wave, one global read per element; backward keeps the per-channel dw/db partials
+// in registers (a thread's channels are fixed) and reduces them once per workgroup.
+template <typename T, int L>
+__global__ void __launch_bounds__(256) ln_fwd_vec(const T* __restrict__ x, long xps, const float* __restrict__ w,
+                                                  const float* __restrict__ b, T* __restrict__ y,
+                                                  float* __restrict__ mean, float* __restrict__ rstd, long M, int C,
+                                                  float eps) {
+  constexpr int VW = Traits<T>::VW, RPW = 64 / L;
+  const int lane = threadIdx.x & 63, sub = lane % L, rw = lane / L;
+  const int c0 = sub * VW;
+  const bool on = c0 < C;
+  float wv[VW], bv[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    wv[j] = on ? w[c0 + j] : 0.f;
+    bv[j] = on ? b[c0 + j] : 0.f;
+  }
+  const long rpb = (long)(blockDim.x >> 6) * RPW;
+  for (long mb = (long)blockIdx.x * rpb; mb < M; mb += (long)gridDim.x * rpb) {
+    const long m = mb + (threadIdx.x >> 6) * RPW + rw;
+    const bool ok = on && m < M;
+    float v[VW];
+    if (ok) unpack<T>(*reinterpret_cast<const uint4*>(x + m * xps + c0), v);
+    else
+#pragma unroll
+      for (int j = 0; j < VW; ++j) v[j] = 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s += v[j];
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mu = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      v[j] -= mu;
+      q += ok ? v[j] * v[j] : 0.f;
+    }
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rs = rsqrtf(q / C + eps);
+    if (ok) {
+      float o_[VW];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) o_[j] = v[j] * rs * wv[j] + bv[j];
+      *reinterpret_cast<uint4*>(y + m * C + c0) = pack<T>(o_);
+    }
+    if (sub == 0 && m < M) {
+      mean[m] = mu;
+      rstd[m] = rs;
+    }
+  }
+}
+
+template <typename T, int L>
+__global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long xps, const T* __restrict__ dy, long dps,
+                                                  const float* __restrict__ w, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd, T* __restrict__ dx, long dxps,
+                                                  long M, int C, float* __restrict__ pdw, float* __restrict__ pdb) {
+  constexpr int VW = Traits<T>::VW, RPW = 64 / L;
+  extern __shared__ float sh[];  // [2][C]
+  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) sh[c] = 0.f;
+  const int lane = threadIdx.x & 63, sub = lane % L, rw = lane / L;
+  const int c0 = sub * VW;
+  const bool on = c0 < C;
+  float wv[VW], aw[VW], ab[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    wv[j] = on ? w[c0 + j] : 0.f;
+    aw[j] = 0.f;
+    ab[j] = 0.f;
+  }
+  const long rpb = (long)(blockDim.x >> 6) * RPW;
+  for (long mb = (long)blockIdx.x * rpb; mb < M; mb += (long)gridDim.x * rpb) {
+    const long m = mb + (threadIdx.x >> 6) * RPW + rw;
+    const bool ok = on && m < M;
+    float xv[VW], gv[VW];
+    float mu = 0.f, rs = 0.f;
+    if (ok) {
+      unpack<T>(*reinterpret_cast<const uint4*>(x + m * xps + c0), xv);
+      unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gv);
+      mu = mean[m];
+      rs = rstd[m];
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) xv[j] = gv[j] = 0.f;
+    }
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      xv[j] = (xv[j] - mu) * rs;  // xhat
+      aw[j] += gv[j] * xv[j];
+      ab[j] += gv[j];
+      gv[j] *= wv[j];
+      a1 += gv[j];
+      a2 += gv[j] * xv[j];
+    }
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) {
+      a1 += __shfl_xor(a1, o, 64);
+      a2 += __shfl_xor(a2, o, 64);
+    }
+    a1 /= C;
+    a2 /= C;
+    if (ok) {
+      float o_[VW];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) o_[j] = rs * (gv[j] - a1 - xv[j] * a2);
+      *reinterpret_cast<uint4*>(dx + m * dxps + c0) = pack<T>(o_);
+    }
+  }
+  __syncthreads();
+  if (on) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      atomicAdd(&sh[c0 + j], aw[j]);
+      atomicAdd(&sh[C + c0 + j], ab[j]);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    pdw[(long)blockIdx.x * C + c] = sh[c];
+    pdb[(long)blockIdx.x * C + c] = sh[C + c];
+  }
+}
+
+// L = lanes per row (pow2 >= C / VW); 0 if the vector kernels do not apply
+template <typename T> int ln_lanes(int C, long xps, long yps, const void* x, const void* y) {
+  constexpr int VW = Traits<T>::VW;
+  if (C % VW || xps % VW || yps % VW || (((uintptr_t)x | (uintptr_t)y) & 15)) return 0;
+  const int n = C / VW;
+  int L = 4;
+  while (L < n) L <<= 1;
+  return L <= 64 ? L : 0;
+}
+
 // ---------------------------------------------------------------- window attention
 // LDS layout (floats): Q[64][33] K[64][33] V[64][33] P[64][65]
 constexpr int QS = HD + 1, PS = NTOK + 1;
@@ -308,6 +445,301 @@ __global__ void sample_scale_kernel(const T* __restrict__ x, const float* __rest
     y[i] = from_f<T>(to_f(x[i]) * sc[i / per]);
 }
 
+// ---------------------------------------------------------------- bf16 window attention on MFMA
+// Throughput mode: one wave per (window, head), NW waves per workgroup sharing one head (the
+// bias-table column is staged once per workgroup).  All six products are 16x16x32 bf16 MFMAs
+// over LDS-staged [64][32] / [64][64] bf16 tiles:
+//   fwd: S^T = K Q^T (lane holds 4 consecutive keys of one query row), softmax in registers,
+//        P -> LDS, O^T = V^T P^T;
+//   bwd: recompute P; dP^T = V dO^T; dS = P (dP - rowsum(P dP)); dV^T = dO^T P; dQ^T = K^T dS^T;
+//        dK^T = Q^T dS (scale folded into the fp32 epilogue); dS also feeds the bias-table grad.
+// Operand fragments: fr_row = 16-B row read, fr_col = transposed read (ds_read_b64_tr_b16).
+constexpr int LQ = HD + 8;      // [64][32] bf16 row stride (80 B)
+constexpr int LP = NTOK + 8;    // [64][64] bf16 row stride (144 B)
+constexpr int MATQ = NTOK * LQ;
+constexpr int MATP = NTOK * LP;
+constexpr int NTAB = (2 * WS - 1) * (2 * WS - 1);
+
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+// lane gets X[r0 + (lane&15)][k0 + 8g .. +8)   (g = lane >> 4)
+DEV bf16x8 fr_row(const bf16* X, int ld, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(X + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));
+}
+// lane gets X[k0 + 8g + e][r0 + (lane&15)], e = 0..7
+DEV bf16x8 fr_col(const bf16* X, int ld, int r0, int k0, int lane) {
+  const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3;
+  const bf16* a0 = X + (k0 + 8 * g + q) * ld + r0 + 4 * p;
+  const bf16* a1 = X + (k0 + 8 * g + 4 + q) * ld + r0 + 4 * p;
+  s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a0));
+  s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a1));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+DEV f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// 4 fp32 -> 4 bf16 as one 8-byte LDS store
+DEV void st4(bf16* dst, float a, float b, float c, float d) {
+  union { bf16 h[4]; uint2 u; } v;
+  v.h[0] = __float2bfloat16(a); v.h[1] = __float2bfloat16(b);
+  v.h[2] = __float2bfloat16(c); v.h[3] = __float2bfloat16(d);
+  *reinterpret_cast<uint2*>(dst) = v.u;
+}
+
+// lane t = token: gather the head slice (32 bf16 = 4 x 16 B) of `nm` matrices at column offsets
+// off[m] into LDS rows; padding tokens read as zeros.  Returns the token's pixel (-1 = padding).
+DEV long load_tok(const bf16* src, long sps, const SwinGeom& g, int b, int wr, int wc, int lane, int nm,
+                  const long* off, bf16* const* dst) {
+  const long p = tok_pixel(g, b, wr, wc, lane);
+  for (int m = 0; m < nm; ++m) {
+    const uint4* s = reinterpret_cast<const uint4*>(src + (p >= 0 ? p : 0) * sps + off[m]);
+    uint4* d = reinterpret_cast<uint4*>(dst[m] + lane * LQ);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) d[c] = p >= 0 ? s[c] : make_uint4(0, 0, 0, 0);
+  }
+  return p;
+}
+
+// S^T tiles (lane: query q = 16bq + il, keys 16bk + 4g + r) -> scaled, biased, masked -> softmax.
+// P[bq][bk][r] in fp32 on return.
+DEV void softmax_t(const bf16* Qs, const bf16* Ks, const float* tab, const SwinGeom& g, int wr, int wc, int lane,
+                   float (&P)[4][4][4]) {
+  const int il = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int bq = 0; bq < 4; ++bq) {
+    const bf16x8 qf = fr_row(Qs, LQ, 16 * bq, 0, lane);
+    const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
+    const int lq = g.shift > 0 ? win_label(wr * WS + ri, wc * WS + ci, g.Rp, g.Cp, g.shift) : 0;
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk) {
+      f32x4 acc = mma(fr_row(Ks, LQ, 16 * bk, 0, lane), qf, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
+        float v = acc[r] * g.scale + tab[(ri - rj + WS - 1) * (2 * WS - 1) + (ci - cj + WS - 1)];
+        if (g.shift > 0 && win_label(wr * WS + rj, wc * WS + cj, g.Rp, g.Cp, g.shift) != lq) v += -100.0f;
+        P[bq][bk][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        P[bq][bk][r] = __expf(P[bq][bk][r] - mx);
+        sum += P[bq][bk][r];
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[bq][bk][r] *= inv;
+  }
+}
+
+// P (registers, S^T layout) -> Ps[q][k] bf16
+DEV void store_p(bf16* Ps, const float (&P)[4][4][4], int lane) {
+  const int il = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int bq = 0; bq < 4; ++bq)
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk)
+      st4(Ps + (16 * bq + il) * LP + 16 * bk + 4 * gq, P[bq][bk][0], P[bq][bk][1], P[bq][bk][2], P[bq][bk][3]);
+}
+
+// acc tiles X^T[d = 16dt + 4g + r][t = 16bt + il] -> Xs[t][d] (LQ rows)
+DEV void store_t(bf16* Xs, const f32x4 (&A)[2][4], float scale, int lane) {
+  const int il = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt)
+      st4(Xs + (16 * bt + il) * LQ + 16 * dt + 4 * gq, A[dt][bt][0] * scale, A[dt][bt][1] * scale,
+          A[dt][bt][2] * scale, A[dt][bt][3] * scale);
+}
+
+// lane t = token: 4 x 16 B of the staged row -> dst[p * dps + off]
+DEV void store_tok(const bf16* Xs, bf16* dst, long dps, long off, long p, int lane) {
+  if (p < 0) return;
+  const uint4* s = reinterpret_cast<const uint4*>(Xs + lane * LQ);
+  uint4* d = reinterpret_cast<uint4*>(dst + p * dps + off);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) d[c] = s[c];
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) winattn_fwd_mfma(const bf16* __restrict__ qkv,
+                                                            const float* __restrict__ table, bf16* __restrict__ out,
+                                                            SwinGeom g, int nwin) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (3 * MATQ + MATP)];
+  __shared__ float tab[NTAB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, head = blockIdx.y;
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) tab[e] = table[e * g.nh + head];
+  const int wid = blockIdx.x * NW + w;
+  const bool live = wid < nwin;
+  const int nwr = g.Rp / WS, nwc = g.Cp / WS;
+  const int b = live ? wid / (nwr * nwc) : 0, wr = (wid / nwc) % nwr, wc = wid % nwc;
+  bf16* Qs = sm + w * (3 * MATQ + MATP);
+  bf16* Ks = Qs + MATQ;
+  bf16* Vs = Ks + MATQ;
+  bf16* Ps = Vs + MATQ;
+  long p = -1;
+  if (live) {
+    const long off[3] = {(long)head * HD, (long)g.C + head * HD, 2L * g.C + head * HD};
+    bf16* const dst[3] = {Qs, Ks, Vs};
+    p = load_tok(qkv, 3L * g.C, g, b, wr, wc, lane, 3, off, dst);
+  }
+  __syncthreads();
+  if (live) {
+    float P[4][4][4];
+    softmax_t(Qs, Ks, tab, g, wr, wc, lane, P);
+    store_p(Ps, P, lane);
+  }
+  __syncthreads();
+  if (live) {
+    // O^T[d][q] = sum_k V[k][d] P[q][k]
+    f32x4 O[2][4];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int bq = 0; bq < 4; ++bq) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc = mma(fr_col(Vs, LQ, 16 * dt, 32 * c, lane), fr_row(Ps, LP, 16 * bq, 32 * c, lane), acc);
+        O[dt][bq] = acc;
+      }
+    store_t(Qs, O, 1.f, lane);  // Q no longer needed
+  }
+  __syncthreads();
+  if (live) store_tok(Qs, out, g.C, (long)head * HD, p, lane);
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                            const float* __restrict__ table, bf16* __restrict__ dqkv,
+                                                            float* __restrict__ dtab_part, int nwin, int wpb, SwinGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (4 * MATQ + MATP)];
+  __shared__ float tab[NTAB], dtab[NTAB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, head = blockIdx.y;
+  const int il = lane & 15, gq = lane >> 4;
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) {
+    tab[e] = table[e * g.nh + head];
+    dtab[e] = 0.f;
+  }
+  const int nwr = g.Rp / WS, nwc = g.Cp / WS;
+  bf16* Qs = sm + w * (4 * MATQ + MATP);
+  bf16* Ks = Qs + MATQ;
+  bf16* Vs = Ks + MATQ;
+  bf16* Ds = Vs + MATQ;  // dO
+  bf16* Ps = Ds + MATQ;  // P, then dS
+  const int w0 = blockIdx.x * wpb, w1 = min(nwin, w0 + wpb);
+  for (int base = w0; base < w1; base += NW) {
+    const int wid = base + w;
+    const bool live = wid < w1;
+    const int b = live ? wid / (nwr * nwc) : 0, wr = (wid / nwc) % nwr, wc = wid % nwc;
+    long p = -1;
+    __syncthreads();
+    if (live) {
+      const long off[3] = {(long)head * HD, (long)g.C + head * HD, 2L * g.C + head * HD};
+      bf16* const dst[3] = {Qs, Ks, Vs};
+      p = load_tok(qkv, 3L * g.C, g, b, wr, wc, lane, 3, off, dst);
+      const long offd[1] = {(long)head * HD};
+      bf16* const dstd[1] = {Ds};
+      load_tok(dout, g.C, g, b, wr, wc, lane, 1, offd, dstd);
+    }
+    __syncthreads();
+    float P[4][4][4];
+    if (live) {
+      softmax_t(Qs, Ks, tab, g, wr, wc, lane, P);
+      store_p(Ps, P, lane);
+    }
+    __syncthreads();
+    f32x4 dV[2][4], dQ[2][4], dK[2][4];
+    if (live) {
+      // dV^T[d][k] = sum_q dO[q][d] P[q][k]
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int bk = 0; bk < 4; ++bk) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 2; ++c) acc = mma(fr_col(Ds, LQ, 16 * dt, 32 * c, lane), fr_col(Ps, LP, 16 * bk, 32 * c, lane), acc);
+          dV[dt][bk] = acc;
+        }
+      // dP^T[k][q] = V[k] . dO[q]  (same layout as P);  dS = P (dP - sum_k P dP)
+#pragma unroll
+      for (int bq = 0; bq < 4; ++bq) {
+        const bf16x8 df = fr_row(Ds, LQ, 16 * bq, 0, lane);
+        float dp[4][4];
+        float rs = 0.f;
+#pragma unroll
+        for (int bk = 0; bk < 4; ++bk) {
+          f32x4 acc = mma(fr_row(Vs, LQ, 16 * bk, 0, lane), df, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dp[bk][r] = acc[r];
+            rs += acc[r] * P[bq][bk][r];
+          }
+        }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
+#pragma unroll
+        for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float ds = P[bq][bk][r] * (dp[bk][r] - rs);
+            P[bq][bk][r] = ds;
+            const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
+            atomicAdd(&dtab[(ri - rj + WS - 1) * (2 * WS - 1) + (ci - cj + WS - 1)], ds);
+          }
+      }
+    }
+    __syncthreads();  // all fr_col reads of P done before dS overwrites it
+    if (live) store_p(Ps, P, lane);
+    __syncthreads();
+    if (live) {
+      // dQ^T[d][q] = sum_k K[k][d] dS[q][k];  dK^T[d][k] = sum_q Q[q][d] dS[q][k]
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+          f32x4 aq = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            aq = mma(fr_col(Ks, LQ, 16 * dt, 32 * c, lane), fr_row(Ps, LP, 16 * bt, 32 * c, lane), aq);
+            ak = mma(fr_col(Qs, LQ, 16 * dt, 32 * c, lane), fr_col(Ps, LP, 16 * bt, 32 * c, lane), ak);
+          }
+          dQ[dt][bt] = aq;
+          dK[dt][bt] = ak;
+        }
+    }
+    __syncthreads();
+    if (live) {
+      store_t(Qs, dQ, g.scale, lane);
+      store_t(Ks, dK, g.scale, lane);
+      store_t(Vs, dV, 1.f, lane);
+    }
+    __syncthreads();
+    if (live) {
+      store_tok(Qs, dqkv, 3L * g.C, (long)head * HD, p, lane);
+      store_tok(Ks, dqkv, 3L * g.C, (long)g.C + head * HD, p, lane);
+      store_tok(Vs, dqkv, 3L * g.C, 2L * g.C + head * HD, p, lane);
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) dtab_part[((long)blockIdx.x * g.nh + head) * NTAB + e] = dtab[e];
+}
+
 SwinGeom make(int B, int H, int W, int C, int nh, int shift, float scale) {
   SwinGeom g;
   g.B = B; g.H = H; g.W = W; g.C = C; g.nh = nh; g.shift = shift; g.scale = scale;
@@ -318,34 +750,75 @@ SwinGeom make(int B, int H, int W, int C, int nh, int shift, float scale) {
 
 }  // namespace
 
+template <typename T>
+int ln_fwd_t(const T* x, long xps, const float* w, const float* b, T* y, float* mean, float* rstd, long M, int C,
+             float eps, hipStream_t st) {
+  const int L = ln_lanes<T>(C, xps, C, x, y);
+  if (L) {
+    const int g = grid_cap(ceil_div(M, 4L * (64 / L)), 8192);
+    switch (L) {
+      case 4: ln_fwd_vec<T, 4><<<g, 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps); break;
+      case 8: ln_fwd_vec<T, 8><<<g, 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps); break;
+      case 16: ln_fwd_vec<T, 16><<<g, 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps); break;
+      case 32: ln_fwd_vec<T, 32><<<g, 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps); break;
+      default: ln_fwd_vec<T, 64><<<g, 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps); break;
+    }
+  } else {
+    ln_fwd_kernel<T><<<grid_cap(ceil_div(M, 4), 4096), 256, 0, st>>>(x, xps, w, b, y, mean, rstd, M, C, eps);
+  }
+  return (int)hipGetLastError();
+}
+
 DMY_API int dmy_layernorm_fwd(int dtype, const void* x, long xps, const float* w, const float* b, void* y, float* mean,
                               float* rstd, long M, int C, float eps, void* stream) {
-  const int g = grid_cap(ceil_div(M, 4), 4096);
-  if (dtype) ln_fwd_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>((const bf16*)x, xps, w, b, (bf16*)y, mean, rstd, M, C, eps);
-  else ln_fwd_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)x, xps, w, b, (float*)y, mean, rstd, M, C, eps);
-  return (int)hipGetLastError();
+  if (dtype) return ln_fwd_t<bf16>((const bf16*)x, xps, w, b, (bf16*)y, mean, rstd, M, C, eps, (hipStream_t)stream);
+  return ln_fwd_t<float>((const float*)x, xps, w, b, (float*)y, mean, rstd, M, C, eps, (hipStream_t)stream);
 }
 
 DMY_API int dmy_layernorm_bwd_blocks(long M) { return grid_cap(ceil_div(M, 64), 1024); }
 
+template <typename T>
+int ln_bwd_t(const T* x, long xps, const T* dy, long dps, const float* w, const float* mean, const float* rstd, T* dx,
+             long dxps, long M, int C, float* pdw, float* pdb, hipStream_t st) {
+  const int P = dmy_layernorm_bwd_blocks(M);
+  const size_t lds = 2 * sizeof(float) * C;
+  int L = ln_lanes<T>(C, xps, dxps, x, dx);
+  if (L && (dps % Traits<T>::VW || ((uintptr_t)dy & 15))) L = 0;
+  switch (L) {
+    case 4: ln_bwd_vec<T, 4><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    case 8: ln_bwd_vec<T, 8><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    case 16: ln_bwd_vec<T, 16><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    case 32: ln_bwd_vec<T, 32><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    case 64: ln_bwd_vec<T, 64><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    default: {
+      const int rpb = (int)((M + P - 1) / P);
+      ln_bwd_kernel<T><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, rpb, pdw, pdb);
+    }
+  }
+  return (int)hipGetLastError();
+}
+
 DMY_API int dmy_layernorm_bwd(int dtype, const void* x, long xps, const void* dy, long dps, const float* w,
                               const float* mean, const float* rstd, void* dx, long dxps, long M, int C, float* pdw,
                               float* pdb, void* stream) {
-  const int P = dmy_layernorm_bwd_blocks(M);
-  const int rpb = (int)((M + P - 1) / P);
-  const size_t lds = 2 * sizeof(float) * C;
-  if (dtype) ln_bwd_kernel<bf16><<<P, 256, lds, (hipStream_t)stream>>>((const bf16*)x, xps, (const bf16*)dy, dps, w, mean, rstd, (bf16*)dx, dxps, M, C, rpb, pdw, pdb);
-  else ln_bwd_kernel<float><<<P, 256, lds, (hipStream_t)stream>>>((const float*)x, xps, (const float*)dy, dps, w, mean, rstd, (float*)dx, dxps, M, C, rpb, pdw, pdb);
-  return (int)hipGetLastError();
+  if (dtype)
+    return ln_bwd_t<bf16>((const bf16*)x, xps, (const bf16*)dy, dps, w, mean, rstd, (bf16*)dx, dxps, M, C, pdw, pdb,
+                          (hipStream_t)stream);
+  return ln_bwd_t<float>((const float*)x, xps, (const float*)dy, dps, w, mean, rstd, (float*)dx, dxps, M, C, pdw, pdb,
+                         (hipStream_t)stream);
 }
 
 DMY_API int dmy_winattn_fwd(int dtype, const void* qkv, const float* table, void* out, int B, int H, int W, int C,
                             int nh, int shift, float scale, void* stream) {
   if (C != nh * HD) return (int)hipErrorInvalidValue;
   SwinGeom g = make(B, H, W, C, nh, shift, scale);
-  dim3 grid(B * (g.Rp / WS) * (g.Cp / WS), nh);
-  if (dtype) winattn_fwd_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)qkv, table, (bf16*)out, g);
-  else winattn_fwd_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)qkv, table, (float*)out, g);
+  const int nwin = B * (g.Rp / WS) * (g.Cp / WS);
+  dim3 grid(nwin, nh);
+  if (dtype) {
+    constexpr int NW = 2;
+    dim3 gm(ceil_div(nwin, NW), nh);
+    winattn_fwd_mfma<NW><<<gm, 64 * NW, 0, (hipStream_t)stream>>>((const bf16*)qkv, table, (bf16*)out, g, nwin);
+  } else winattn_fwd_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)qkv, table, (float*)out, g);
   return (int)hipGetLastError();
 }
 
@@ -368,7 +841,7 @@ DMY_API int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const 
   const int wpb = (nwin + groups - 1) / groups;
   dim3 grid(groups, nh);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype) winattn_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)qkv, (const bf16*)dout, table, (bf16*)dqkv, dtab_part, nwin, wpb, g);
+  if (dtype) winattn_bwd_mfma<2><<<grid, 128, 0, st>>>((const bf16*)qkv, (const bf16*)dout, table, (bf16*)dqkv, dtab_part, nwin, wpb, g);
   else winattn_bwd_kernel<float><<<grid, 256, 0, st>>>((const float*)qkv, (const float*)dout, table, (float*)dqkv, dtab_part, nwin, wpb, g);
   const int ntab = (2 * WS - 1) * (2 * WS - 1) * nh;
   dtab_reduce_kernel<<<ceil_div(ntab, 256), 256, 0, st>>>(dtab_part, groups, nh, dtab);

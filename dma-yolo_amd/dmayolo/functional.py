@@ -414,8 +414,8 @@ class SCGateFn(torch.autograd.Function):
         dout = dout.contiguous(memory_format=CL)
         du3 = new_act(N, C, H, W, x)
         dpre = new_act(N, C, H, W, x)
-        call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), N, H, W, C,
-             GH, GW, stream())
+        call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), C, 0, N, H,
+             W, C, GH, GW, stream())
         dg = new_act(N, C, GH, GW, x)
         call('dmy_resize_bwd', dcode(x), ptr(dpre), C, ptr(dg), C, N, GH, GW, H, W, C, stream())
         return dpre, du3, dg

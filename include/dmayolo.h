@@ -89,7 +89,7 @@ int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* w, float e
 int dmy_scgate_fwd(int dtype, const void* x, long xps, const void* u3, const void* g, void* out, int N, int H, int W,
                    int C, int GH, int GW, void* stream);
 int dmy_scgate_bwd(int dtype, const void* x, long xps, const void* u3, const void* g, const void* dout, void* du3,
-                   void* dpre, int N, int H, int W, int C, int GH, int GW, void* stream);
+                   void* dpre, long dpps, int accumulate, int N, int H, int W, int C, int GH, int GW, void* stream);
 /* CoorAttention pooling + re-weighting: common.py:1183-1207 */
 int dmy_ca_pool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, void* stream);
 int dmy_ca_pool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C,
