@@ -69,8 +69,8 @@ __global__ void ln_fwd_kernel(const T* __restrict__ x, long xps, const float* __
 template <typename T>
 __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ dy, long dps,
                               const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
-                              T* __restrict__ dx, long dxps, long M, int C, int rows_per_block, float* __restrict__ pdw,
-                              float* __restrict__ pdb) {
+                              T* __restrict__ dx, long dxps, int accumulate, long M, int C, int rows_per_block,
+                              float* __restrict__ pdw, float* __restrict__ pdb) {
   extern __shared__ float sh[];  // [2][C]
   float* sdw = sh;
   float* sdb = sh + C;
@@ -95,7 +95,8 @@ __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __rest
     for (int c = lane; c < C; c += 64) {
       const float xh = (to_f(x[m * xps + c]) - mu) * rs;
       const float g = to_f(dy[m * dps + c]) * w[c];
-      dx[m * dxps + c] = from_f<T>(rs * (g - a1 - xh * a2));
+      const float v = rs * (g - a1 - xh * a2);
+      dx[m * dxps + c] = from_f<T>(accumulate ? v + to_f(dx[m * dxps + c]) : v);
     }
   }
   __syncthreads();
@@ -164,7 +165,8 @@ template <typename T, int L>
 __global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long xps, const T* __restrict__ dy, long dps,
                                                   const float* __restrict__ w, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, T* __restrict__ dx, long dxps,
-                                                  long M, int C, float* __restrict__ pdw, float* __restrict__ pdb) {
+                                                  int accumulate, long M, int C, float* __restrict__ pdw,
+                                                  float* __restrict__ pdb) {
   constexpr int VW = Traits<T>::VW, RPW = 64 / L;
   extern __shared__ float sh[];  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) sh[c] = 0.f;
@@ -211,9 +213,10 @@ __global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long 
     a1 /= C;
     a2 /= C;
     if (ok) {
-      float o_[VW];
+      float o_[VW], p_[VW];
+      if (accumulate) unpack<T>(*reinterpret_cast<const uint4*>(dx + m * dxps + c0), p_);
 #pragma unroll
-      for (int j = 0; j < VW; ++j) o_[j] = rs * (gv[j] - a1 - xv[j] * a2);
+      for (int j = 0; j < VW; ++j) o_[j] = rs * (gv[j] - a1 - xv[j] * a2) + (accumulate ? p_[j] : 0.f);
       *reinterpret_cast<uint4*>(dx + m * dxps + c0) = pack<T>(o_);
     }
   }
@@ -779,33 +782,33 @@ DMY_API int dmy_layernorm_bwd_blocks(long M) { return grid_cap(ceil_div(M, 64), 
 
 template <typename T>
 int ln_bwd_t(const T* x, long xps, const T* dy, long dps, const float* w, const float* mean, const float* rstd, T* dx,
-             long dxps, long M, int C, float* pdw, float* pdb, hipStream_t st) {
+             long dxps, int acc, long M, int C, float* pdw, float* pdb, hipStream_t st) {
   const int P = dmy_layernorm_bwd_blocks(M);
   const size_t lds = 2 * sizeof(float) * C;
   int L = ln_lanes<T>(C, xps, dxps, x, dx);
   if (L && (dps % Traits<T>::VW || ((uintptr_t)dy & 15))) L = 0;
   switch (L) {
-    case 4: ln_bwd_vec<T, 4><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
-    case 8: ln_bwd_vec<T, 8><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
-    case 16: ln_bwd_vec<T, 16><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
-    case 32: ln_bwd_vec<T, 32><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
-    case 64: ln_bwd_vec<T, 64><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, pdw, pdb); break;
+    case 4: ln_bwd_vec<T, 4><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, pdw, pdb); break;
+    case 8: ln_bwd_vec<T, 8><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, pdw, pdb); break;
+    case 16: ln_bwd_vec<T, 16><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, pdw, pdb); break;
+    case 32: ln_bwd_vec<T, 32><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, pdw, pdb); break;
+    case 64: ln_bwd_vec<T, 64><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, pdw, pdb); break;
     default: {
       const int rpb = (int)((M + P - 1) / P);
-      ln_bwd_kernel<T><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, M, C, rpb, pdw, pdb);
+      ln_bwd_kernel<T><<<P, 256, lds, st>>>(x, xps, dy, dps, w, mean, rstd, dx, dxps, acc, M, C, rpb, pdw, pdb);
     }
   }
   return (int)hipGetLastError();
 }
 
 DMY_API int dmy_layernorm_bwd(int dtype, const void* x, long xps, const void* dy, long dps, const float* w,
-                              const float* mean, const float* rstd, void* dx, long dxps, long M, int C, float* pdw,
-                              float* pdb, void* stream) {
+                              const float* mean, const float* rstd, void* dx, long dxps, int accumulate, long M, int C,
+                              float* pdw, float* pdb, void* stream) {
   if (dtype)
-    return ln_bwd_t<bf16>((const bf16*)x, xps, (const bf16*)dy, dps, w, mean, rstd, (bf16*)dx, dxps, M, C, pdw, pdb,
-                          (hipStream_t)stream);
-  return ln_bwd_t<float>((const float*)x, xps, (const float*)dy, dps, w, mean, rstd, (float*)dx, dxps, M, C, pdw, pdb,
-                         (hipStream_t)stream);
+    return ln_bwd_t<bf16>((const bf16*)x, xps, (const bf16*)dy, dps, w, mean, rstd, (bf16*)dx, dxps, accumulate, M, C,
+                          pdw, pdb, (hipStream_t)stream);
+  return ln_bwd_t<float>((const float*)x, xps, (const float*)dy, dps, w, mean, rstd, (float*)dx, dxps, accumulate, M,
+                         C, pdw, pdb, (hipStream_t)stream);
 }
 
 DMY_API int dmy_winattn_fwd(int dtype, const void* qkv, const float* table, void* out, int B, int H, int W, int C,

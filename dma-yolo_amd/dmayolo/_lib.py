@@ -71,7 +71,7 @@ SIGNATURES = {
     # swin.hip
     'dmy_layernorm_fwd': [I, P, L, P, P, P, P, P, L, I, F, P],
     'dmy_layernorm_bwd_blocks': [L],
-    'dmy_layernorm_bwd': [I, P, L, P, L, P, P, P, P, L, L, I, P, P, P],
+    'dmy_layernorm_bwd': [I, P, L, P, L, P, P, P, P, L, I, L, I, P, P, P],
     'dmy_winattn_fwd': [I, P, P, P, I, I, I, I, I, I, F, P],
     'dmy_winattn_bwd_groups': [I, I, I, I],
     'dmy_winattn_bwd': [I, P, P, P, P, P, P, I, I, I, I, I, I, F, P],

@@ -42,6 +42,67 @@ def f32(n, dev):
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
+class GradSink:
+    """Input-gradient accumulator for an activation with several consumers inside one module.
+
+    Autograd would sum the consumers' gradient contributions with separate add kernels.  Here
+    the consumers' backward kernels write (first contribution in backward order) or accumulate
+    (the rest, through the kernels' accumulate flags) into one NHWC buffer, and only the LAST of
+    the `n` contributions hands the finished buffer to autograd (the others return None).  The
+    activation's producer runs only after all of its consumers' backwards, and any contribution
+    from outside the module is added by autograd to the finished buffer.  The sink resets after
+    the n-th contribution, so a retained graph can run backward again.
+    """
+    __slots__ = ('n', 'seen', 'buf', 'ps')
+
+    def __init__(self, n):
+        self.n, self.seen, self.buf, self.ps = n, 0, None, 0
+
+    def _tick(self):
+        self.seen += 1
+        if self.seen < self.n:
+            return None
+        ret = self.buf
+        self.buf, self.seen = None, 0
+        return ret
+
+    def target(self, N, C, H, W, like):
+        """-> (buffer, pixel stride, accumulate flag, tensor to hand to autograd or None); call
+        `done()` after the kernel has been launched"""
+        if self.buf is None:
+            self.buf, self.ps = new_act(N, C, H, W, like), C
+            return self.buf, C, 0
+        return self.buf, self.ps, 1
+
+    def done(self):
+        return self._tick()
+
+    def passthrough(self, g):
+        """identity contribution (a residual / concat slice): adopt g as the buffer, or add it in.
+        Adoption is safe for the residual pattern: every other reader of g lies inside the branch,
+        whose backwards all finish before the branch's first consumer accumulates into g."""
+        g, gps = pixel_stride(g)
+        if self.buf is None:
+            self.buf, self.ps = g, gps
+        else:
+            N, C, H, W = g.shape
+            call('dmy_slice_copy', dcode(g), ptr(g), gps, ptr(self.buf), self.ps, N * H * W, C, None, 0, 0, 0.0, 1,
+                 stream())
+        return self._tick()
+
+
+def sink_target(sink, N, C, H, W, like):
+    """-> (buffer, pixel stride, accumulate flag) for an input gradient; see sink_result"""
+    if sink is None:
+        return new_act(N, C, H, W, like), C, 0
+    return sink.target(N, C, H, W, like)
+
+
+def sink_result(sink, buf):
+    """what the backward returns for that input: its own buffer, or the sink's verdict"""
+    return buf if sink is None else sink.done()
+
+
 # ------------------------------------------------------------------ convolution (+BN +act)
 
 class ConvSpec:
@@ -121,7 +182,7 @@ def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
 
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, gamma, beta, res, spec):
+    def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None):
         cpad = zero_padded_channels(x)
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
@@ -189,6 +250,7 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
         ctx.cp = Cp
         ctx.has_bias = bias is not None
+        ctx.xsink, ctx.rsink = xsink, rsink
         return y
 
     @staticmethod
@@ -243,38 +305,42 @@ class ConvBNActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if Cp != C:
                 raise NotImplementedError('input gradient of a channel-padded stem conv')
-            dx = new_act(N, C, H, W, z)
-            KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(dx), 0,
-                            N, H, W, C, C, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s))
+            buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
+            KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf),
+                            acc, N, H, W, C, bps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s))
+            dx = sink_result(ctx.xsink, buf)
         if ctx.needs_input_grad[1]:
             dwo = f32(K * Cp * k * k, dev)
             KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
                             H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s))
             dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
             call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
-        dres = dy if ctx.has_res else None
-        return dx, dw, dbias, dgamma, dbeta, dres, None
+        dres = None
+        if ctx.has_res:
+            dres = dy if ctx.rsink is None else ctx.rsink.passthrough(dy)
+        return dx, dw, dbias, dgamma, dbeta, dres, None, None, None
 
 
-def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None):
+def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None):
+    """xsink / rsink: GradSinks collecting the gradient of x / of the residual (see GradSink)."""
     spec = spec or ConvSpec(stride, pad, act, bn)
     gamma = bn.weight if bn is not None else None
     beta = bn.bias if bn is not None else None
-    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec)
+    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec, xsink, rsink)
 
 
 # ------------------------------------------------------------------ pooling / resize / concat
 
 class MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k):
+    def forward(ctx, x, k, sink=None):
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
         y = new_act(N, C, H, W, x)
         arg = torch.empty((N, H, W, C), dtype=torch.uint8, device=x.device)
         call('dmy_maxpool_fwd', dcode(x), ptr(x), xps, ptr(y), C, ptr(arg), N, H, W, C, k, stream())
         ctx.save_for_backward(arg)
-        ctx.k, ctx.shape = k, (N, C, H, W)
+        ctx.k, ctx.shape, ctx.sink = k, (N, C, H, W), sink
         return y
 
     @staticmethod
@@ -282,28 +348,28 @@ class MaxPoolFn(torch.autograd.Function):
         (arg,) = ctx.saved_tensors
         N, C, H, W = ctx.shape
         dy, dps = pixel_stride(dy)
-        dx = new_act(N, C, H, W, dy)
-        call('dmy_maxpool_bwd', dcode(dy), ptr(dy), dps, ptr(arg), ptr(dx), C, 0, N, H, W, C, ctx.k, stream())
-        return dx, None
+        buf, bps, acc = sink_target(ctx.sink, N, C, H, W, dy)
+        call('dmy_maxpool_bwd', dcode(dy), ptr(dy), dps, ptr(arg), ptr(buf), bps, acc, N, H, W, C, ctx.k, stream())
+        return sink_result(ctx.sink, buf), None, None
 
 
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r):
+    def forward(ctx, x, r, sink=None):
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
         y = new_act(N, C, H // r, W // r, x)
         call('dmy_avgpool_fwd', dcode(x), ptr(x), xps, ptr(y), N, H, W, C, r, stream())
-        ctx.r, ctx.shape = r, (N, C, H, W)
+        ctx.r, ctx.shape, ctx.sink = r, (N, C, H, W), sink
         return y
 
     @staticmethod
     def backward(ctx, dy):
         N, C, H, W = ctx.shape
         dy = dy.contiguous(memory_format=CL)
-        dx = new_act(N, C, H, W, dy)
-        call('dmy_avgpool_bwd', dcode(dy), ptr(dy), ptr(dx), C, 0, N, H, W, C, ctx.r, stream())
-        return dx, None
+        buf, bps, acc = sink_target(ctx.sink, N, C, H, W, dy)
+        call('dmy_avgpool_bwd', dcode(dy), ptr(dy), ptr(buf), bps, acc, N, H, W, C, ctx.r, stream())
+        return sink_result(ctx.sink, buf), None, None
 
 
 class ResizeFn(torch.autograd.Function):
@@ -331,7 +397,9 @@ class ConcatFn(torch.autograd.Function):
     """cat(w_i/(sum w + eps) * x_i) along channels (w=None: plain Concat)."""
 
     @staticmethod
-    def forward(ctx, w, eps, *xs):
+    def forward(ctx, w, eps, sinks, *xs):
+        """sinks: None or one GradSink-or-None per input (the slice gradient is handed to it)"""
+        ctx.sinks = sinks
         xs = [pixel_stride(x) for x in xs]
         N, _, H, W = xs[0][0].shape
         Ct = sum(x.shape[1] for x, _ in xs)
@@ -358,20 +426,23 @@ class ConcatFn(torch.autograd.Function):
         N, Ct, H, W = dy.shape
         M = N * H * W
         grads, c0 = [], 0
+        sinks = ctx.sinks or [None] * len(ctx.chans)
         if not ctx.has_w:
-            for C in ctx.chans:
-                grads.append(dy[:, c0:c0 + C])
+            for C, sk in zip(ctx.chans, sinks):
+                sl = dy[:, c0:c0 + C]
+                grads.append(sl if sk is None else sk.passthrough(sl))
                 c0 += C
-            return (None, None, *grads)
+            return (None, None, None, *grads)
         w, *xs = ctx.saved_tensors
         nb = call('dmy_dot_partial_blocks', M, max(ctx.chans))
         part = torch.zeros((len(xs), nb), dtype=torch.float32, device=dy.device)
         for i, (x, C) in enumerate(zip(xs, ctx.chans)):
             x, xps = pixel_stride(x)
-            g = new_act(N, C, H, W, dy)
+            g, gps, acc = sink_target(sinks[i], N, C, H, W, dy)
             sl = dy[:, c0:c0 + C]
-            call('dmy_slice_copy', dcode(dy), ptr(sl), dps, ptr(g), C, M, C, ptr(w), i, len(xs), float(ctx.eps), 0,
+            call('dmy_slice_copy', dcode(dy), ptr(sl), dps, ptr(g), gps, M, C, ptr(w), i, len(xs), float(ctx.eps), acc,
                  stream())
+            g = sink_result(sinks[i], g)
             nbi = call('dmy_dot_partial_blocks', M, C)
             call('dmy_dot_partial', dcode(dy), ptr(sl), dps, ptr(x), xps, M, C, ptr(part[i]), stream())
             if nbi < nb:
@@ -380,7 +451,7 @@ class ConcatFn(torch.autograd.Function):
             c0 += C
         dw = torch.empty_like(w)
         call('dmy_bifpn_wgrad', ptr(part), nb, len(xs), ptr(w), float(ctx.eps), ptr(dw), stream())
-        return (dw, None, *grads)
+        return (dw, None, None, *grads)
 
 
 def ctypes_off(t, c0):
@@ -394,7 +465,8 @@ class SCGateFn(torch.autograd.Function):
     """out = u3 * sigmoid(x + nearest(g))  (models/common.py:1311-1314)."""
 
     @staticmethod
-    def forward(ctx, x, u3, g):
+    def forward(ctx, x, u3, g, sink=None):
+        ctx.sink = sink
         x, xps = pixel_stride(x)
         u3 = u3.contiguous(memory_format=CL)
         g = g.contiguous(memory_format=CL)
@@ -413,12 +485,14 @@ class SCGateFn(torch.autograd.Function):
         GH, GW = g.shape[2:]
         dout = dout.contiguous(memory_format=CL)
         du3 = new_act(N, C, H, W, x)
+        # d(x + up(g)) -> x's gradient sink; the resize backward of g needs it on its own
         dpre = new_act(N, C, H, W, x)
         call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), C, 0, N, H,
              W, C, GH, GW, stream())
         dg = new_act(N, C, GH, GW, x)
         call('dmy_resize_bwd', dcode(x), ptr(dpre), C, ptr(dg), C, N, GH, GW, H, W, C, stream())
-        return dpre, du3, dg
+        dx = dpre if ctx.sink is None else ctx.sink.passthrough(dpre)
+        return dx, du3, dg, None
 
 
 class CAPoolFn(torch.autograd.Function):
@@ -474,7 +548,8 @@ class CAApplyFn(torch.autograd.Function):
 
 class AddFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b):
+    def forward(ctx, a, b, asink=None):
+        ctx.asink = asink
         a = a.contiguous(memory_format=CL) if a.dim() == 4 else a.contiguous()
         b = b.contiguous(memory_format=CL) if b.dim() == 4 else b.contiguous()
         y = torch.empty_like(a)
@@ -483,7 +558,8 @@ class AddFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        return dy, dy
+        da = dy if ctx.asink is None else ctx.asink.passthrough(dy)
+        return da, dy, None
 
 
 class ToNHWC(torch.autograd.Function):
@@ -522,7 +598,8 @@ class LayerNormFn(torch.autograd.Function):
     """nn.LayerNorm over channels of an NHWC activation (common.py:560, 565)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, eps):
+    def forward(ctx, x, w, b, eps, sink=None):
+        ctx.sink = sink
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -540,15 +617,16 @@ class LayerNormFn(torch.autograd.Function):
         N, C, H, W = x.shape
         M = N * H * W
         dy, dps = pixel_stride(dy)
-        dx = new_act(N, C, H, W, x)
+        buf, bps, acc = sink_target(ctx.sink, N, C, H, W, x)
         P = call('dmy_layernorm_bwd_blocks', M)
         pdw, pdb = f32(P * C, x.device), f32(P * C, x.device)
-        call('dmy_layernorm_bwd', dcode(x), ptr(x), ctx.xps, ptr(dy), dps, ptr(w), ptr(mean), ptr(rstd), ptr(dx), C,
-             M, C, ptr(pdw), ptr(pdb), stream())
+        call('dmy_layernorm_bwd', dcode(x), ptr(x), ctx.xps, ptr(dy), dps, ptr(w), ptr(mean), ptr(rstd), ptr(buf), bps,
+             acc, M, C, ptr(pdw), ptr(pdb), stream())
+        dx = sink_result(ctx.sink, buf)
         dw, db = f32(C, x.device), f32(C, x.device)
         call('dmy_reduce_rows', ptr(pdw), P, C, ptr(dw), 0, stream())
         call('dmy_reduce_rows', ptr(pdb), P, C, ptr(db), 0, stream())
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class WinAttnFn(torch.autograd.Function):

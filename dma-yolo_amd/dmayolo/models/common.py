@@ -45,11 +45,13 @@ def _pad_int(p):
     return p if isinstance(p, int) else p[0]
 
 
-def conv_forward(conv, bn, act, x, res=None):
-    """conv (nn.Conv2d, groups=1, dilation=1) -> optional BN -> act (+ residual) on the HIP path."""
+def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None):
+    """conv (nn.Conv2d, groups=1, dilation=1) -> optional BN -> act (+ residual) on the HIP path.
+    xsink / rsink: Fn.GradSink for the gradients of x / res when they have other consumers."""
     assert conv.groups == 1 and conv.dilation in (1, (1, 1)), 'grouped/dilated conv not on the DMA-YOLO path'
     s = conv.stride if isinstance(conv.stride, int) else conv.stride[0]
-    return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, _pad_int(conv.padding), act_code(act), res=res)
+    return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, _pad_int(conv.padding), act_code(act), res=res,
+                          xsink=xsink, rsink=rsink)
 
 
 class Conv(nn.Module):
@@ -61,11 +63,11 @@ class Conv(nn.Module):
         self.bn = nn.BatchNorm2d(c2)
         self.act = nn.SiLU() if act is True else (act if isinstance(act, nn.Module) else nn.Identity())
 
-    def forward(self, x, res=None):
-        return conv_forward(self.conv, self.bn, self.act, x, res)
+    def forward(self, x, res=None, xsink=None, rsink=None):
+        return conv_forward(self.conv, self.bn, self.act, x, res, xsink, rsink)
 
-    def forward_fuse(self, x, res=None):
-        return conv_forward(self.conv, None, self.act, x, res)
+    def forward_fuse(self, x, res=None, xsink=None, rsink=None):
+        return conv_forward(self.conv, None, self.act, x, res, xsink, rsink)
 
 
 class Bottleneck(nn.Module):
@@ -79,7 +81,10 @@ class Bottleneck(nn.Module):
         self.add = shortcut and c1 == c2
 
     def forward(self, x):
-        return self.cv2(self.cv1(x), res=x if self.add else None)
+        if not self.add:
+            return self.cv2(self.cv1(x))
+        sk = Fn.GradSink(2)  # x -> cv1 and the residual
+        return self.cv2(self.cv1(x, xsink=sk), res=x, rsink=sk)
 
 
 class C3(nn.Module):
@@ -94,7 +99,8 @@ class C3(nn.Module):
         self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, e=1.0) for _ in range(n)))
 
     def forward(self, x):
-        return self.cv3(Fn.ConcatFn.apply(None, 0.0, self.m(self.cv1(x)), self.cv2(x)))
+        sk = Fn.GradSink(2)  # x -> cv1 and cv2
+        return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(self.cv1(x, xsink=sk)), self.cv2(x, xsink=sk)))
 
 
 class SPPF(nn.Module):
@@ -110,9 +116,10 @@ class SPPF(nn.Module):
     def forward(self, x):
         k = self.m.kernel_size
         x = self.cv1(x)
-        y1 = Fn.MaxPoolFn.apply(x, k)
-        y2 = Fn.MaxPoolFn.apply(y1, k)
-        return self.cv2(Fn.ConcatFn.apply(None, 0.0, x, y1, y2, Fn.MaxPoolFn.apply(y2, k)))
+        s0, s1, s2 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)  # each pool input -> next pool + concat
+        y1 = Fn.MaxPoolFn.apply(x, k, s0)
+        y2 = Fn.MaxPoolFn.apply(y1, k, s1)
+        return self.cv2(Fn.ConcatFn.apply(None, 0.0, (s0, s1, s2, None), x, y1, y2, Fn.MaxPoolFn.apply(y2, k, s2)))
 
 
 class SPPFCSPC(nn.Module):
@@ -132,12 +139,15 @@ class SPPFCSPC(nn.Module):
 
     def forward(self, x):
         k = self.m.kernel_size
-        x1 = self.cv4(self.cv3(self.cv1(x)))
-        x2 = Fn.MaxPoolFn.apply(x1, k)
-        x3 = Fn.MaxPoolFn.apply(x2, k)
-        y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, x1, x2, x3, Fn.MaxPoolFn.apply(x3, k))))
-        y2 = self.cv2(x)
-        return self.cv7(Fn.ConcatFn.apply(None, 0.0, y1, y2))
+        sx = Fn.GradSink(2)  # x -> cv1 and cv2
+        x1 = self.cv4(self.cv3(self.cv1(x, xsink=sx)))
+        s1, s2, s3 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)
+        x2 = Fn.MaxPoolFn.apply(x1, k, s1)
+        x3 = Fn.MaxPoolFn.apply(x2, k, s2)
+        y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, (s1, s2, s3, None), x1, x2, x3,
+                                                 Fn.MaxPoolFn.apply(x3, k, s3))))
+        y2 = self.cv2(x, xsink=sx)
+        return self.cv7(Fn.ConcatFn.apply(None, 0.0, None, y1, y2))
 
 
 class SCConv(nn.Module):
@@ -159,9 +169,10 @@ class SCConv(nn.Module):
     def forward(self, x):
         r = self.k2[0].kernel_size
         r = r if isinstance(r, int) else r[0]
-        g = conv_forward(self.k2[1], self.k2[2], None, Fn.AvgPoolFn.apply(x, r))
-        u3 = conv_forward(self.k3[0], self.k3[1], None, x)
-        return conv_forward(self.k4[0], self.k4[1], None, Fn.SCGateFn.apply(x, u3, g))
+        sk = Fn.GradSink(3)  # x -> avg-pool (k2), k3, the gate
+        g = conv_forward(self.k2[1], self.k2[2], None, Fn.AvgPoolFn.apply(x, r, sk))
+        u3 = conv_forward(self.k3[0], self.k3[1], None, x, xsink=sk)
+        return conv_forward(self.k4[0], self.k4[1], None, Fn.SCGateFn.apply(x, u3, g, sk))
 
 
 class CoorAttention(nn.Module):
@@ -200,8 +211,10 @@ class CABottleneck(nn.Module):
         self.add = shortcut and c1 == c2
 
     def forward(self, x):
-        y = self.ca(self.cv2(self.cv1(x)))
-        return Fn.AddFn.apply(x, y) if self.add else y
+        if not self.add:
+            return self.ca(self.cv2(self.cv1(x)))
+        sk = Fn.GradSink(2)  # x -> cv1 and the residual
+        return Fn.AddFn.apply(x, self.ca(self.cv2(self.cv1(x, xsink=sk))), sk)
 
 
 class C3CA(C3):
@@ -222,7 +235,7 @@ class Concat(nn.Module):
 
     def forward(self, x):
         assert self.d == 1
-        return Fn.ConcatFn.apply(None, 0.0, *x)
+        return Fn.ConcatFn.apply(None, 0.0, None, *x)
 
 
 class AdConcat2(nn.Module):
@@ -236,7 +249,7 @@ class AdConcat2(nn.Module):
 
     def forward(self, x):
         assert self.d == 1 and len(x) == 2
-        return Fn.ConcatFn.apply(self.w, self.epsilon, *x)
+        return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
 
 
 class AdConcat3(AdConcat2):
@@ -248,7 +261,7 @@ class AdConcat3(AdConcat2):
 
     def forward(self, x):
         assert self.d == 1 and len(x) == 3
-        return Fn.ConcatFn.apply(self.w, self.epsilon, *x)
+        return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
 
 
 class Upsample(nn.Upsample):

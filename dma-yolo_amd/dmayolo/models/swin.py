@@ -72,23 +72,26 @@ class SwinTransformerLayer(nn.Module):
         folded into the kernel's addressing) -> proj (+ residual) -> LN -> MLP(GELU) (+ residual)."""
         c = x.shape[1]
         a = self.attn
-        u = Fn.LayerNormFn.apply(x, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        s1, s2 = Fn.GradSink(2), Fn.GradSink(2)  # x -> norm1 + residual; x2 -> norm2 + residual
+        u = Fn.LayerNormFn.apply(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, s1)
         qkv = Fn.conv_bn_act(u, a.qkv.weight.view(3 * c, c, 1, 1), a.qkv.bias, None, 1, 0, Fn.ACT_NONE)
         o = Fn.WinAttnFn.apply(qkv, a.relative_position_bias_table, a.num_heads, self.shift_size, a.scale)
         dp = isinstance(self.drop_path, DropPath) and self.training and self.drop_path.drop_prob
         if dp:
             x = Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias,
-                                                                None, 1, 0, Fn.ACT_NONE)))
+                                                                None, 1, 0, Fn.ACT_NONE)), s1)
         else:
-            x = Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias, None, 1, 0, Fn.ACT_NONE, res=x)
+            x = Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias, None, 1, 0, Fn.ACT_NONE, res=x,
+                               rsink=s1)
         m = self.mlp
-        u2 = Fn.LayerNormFn.apply(x, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        u2 = Fn.LayerNormFn.apply(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, s2)
         hd = m.fc1.weight.shape[0]
         h = Fn.conv_bn_act(u2, m.fc1.weight.view(hd, c, 1, 1), m.fc1.bias, None, 1, 0, Fn.ACT_GELU)
         if dp:
             return Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias,
-                                                                   None, 1, 0, Fn.ACT_NONE)))
-        return Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0, Fn.ACT_NONE, res=x)
+                                                                   None, 1, 0, Fn.ACT_NONE)), s2)
+        return Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0, Fn.ACT_NONE, res=x,
+                              rsink=s2)
 
 
 class SwinTransformerBlock(nn.Module):

@@ -135,7 +135,8 @@ int dmy_layernorm_fwd(int dtype, const void* x, long xps, const float* w, const 
                       float* rstd, long M, int C, float eps, void* stream);
 int dmy_layernorm_bwd_blocks(long M);
 int dmy_layernorm_bwd(int dtype, const void* x, long xps, const void* dy, long dps, const float* w, const float* mean,
-                      const float* rstd, void* dx, long dxps, long M, int C, float* pdw, float* pdb, void* stream);
+                      const float* rstd, void* dx, long dxps, int accumulate, long M, int C, float* pdw, float* pdb,
+                      void* stream);
 int dmy_winattn_fwd(int dtype, const void* qkv, const float* table, void* out, int B, int H, int W, int C, int nh,
                     int shift, float scale, void* stream);
 int dmy_winattn_bwd_groups(int B, int H, int W, int nh);
