@@ -692,6 +692,365 @@ __global__ void wgrad_to_oihw_kernel(const float* __restrict__ src, float* __res
   }
 }
 
+// ---------------------------------------------------------------- v3 forward: LDS-DMA staged (bf16)
+// BM x BN block tile of (BM/64) x (BN/64) waves, 64 x 64 per wave, BK = 64, a 3-stage LDS ring filled by
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write), counted vmcnt + raw s_barrier so the next
+// stage's loads stay in flight across the barrier.  Operand rows are 128 B (64 bf16 of K) with the
+// 16-B chunks XOR-swizzled by (row & 6): the LDS-DMA image is lane-linear (the swizzle is applied to
+// each lane's SOURCE address) and the MFMA fragment reads (ds_read_b128) are conflict-free.
+// Out-of-image taps / rows past M / channels past K read a zero page.
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[4] = {};
+
+namespace v3 {
+constexpr int BK = 64;
+template <int BM, int BN, int NS = 3> struct Cfg3 {
+  static constexpr int NSTAGE = NS;
+  static constexpr int WM = BM / 64, WN = BN / 64, NW = WM * WN, NTH = NW * 64;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int APW = A_BYTES / 1024 / NW, BPW = B_BYTES / 1024 / NW;  // 1-KiB pieces per wave
+  static constexpr int CT = BM * (BN + 8) * 2;
+  static constexpr int LDS = NSTAGE * STAGE > CT ? NSTAGE * STAGE : CT;
+  static_assert(APW >= 1 && BPW >= 1 && APW * NW * 1024 == A_BYTES && BPW * NW * 1024 == B_BYTES, "tile");
+};
+
+DEV void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// swizzled fragment read: rows of 64 bf16, lane gets X[r0 + (l&15)][k0 + 8(l>>4) .. +8)
+DEV bf16x8 frag_sw(const bf16* X, int r0, int k0, int lane) {
+  const int row = r0 + (lane & 15);
+  const int chunk = (k0 >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(X + row * 64 + ((chunk ^ (row & 6)) << 3));
+}
+
+// Forward (DG = false): A row m = output pixel, K = (kh, kw, ci), source x[oh*S - P + kh][ow*S - P + kw].
+// Data-grad, stride 1 (DG = true): A row m = input pixel, K = (kh, kw, co), source dy[ih + P - kh][iw + P - kw];
+// B = the IHWO weight copy.  Both are the same gather with a sign on the tap.
+template <int BM, int BN, int NS, bool P1, bool DG>
+struct FwdLds {
+  using C3_ = Cfg3<BM, BN, NS>;
+  const bf16* x; const bf16* w; Geom g; int Ktot;
+  int k, ci, kh, kw;  // this lane's K chunk for the next issue (advanced incrementally)
+  long abase[C3_::APW]; int ih0[C3_::APW], iw0[C3_::APW]; bool aval[C3_::APW];
+  long boff[C3_::BPW]; bool bval[C3_::BPW];
+  // g here is the GEMM view: (H, W, C) = gathered tensor, (OH, OW) = rows, K = columns, xps = gather stride
+  DEV FwdLds(const bf16* x_, const bf16* w_, const Geom& g_, long M, long m0, int n0, int wid, int lane)
+      : x(x_), w(w_), g(g_) {
+    Ktot = g.KH * g.KW * g.C;
+    k = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;  // swizzled source chunk (row & 6 == (lane >> 3) & 6)
+    ci = k % g.C;
+    const int t = k / g.C;
+    kw = t % g.KW;
+    kh = t / g.KW;
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      const long m = m0 + (wid * C3_::APW + j) * 8 + (lane >> 3);
+      aval[j] = m < M;
+      const long mm = aval[j] ? m : 0;
+      const int ow = (int)(mm % g.OW);
+      const long tt = mm / g.OW;
+      const int oh = (int)(tt % g.OH);
+      const int b = (int)(tt / g.OH);
+      if (P1) { abase[j] = mm * g.xps; ih0[j] = 0; iw0[j] = 0; }
+      else if (DG) { abase[j] = (long)b * g.H * g.W * g.xps; ih0[j] = oh + g.P; iw0[j] = ow + g.P; }
+      else { abase[j] = (long)b * g.H * g.W * g.xps; ih0[j] = oh * g.S - g.P; iw0[j] = ow * g.S - g.P; }
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j) {
+      const int n = n0 + (wid * C3_::BPW + j) * 8 + (lane >> 3);
+      bval[j] = n < g.K;
+      boff[j] = (long)(bval[j] ? n : 0) * Ktot;
+    }
+  }
+  // issue the LDS-DMA loads of the next K step into `stage`, then advance one K step
+  DEV void issue(char* stage, int wid) {
+    const bool kin = k < Ktot;
+    const bf16* zero = reinterpret_cast<const bf16*>(g_zero_page);
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      const bf16* src;
+      if (P1) {
+        src = (aval[j] && kin) ? x + abase[j] + k : zero;
+      } else {
+        const int ih = DG ? ih0[j] - kh : ih0[j] + kh, iw = DG ? iw0[j] - kw : iw0[j] + kw;
+        const bool ok = aval[j] && kin && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        src = ok ? x + abase[j] + ((long)ih * g.W + iw) * g.xps + ci : zero;
+      }
+      glds16(src, stage + (wid * C3_::APW + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j) {
+      const bf16* src = (bval[j] && kin) ? w + boff[j] + k : zero;
+      glds16(src, stage + C3_::A_BYTES + (wid * C3_::BPW + j) * 1024);
+    }
+    k += BK;
+    if (!P1) {
+      ci += BK;
+      while (ci >= g.C) {
+        ci -= g.C;
+        if (++kw == g.KW) { kw = 0; ++kh; }
+      }
+    }
+  }
+};
+
+template <int N> DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int BM, int BN, int NS, class LD>
+DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int lane) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  constexpr int PER = C3_::APW + C3_::BPW;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  ld.issue(smem, wid);
+  if (NS == 3 && nk > 1) ld.issue(smem + C3_::STAGE, wid);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
+    const bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag_sw(As, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+// Forward (DG = false) or stride-1 data-grad (DG = true; `g` is the GEMM view built by the host:
+// rows = input pixels, columns = input channels, gather = dy) with the BN-partial / accumulate epilogue.
+template <int BM, int BN, int NS, bool P1, bool DG>
+__global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y,
+                                                            float* __restrict__ psum, float* __restrict__ psq,
+                                                            int accumulate, Geom g, int gm, int gn) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
+  mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  // epilogue: (+bias) -> bf16 tile in LDS [BM][BN+8] + BN partials.  Partial rows follow the v2
+  // numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  constexpr int RS = BN + 8;
+  bf16* ct = reinterpret_cast<bf16*>(smem);
+  const bool half = g.K <= 64;
+  const long nprow = half ? 2 * ((M + 63) / 64) : 2 * ((M + 127) / 128);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = wn * 64 + j * 16 + (lane & 15);
+    const float bv = (bias != nullptr && n0 + c < g.K) ? bias[n0 + c] : 0.f;
+    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const float v = acc[i][j][r] + bv;
+        ct[row * RS + c] = __float2bfloat16(v);
+        if (m0 + row < M) {
+          s1[i >> 1] += v;
+          s2[i >> 1] += v * v;
+        }
+      }
+    if (psum != nullptr) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        s1[h] += __shfl_xor(s1[h], 16, 64);
+        s1[h] += __shfl_xor(s1[h], 32, 64);
+        s2[h] += __shfl_xor(s2[h], 16, 64);
+        s2[h] += __shfl_xor(s2[h], 32, 64);
+      }
+      const int n = n0 + c;
+      if (lane < 16 && n < g.K) {
+        const long wr = (long)tm * C3_::WM + wm;  // 64-row block index
+        if (half) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (2 * wr + h < nprow) {
+              psum[(2 * wr + h) * g.K + n] = s1[h];
+              psq[(2 * wr + h) * g.K + n] = s2[h];
+            }
+        } else if (wr < nprow) {
+          psum[wr * g.K + n] = s1[0] + s1[1];
+          psq[wr * g.K + n] = s2[0] + s2[1];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int e = threadIdx.x; e < BM * CPR; e += C3_::NTH) {
+    const int row = e / CPR, cv = e % CPR;
+    const long m = m0 + row;
+    const int n = n0 + cv * 8;
+    if (m >= M || n >= g.K) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(ct + row * RS + cv * 8);
+    uint4* dst = reinterpret_cast<uint4*>(y + m * g.yps + n);
+    if (accumulate) {
+      float a[8], b[8];
+      unpack<bf16>(v, a);
+      unpack<bf16>(*dst, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += b[j];
+      v = pack<bf16>(a);
+    }
+    *dst = v;
+  }
+}
+
+// Weight-grad: rows m = output channel, columns n = (kh, kw, ci), reduction over pixels (split-K).
+// Both operands are k-major ([64 pixels][128 channels], 256-B pixel rows) in the kmaj_off layout of
+// the v2 kernel (16-B chunks XOR-swizzled per pixel row, read with ds_read_b64_tr_b16).  One 1-KiB
+// LDS-DMA piece = 4 pixel rows; lane l fills pixel row 4i + (l >> 4), slot l & 15, i.e. logical chunk
+// (l & 15) ^ key(row), key(row) = 2 ((row & 3) | ((row >> 3) & 1) << 2): two chunk values per lane.
+template <int NS>
+struct WgradLds {
+  static constexpr int BM = 128, BN = 128, PPW = 4;  // pieces per wave per operand (4 waves)
+  const bf16* x; const bf16* dy; Geom g; long NP; int Ntot, m0, n0;
+  int cA[2], cB[2];                 // logical chunk for key bit 3 = 0 / 1
+  bool bok[2]; int bkh[2], bkw[2], bci[2];
+  long pix[PPW]; int pb[PPW], poh[PPW], pow_[PPW];  // this lane's pixel per piece (advanced by 64 per step)
+  DEV WgradLds(const bf16* x_, const bf16* dy_, const Geom& g_, int m0_, int n0_, int kt0, int wid, int lane)
+      : x(x_), dy(dy_), g(g_), m0(m0_), n0(n0_) {
+    NP = (long)g.N * g.OH * g.OW;
+    Ntot = g.KH * g.KW * g.C;
+    const int q = lane >> 4, sl = lane & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = sl ^ (2 * (q | (h << 2)));
+      cA[h] = c;
+      cB[h] = c;
+      const int n = n0 + c * 8;
+      bok[h] = n < Ntot;
+      bci[h] = n % g.C;
+      const int t = n / g.C;
+      bkw[h] = t % g.KW;
+      bkh[h] = t / g.KW;
+    }
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      pix[j] = (long)kt0 * 64 + (wid * PPW + j) * 4 + q;
+      const long pp = pix[j] < NP ? pix[j] : 0;
+      pow_[j] = (int)(pp % g.OW);
+      const long t = pp / g.OW;
+      poh[j] = (int)(t % g.OH);
+      pb[j] = (int)(t / g.OH);
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+    const bf16* zero = reinterpret_cast<const bf16*>(g_zero_page);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int piece = wid * PPW + j;
+      const int h = (piece >> 1) & 1;  // bit 3 of the pixel row (rows 4 piece .. 4 piece + 3)
+      const bool pin = pix[j] < NP;
+      const int co = m0 + cA[h] * 8;
+      const bf16* sa = (pin && co < g.K) ? dy + pix[j] * g.yps + co : zero;
+      glds16(sa, stage + piece * 1024);
+      const int ih = poh[j] * g.S - g.P + bkh[h], iw = pow_[j] * g.S - g.P + bkw[h];
+      const bool okb = pin && bok[h] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const bf16* sb = okb ? x + (((long)pb[j] * g.H + ih) * g.W + iw) * g.xps + bci[h] : zero;
+      glds16(sb, stage + 16384 + piece * 1024);
+      // advance this piece's pixel by one K step (64 pixels)
+      pix[j] += 64;
+      pow_[j] += 64;
+      while (pow_[j] >= g.OW) {
+        pow_[j] -= g.OW;
+        if (++poh[j] == g.OH) { poh[j] = 0; ++pb[j]; }
+      }
+    }
+  }
+};
+
+template <int NS>
+__global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                     float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn) {
+  constexpr int BM = 128, BN = 128, STAGE = 32768;
+  constexpr int LDS = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int nk_all = (int)((NP + 63) / 64);
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    WgradLds<NS> ld(x, dy, g, m0, n0, kt0, wid, lane);
+    ld.issue(smem, wid);
+    if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (NS == 3 && kt + 1 < nk) vm_wait<8>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = As + 64 * BM;
+#pragma unroll
+      for (int ks = 0; ks < 64; ks += 32) {
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = frag_k<BM>(As, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag_k<BN>(Bs, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int RS = BN + 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int Ntot = g.KH * g.KW * g.C;
+  for (int e = threadIdx.x; e < BM * BN; e += 256) {
+    const int row = e / BN, c = e % BN;
+    const int m = m0 + row, n = n0 + c;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+  }
+}
+}  // namespace v3
+
 // ---------------------------------------------------------------- host dispatch
 Geom make_geom(int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps) {
   Geom g;
@@ -766,9 +1125,39 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
   return (int)hipGetLastError();
 }
 
+// v3 (LDS-DMA) kernels apply to bf16 with 16-B vectors everywhere and enough rows to fill the chip
+inline bool v3_ok(int C, long xps, int K, long yps, const void* x, const void* w, const void* y, long M) {
+  return C % 8 == 0 && xps % 8 == 0 && K % 8 == 0 && yps % 8 == 0 && aligned16(x) && aligned16(w) && aligned16(y) &&
+         M >= 16384 && K >= 64;
+}
+
+// gv = GEMM view (rows N*OH*OW, columns K, gather tensor H x W x C with stride xps); BN partials need
+// 64-row wave rows, numbered 4 per 256-row tile (= dmy_conv_fwd_partial_rows when K > 64)
+template <bool DG>
+int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
+              hipStream_t st) {
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
+#define V3_LAUNCH(BM, BN, NS)                                                                                      \
+  {                                                                                                                \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
+    const unsigned grid = (unsigned)gm * gn;                                                                       \
+    if (p1) v3::conv_fwd_v3<BM, BN, NS, true, DG><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn); \
+    else v3::conv_fwd_v3<BM, BN, NS, false, DG><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn); \
+  }
+  if (gv.K > 64) V3_LAUNCH(256, 128, 3)
+  else V3_LAUNCH(256, 64, 2)
+#undef V3_LAUNCH
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st) {
   const long M = (long)g.N * g.OH * g.OW;
+  if constexpr (sizeof(T) == 2) {
+    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M))
+      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st);
+  }
   if (big_tile(M, g.K))
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
   return launch_fwd<T, 64, 64>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
@@ -776,11 +1165,43 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
 template <typename T>
 int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st) {
   const long M = (long)g.N * g.H * g.W / (g.S == 2 ? 4 : 1);
+  if constexpr (sizeof(T) == 2) {
+    if (g.S == 1 && g.OH == g.H + 2 * g.P - g.KH + 1 && g.OW == g.W + 2 * g.P - g.KW + 1 &&
+        v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M)) {
+      // GEMM view: rows = input pixels (N, H, W), columns = C, gather dy (OH x OW x K, stride yps)
+      Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 1, g.P, g.H, g.W, g.xps);
+      return launch_v3<true>((const bf16*)dy, (const bf16*)wt, nullptr, (bf16*)dx, nullptr, nullptr, acc, gv, st);
+    }
+  }
   if (big_tile(M, g.C)) return launch_dgrad<T, 128, 128>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
   return launch_dgrad<T, 64, 64>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
 }
+inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int Ntot = g.KH * g.KW * g.C;
+  const int gm = ceil_div(g.K, 128), gn = ceil_div(Ntot, 128);
+  const int nk = ceil_div(NP, 64);
+  int splits = 1024 / (gm * gn);
+  if (splits < 1) splits = 1;
+  int maxs = nk / 8;
+  if (maxs < 1) maxs = 1;
+  if (splits > maxs) splits = maxs;
+  const int per = ceil_div(nk, splits);
+  splits = ceil_div(nk, per);
+  const dim3 grid((unsigned)gm * gn, splits);
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  v3::conv_wgrad_v3<2><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    const long NP = (long)g.N * g.OH * g.OW;
+    if (g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy) &&
+        g.K > 64 && g.KH * g.KW * g.C > 64 && NP >= 16384)
+      return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
+  }
   if (g.K > 64 && g.KH * g.KW * g.C > 64) return launch_wgrad<T, 128, 128>((const T*)x, (const T*)dy, dw, g, st);
   return launch_wgrad<T, 64, 64>((const T*)x, (const T*)dy, dw, g, st);
 }
@@ -788,6 +1209,8 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
 }  // namespace
 
 // ================================================================ C ABI (include/dmayolo.h)
+// BN partial rows of the forward epilogue: 2 per 128 (big tile) or 64 rows of M.  The v3 kernel's
+// 64-row wave rows number the same way (wave row wm of 256-row tile tm = row 4 tm + wm).
 DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile(M, K) ? 128 : 64); }
 
 DMY_API int dmy_conv_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, float* psum, float* psq,

@@ -1,0 +1,92 @@
+"""GPU: the implicit-GEMM conv kernels (all tile paths: v2 64/128 tiles, the v3 LDS-DMA forward)
+against a plain PyTorch fp32 convolution of the same bf16-rounded operands, including the BN
+batch-statistic partials the forward epilogue emits and ragged M / K / C edges."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# (N, C, H, W, K, k, s): small (v2 64-tiles), mid (v2 128-tiles), large (v3: M >= 16384, K >= 128)
+SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 128, 3, 1),
+          (16, 128, 40, 40, 256, 1, 1), (16, 64, 64, 64, 128, 3, 2), (12, 96, 37, 45, 136, 3, 1),
+          (9, 256, 48, 50, 384, 1, 1), (8, 8, 192, 192, 64, 6, 2), (8, 8, 192, 192, 128, 6, 2),
+          (4, 40, 96, 70, 200, 3, 1)]
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', SHAPES)
+def test_conv_fwd_bf16_vs_torch(N, C, H, W, K, k, s):
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    g = torch.Generator().manual_seed(N * 1000 + C + K)
+    p = k // 2 if k != 6 else 2
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = (torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5)
+    ref = F.conv2d(x.float().cuda(), w.bfloat16().float().cuda(), stride=s, padding=p)
+    OH, OW = ref.shape[2:]
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    wf, _ = prep_weight(w.cuda(), torch.bfloat16, False)
+    y = torch.empty(N, K, OH, OW, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
+    M = N * OH * OW
+    P = call('dmy_conv_fwd_partial_rows', M, K)
+    ps = torch.full((P, K), float('nan'), device='cuda')
+    pq = torch.full((P, K), float('nan'), device='cuda')
+    rc = call('dmy_conv_fwd', 1, ptr(xd), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k, k, s, p, OH,
+              OW, K, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+    assert torch.isfinite(ps).all() and torch.isfinite(pq).all(), 'every partial row must be written'
+    s1 = ref.sum((0, 2, 3)).double()
+    s2 = (ref.double() ** 2).sum((0, 2, 3))
+    assert _rel(ps.sum(0), s1) < 1e-3 or float((ps.sum(0).double() - s1).abs().max()) < 1e-2 * M ** 0.5
+    assert _rel(pq.sum(0), s2) < 1e-3
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', SHAPES)
+@pytest.mark.parametrize('acc', [0, 1])
+def test_conv_dgrad_bf16_vs_torch(N, C, H, W, K, k, s, acc):
+    """data gradient (v3 LDS-DMA for stride 1, v2 parity classes for stride 2), with accumulate."""
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    if k == 6:
+        pytest.skip('the 6x6 stem has no input gradient (image input)')
+    g = torch.Generator().manual_seed(N * 1000 + C + K + 7)
+    p = k // 2
+    w = (torch.randn(K, C, k, k, generator=g) / (K * k * k) ** 0.5)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, K, OH, OW, generator=g).bfloat16()
+    prev = torch.randn(N, C, H, W, generator=g).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.bfloat16().float().cuda(), dy.float().cuda(), stride=s, padding=p)
+    if acc:
+        ref = ref + prev.float().cuda()
+    _, wt = prep_weight(w.cuda(), torch.bfloat16, True)
+    dyd = dy.cuda().contiguous(memory_format=torch.channels_last)
+    dx = prev.cuda().contiguous(memory_format=torch.channels_last)
+    rc = call('dmy_conv_dgrad', 1, ptr(dyd), ptr(wt), ptr(dx), acc, N, H, W, C, C, K, k, k, s, p, OH, OW, K, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert _rel(dx.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', SHAPES)
+def test_conv_wgrad_bf16_vs_torch(N, C, H, W, K, k, s):
+    """weight gradient (v3 LDS-DMA split-K for wide layers, v2 otherwise), fp32 accumulation."""
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(N * 1000 + C + K + 11)
+    p = k // 2 if k != 6 else 2
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    dy = torch.randn(N, K, OH, OW, generator=g).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float().cuda(), (K, C, k, k), dy.float().cuda(), stride=s, padding=p)
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    dyd = dy.cuda().contiguous(memory_format=torch.channels_last)
+    dwo = torch.empty(K * C * k * k, device='cuda')
+    dw = torch.empty(K, C, k, k, device='cuda')
+    rc = call('dmy_conv_wgrad', 1, ptr(xd), ptr(dyd), ptr(dwo), N, H, W, C, C, K, k, k, s, p, OH, OW, K, stream())
+    assert rc == 0
+    call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, C, k, k, stream())
+    torch.cuda.synchronize()
+    assert _rel(dw, ref) < 2e-3
