@@ -44,16 +44,19 @@ template <typename T> DEV uint4 pack(const float* f) {
   return v;
 }
 
-DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// fast transcendental helpers: v_exp_f32 (via __expf) and v_rcp_f32 (1 ulp); the elementwise BN /
+// activation kernels are VALU-bound with the accurate expf + IEEE division
+DEV float rcp_(float x) { return __builtin_amdgcn_rcpf(x); }
+DEV float sigmoidf_(float x) { return rcp_(1.0f + __expf(-x)); }
 
 // Activation codes shared with the host (dmayolo/_lib.py ACT_*).
 enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_HARDSWISH = 2, ACT_SIGMOID = 3, ACT_GELU = 4 };
 
 DEV float act_fwd(int act, float u) {
   switch (act) {
-    case ACT_SILU: return u / (1.0f + expf(-u));
+    case ACT_SILU: return u * sigmoidf_(u);
     case ACT_HARDSWISH: return u * fminf(fmaxf(u + 3.0f, 0.0f), 6.0f) / 6.0f;
-    case ACT_SIGMOID: return 1.0f / (1.0f + expf(-u));
+    case ACT_SIGMOID: return sigmoidf_(u);
     case ACT_GELU: return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f));
     default: return u;
   }
@@ -62,13 +65,13 @@ DEV float act_fwd(int act, float u) {
 DEV float act_grad(int act, float u) {
   switch (act) {
     case ACT_SILU: {
-      float s = 1.0f / (1.0f + expf(-u));
+      const float s = sigmoidf_(u);
       return s * (1.0f + u * (1.0f - s));
     }
     case ACT_HARDSWISH:  // torch hardswish_backward: u<-3 -> 0, u<=3 -> u/3+0.5, else 1
       return u < -3.0f ? 0.0f : (u <= 3.0f ? u / 3.0f + 0.5f : 1.0f);
     case ACT_SIGMOID: {
-      float s = 1.0f / (1.0f + expf(-u));
+      const float s = sigmoidf_(u);
       return s * (1.0f - s);
     }
     case ACT_GELU: {

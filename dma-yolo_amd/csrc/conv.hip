@@ -19,6 +19,7 @@
 // MFMA: bf16 -> v_mfma_f32_16x16x32_bf16, f32 -> v_mfma_f32_16x16x4_f32 (exact fp32, parity mode).
 // Block ids are remapped so consecutive tiles sharing an A panel land on one XCD (L2 reuse).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -1176,12 +1177,23 @@ int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& 
   if (big_tile(M, g.C)) return launch_dgrad<T, 128, 128>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
   return launch_dgrad<T, 64, 64>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
 }
+inline int wgrad_target() {
+  static int t = [] {
+    const char* e = getenv("DMY_WGRAD_TARGET");
+    return e ? atoi(e) : 1024;
+  }();
+  return t;
+}
+
 inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
   const long NP = (long)g.N * g.OH * g.OW;
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, 128), gn = ceil_div(Ntot, 128);
   const int nk = ceil_div(NP, 64);
-  int splits = 1024 / (gm * gn);
+  // split-K over pixels: ~wgrad_target() blocks (rounded), >= 8 K steps per split.  More splits fill
+  // the chip but cost fp32 atomics (64 KiB per block) -- DMY_WGRAD_TARGET overrides for tuning.
+  const int tiles = gm * gn;
+  int splits = (wgrad_target() + tiles / 2) / tiles;
   if (splits < 1) splits = 1;
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;

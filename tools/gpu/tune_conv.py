@@ -1,0 +1,66 @@
+"""Time single conv launches (fwd / dgrad / wgrad, bf16) for a list of layer shapes.
+
+python tools/gpu/tune_conv.py [shape-set]   (env knobs such as DMY_WGRAD_TARGET are read by the library)
+Prints one line per (kind, shape): mean us over 20 launches and TFLOP/s.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, 'dma-yolo_amd'))
+import torch  # noqa: E402
+from dmayolo.functional import call, ptr, stream, prep_weight  # noqa: E402
+
+SETS = {
+    'dma': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1), (32, 128, 192, 192, 128, 3, 1),
+            (32, 64, 768, 768, 64, 3, 1), (32, 64, 384, 384, 64, 3, 1), (32, 256, 96, 96, 256, 1, 1),
+            (32, 512, 96, 96, 512, 3, 1), (32, 512, 192, 192, 128, 1, 1)],
+    'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
+            (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
+}
+
+
+def bench(fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else 'dma'
+    kinds = (sys.argv[2] if len(sys.argv) > 2 else 'fwd,dgrad,wgrad').split(',')
+    for (N, C, H, W, K, k, s) in SETS[which]:
+        p = k // 2
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N, C, H, W, device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
+        dy = torch.randn(N, K, OH, OW, device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
+        w = torch.randn(K, C, k, k, device='cuda') * 0.05
+        wf, wt = prep_weight(w, torch.bfloat16, True)
+        y = torch.empty_like(dy)
+        dx = torch.empty_like(x)
+        M = N * OH * OW
+        P = call('dmy_conv_fwd_partial_rows', M, K)
+        ps, pq = torch.empty(P * K, device='cuda'), torch.empty(P * K, device='cuda')
+        dwo = torch.empty(K * C * k * k, device='cuda')
+        fl = 2.0 * M * K * C * k * k
+        fns = {
+            'fwd': lambda: call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k,
+                                k, s, p, OH, OW, K, stream()),
+            'dgrad': lambda: call('dmy_conv_dgrad', 1, ptr(dy), ptr(wt), ptr(dx), 0, N, H, W, C, C, K, k, k, s, p, OH,
+                                  OW, K, stream()),
+            'wgrad': lambda: call('dmy_conv_wgrad', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s, p, OH, OW,
+                                  K, stream()),
+        }
+        for kind in kinds:
+            us = bench(fns[kind])
+            print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s', flush=True)
+
+
+if __name__ == '__main__':
+    main()
