@@ -20,6 +20,7 @@
 // Block ids are remapped so consecutive tiles sharing an A panel land on one XCD (L2 reuse).
 #include "common.h"
 #include <cstdlib>
+#include <cmath>
 
 namespace {
 
@@ -1180,9 +1181,18 @@ int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& 
 inline int wgrad_target() {
   static int t = [] {
     const char* e = getenv("DMY_WGRAD_TARGET");
-    return e ? atoi(e) : 1024;
+    return e ? atoi(e) : 0;
   }();
   return t;
+}
+inline int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
 }
 
 inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
@@ -1190,13 +1200,25 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, 128), gn = ceil_div(Ntot, 128);
   const int nk = ceil_div(NP, 64);
-  // split-K over pixels: ~wgrad_target() blocks (rounded), >= 8 K steps per split.  More splits fill
-  // the chip but cost fp32 atomics (64 KiB per block) -- DMY_WGRAD_TARGET overrides for tuning.
+  // split-K over pixels.  Cost model (calibrated on MI355X): resident blocks R = 2 per CU; time ~
+  // rounds(tiles*s / R) * (K steps per split) * 1.9 us + tiles*s * 64 KiB of fp32 atomics at 1.3 TB/s.
+  // DMY_WGRAD_TARGET=<blocks> replaces the model by a fixed block-count target (tuning).
   const int tiles = gm * gn;
-  int splits = (wgrad_target() + tiles / 2) / tiles;
-  if (splits < 1) splits = 1;
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
+  int splits = 1;
+  if (wgrad_target() > 0) {
+    splits = (wgrad_target() + tiles / 2) / tiles;
+    if (splits < 1) splits = 1;
+  } else {
+    const double R = 2.0 * num_cus();
+    double best = 1e300;
+    for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
+      const double blocks = (double)tiles * sp;
+      const double t = ceil(blocks / R) * ceil_div(nk, sp) * 1.9 + blocks * 0.0504;
+      if (t < best) { best = t; splits = sp; }
+    }
+  }
   if (splits > maxs) splits = maxs;
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);

@@ -23,7 +23,13 @@ for _f in (lib.dmy_sgd, lib.dmy_adam, lib.dmy_ema):
 
 
 class _Table:
-    """Device-side pointer table + (tensor, chunk) map for a list of tensors."""
+    """Device-side pointer table + (tensor, chunk) map for a list of tensors.
+
+    Tables are cached by the tensors' addresses: with the caching allocator the gradients of one
+    parameter list land at the same addresses every step, so after the first step no table is
+    rebuilt.  A new table is staged in pinned host memory and copied asynchronously -- a pageable
+    H2D copy would block the host until the GPU drained its queue (no run-ahead across steps)."""
+    _cache = {}
 
     def __init__(self, lists, dev):
         n = [t.numel() for t in lists[0]]
@@ -36,7 +42,18 @@ class _Table:
         host = [torch.tensor([t.data_ptr() for t in L], dtype=torch.int64) for L in lists]
         host += [torch.tensor(n, dtype=torch.int64), torch.tensor(tid, dtype=torch.int32),
                  torch.tensor(off, dtype=torch.int64)]
-        self.dev = [h.to(dev, non_blocking=False) for h in host]
+        self.pinned = [h.pin_memory() for h in host]  # kept alive with the cached table
+        self.dev = [h.to(dev, non_blocking=True) for h in self.pinned]
+
+    @classmethod
+    def get(cls, lists, dev):
+        key = (str(dev),) + tuple(tuple(t.data_ptr() for t in L) for L in lists) + (tuple(t.numel() for t in lists[0]),)
+        tb = cls._cache.get(key)
+        if tb is None:
+            if len(cls._cache) > 64:
+                cls._cache.clear()
+            tb = cls._cache[key] = cls(lists, dev)
+        return tb
 
     def p(self, i):
         return ctypes.c_void_p(self.dev[i].data_ptr())
@@ -66,7 +83,7 @@ class FusedSGD(torch.optim.Optimizer):
                 if 'momentum_buffer' not in st:
                     st['momentum_buffer'] = torch.empty_like(p)
                 bufs.append(st['momentum_buffer'])
-            tb = _Table([ps, [p.grad for p in ps], bufs], ps[0].device)
+            tb = _Table.get([ps, [p.grad for p in ps], bufs], ps[0].device)
             _check(lib.dmy_sgd(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.nchunks, float(g['lr']),
                                float(g['momentum']), float(g['weight_decay']), int(g['nesterov']), int(first),
                                stream()), 'dmy_sgd')
@@ -97,7 +114,7 @@ class FusedAdam(torch.optim.Optimizer):
             b1, b2 = g['betas']
             bc1 = 1 - b1 ** t
             bc2s = (1 - b2 ** t) ** 0.5
-            tb = _Table([ps, [p.grad for p in ps], ms, vs], ps[0].device)
+            tb = _Table.get([ps, [p.grad for p in ps], ms, vs], ps[0].device)
             _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
                                 float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
                                 float(bc1), float(bc2s), stream()), 'dmy_adam')
@@ -110,7 +127,7 @@ def ema_update(ema_tensors, model_tensors, d):
     ms = [m.float() if m.dtype != torch.float32 else m for m in model_tensors]
     for e in es:
         assert e.dtype == torch.float32 and e.is_contiguous()
-    tb = _Table([es, [m.contiguous() for m in ms]], es[0].device)
+    tb = _Table.get([es, [m.contiguous() for m in ms]], es[0].device)
     _check(lib.dmy_ema(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.nchunks, float(d), stream()), 'dmy_ema')
 
 

@@ -57,9 +57,13 @@ class ModelEMA:
         with torch.no_grad():
             self.updates += 1
             d = self.decay(self.updates)
-            msd = de_parallel(model).state_dict()
-            pairs = [(v, msd[k].detach()) for k, v in self.ema.state_dict().items() if v.dtype.is_floating_point]
-            ema_update([a for a, _ in pairs], [b for _, b in pairs], d)
+            m = de_parallel(model)
+            if getattr(self, '_pairs_of', None) is not m:  # state_dict walks cost ~2 ms of host time per step
+                msd = m.state_dict()
+                pairs = [(v, msd[k].detach()) for k, v in self.ema.state_dict().items() if v.dtype.is_floating_point]
+                self._pairs = ([a for a, _ in pairs], [b for _, b in pairs])
+                self._pairs_of = m
+            ema_update(self._pairs[0], self._pairs[1], d)
 
     def update_attr(self, model, include=(), exclude=('process_group', 'reducer')):
         for k, v in model.__dict__.items():

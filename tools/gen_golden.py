@@ -484,6 +484,124 @@ def gen_optim():
     print('wrote optim', sum(v.nbytes for k, v in d.items() if k != 'meta') / 1e6, 'MB')
 
 
+def gen_tal():
+    """anchor-free TAL path: TaskAlignedAssigner, ComputeLoss_TAL (+ grads), TDetect, space_to_depth,
+    and the CASPD_ODRTA (TDetect) model's parameter layout."""
+    from utils.tal_assign import TaskAlignedAssigner
+    import utils.tal as T
+    import models.detect_t as DT
+    import yaml
+    shapes, strides = [(8, 8), (4, 4), (2, 2)], [8, 16, 32]
+    img = 64
+    # 1. assigner on crafted crowded inputs (several gts claim the same anchors; one padded gt row)
+    for tag, nc, seed in [('a', 5, 40), ('b', 3, 41)]:
+        g = torch.Generator().manual_seed(seed)
+        B, n = 2, 5
+        pts, st = [], []
+        for (h, w), s_ in zip(shapes, strides):
+            ys, xs = torch.meshgrid(torch.arange(h) + 0.5, torch.arange(w) + 0.5, indexing='ij')
+            pts.append(torch.stack((xs.reshape(-1), ys.reshape(-1)), 1) * s_)
+            st.append(torch.full((h * w, 1), float(s_)))
+        pts, st = torch.cat(pts), torch.cat(st)
+        A = pts.shape[0]
+        c = torch.rand(B, n, 2, generator=g) * 48 + 8
+        wh = torch.rand(B, n, 2, generator=g) * 30 + 6
+        gboxes = torch.cat((c - wh / 2, c + wh / 2), -1)
+        labels = torch.randint(0, nc, (B, n, 1), generator=g).float()
+        gmask = torch.ones(B, n, 1)
+        gboxes[1, -1] = 0
+        labels[1, -1] = 0
+        gmask[1, -1] = 0
+        scores = torch.rand(B, A, nc, generator=g) * 0.9 + 0.05
+        pc = pts[None] + torch.randn(B, A, 2, generator=g) * 4
+        pwh = torch.rand(B, A, 2, generator=g) * 30 + 4
+        pboxes = torch.cat((pc - pwh / 2, pc + pwh / 2), -1)
+        asg = TaskAlignedAssigner(topk=10, num_classes=nc, alpha=0.5, beta=6.0)
+        tl, tb, ts, fg = asg(scores, pboxes, pts, labels, gboxes, gmask)
+        np.savez_compressed(os.path.join(OUT, f'tal_assign_{tag}.npz'), meta=json.dumps(dict(nc=nc)),
+                            scores=npy(scores), pboxes=npy(pboxes), pts=npy(pts), labels=npy(labels),
+                            gboxes=npy(gboxes), gmask=npy(gmask), t_lab=npy(tl), t_box=npy(tb), t_sc=npy(ts),
+                            fg=npy(fg))
+        print('wrote tal_assign', tag, int(fg.sum()))
+    # 2. ComputeLoss_TAL with gradients w.r.t. the TDetect training outputs
+    hyp = yaml.safe_load(open('/root/reference/data/hyps/hyp.VisDrone.yaml'))
+    for tag, nc, seed in [('a', 10, 42), ('b', 4, 43)]:
+        B = 2
+        det = DT.TDetect(nc=nc, ch=(16, 16, 16))
+        det.stride = torch.tensor([8.0, 16.0, 32.0])
+
+        class _M(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.model = nn.Sequential(det)
+        m = _M()
+        m.hyp = hyp
+        A = sum(h * w for h, w in shapes)
+        g = torch.Generator().manual_seed(seed)
+        feats = [torch.zeros(B, nc + 64, h, w) for h, w in shapes]
+        pdist = torch.randn(B, 64, A, generator=g) * 1.5
+        pcls = torch.randn(B, nc, A, generator=g) - 2.0
+        targets = synth_targets(B, 6, nc, seed=seed + 100)
+        targets[:, 4:6] = targets[:, 4:6].clamp(0.08, 0.6)   # boxes of a few cells on the 64-px image
+        cl = T.ComputeLoss_TAL(m)
+        pd_, pc_ = pdist.clone().requires_grad_(True), pcls.clone().requires_grad_(True)
+        loss, items = cl((feats, pd_, pc_), targets)
+        loss.backward()
+        np.savez_compressed(os.path.join(OUT, f'tal_loss_{tag}.npz'),
+                            meta=json.dumps(dict(nc=nc, hyp=hyp, strides=[8, 16, 32], shapes=shapes)),
+                            pdist=npy(pdist), pcls=npy(pcls), targets=npy(targets), loss=npy(loss), items=npy(items),
+                            g_pdist=npy(pd_.grad), g_pcls=npy(pc_.grad))
+        print('wrote tal_loss', tag, npy(items))
+    # 3. TDetect head forward / backward / eval (list input, tuple output flattened)
+    torch.manual_seed(44)
+    det = DT.TDetect(nc=6, ch=(16, 32))
+    det.stride = torch.tensor([8.0, 16.0])
+    det.bias_init()
+    gen = torch.Generator().manual_seed(45)
+    initialize_weights(det)
+    randomize_bn(det, gen)
+    sd0 = {k: v.clone() for k, v in det.state_dict().items()}
+    xs = [rnd(2, 16, 8, 10, seed=46), rnd(2, 32, 4, 5, seed=47)]
+    ins = [x.clone().requires_grad_(True) for x in xs]
+    det.train()
+    lvl, box, cls = det(list(ins))
+    outs = list(lvl) + [box, cls]
+    gups = [torch.randn(o.shape, generator=gen) for o in outs]
+    sum((o * gg).sum() for o, gg in zip(outs, gups)).backward()
+    d = {'meta': json.dumps(dict(module='TDetect', args=[6, [16, 32]], stride=[8.0, 16.0]))}
+    for i, x in enumerate(xs):
+        d[f'in.{i}'] = npy(x)
+        d[f'gin.{i}'] = npy(ins[i].grad)
+    for k, v in sd0.items():
+        d[f'sd.{k}'] = npy(v)
+    for i, (o, gg) in enumerate(zip(outs, gups)):
+        d[f'out.{i}'] = npy(o)
+        d[f'gup.{i}'] = npy(gg)
+    for k, p_ in det.named_parameters():
+        if p_.grad is not None:
+            d[f'gp.{k}'] = npy(p_.grad)
+    det.load_state_dict(sd0)
+    det.eval()
+    with torch.no_grad():
+        y, _ = det([x.clone() for x in xs])
+    d['eout.0'] = npy(y)
+    np.savez_compressed(os.path.join(OUT, 'tdetect.npz'), **d)
+    print('wrote tdetect')
+    # 4. space_to_depth
+    x = rnd(2, 8, 6, 10, seed=48)
+    np.savez_compressed(os.path.join(OUT, 'space_to_depth.npz'), **{'in.0': npy(x), 'out.0': npy(C.space_to_depth()(x))})
+    # 5. CASPD_ODRTA (TDetect, P2-P5) parameter layout
+    torch.manual_seed(49)
+    model = Y.Model('/root/reference/models/CASPD_ODRTA.yaml', nc=10)
+    sd = model.state_dict()
+    np.savez_compressed(os.path.join(OUT, 'model_caspd_layout.npz'),
+                        meta=json.dumps(dict(yaml='CASPD_ODRTA.yaml', nc=10,
+                                             nparams=sum(p.numel() for p in model.parameters()),
+                                             stride=[float(s_) for s_ in model.stride],
+                                             shapes={k: list(v.shape) for k, v in sd.items()})))
+    print('wrote model_caspd_layout', sum(p.numel() for p in model.parameters()))
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['modules', 'detect', 'loss', 'siou', 'nms', 'models', 'optim']
     for w in which:
