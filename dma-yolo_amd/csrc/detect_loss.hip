@@ -11,6 +11,7 @@
 //    integer atomicMax on non-negative float bits -> deterministic.
 // Everything stays on device: target counts are read by the kernels, never by the host.
 #include "common.h"
+#include "dual.h"
 
 namespace {
 
@@ -119,46 +120,6 @@ __global__ void __launch_bounds__(1024) build_targets_kernel(const float* __rest
   }
   if (threadIdx.x == 0) *o.count = base;
 }
-
-// ---------------------------------------------------------------- dual numbers for SIoU
-struct D4 {
-  float v, d[4];
-};
-DEV D4 dc(float v) { D4 r; r.v = v; r.d[0] = r.d[1] = r.d[2] = r.d[3] = 0.f; return r; }
-DEV D4 operator+(D4 a, D4 b) { D4 r; r.v = a.v + b.v; for (int i = 0; i < 4; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
-DEV D4 operator-(D4 a, D4 b) { D4 r; r.v = a.v - b.v; for (int i = 0; i < 4; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
-DEV D4 operator*(D4 a, D4 b) { D4 r; r.v = a.v * b.v; for (int i = 0; i < 4; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
-DEV D4 operator/(D4 a, D4 b) {
-  D4 r; r.v = a.v / b.v;
-  for (int i = 0; i < 4; ++i) r.d[i] = (a.d[i] * b.v - a.v * b.d[i]) / (b.v * b.v);
-  return r;
-}
-DEV D4 scal(D4 a, float s) { D4 r; r.v = a.v * s; for (int i = 0; i < 4; ++i) r.d[i] = a.d[i] * s; return r; }
-DEV D4 dmin(D4 a, D4 b) {  // torch.minimum: ties split the gradient
-  if (a.v < b.v) return a;
-  if (b.v < a.v) return b;
-  D4 r; r.v = a.v; for (int i = 0; i < 4; ++i) r.d[i] = 0.5f * (a.d[i] + b.d[i]); return r;
-}
-DEV D4 dmax(D4 a, D4 b) {
-  if (a.v > b.v) return a;
-  if (b.v > a.v) return b;
-  D4 r; r.v = a.v; for (int i = 0; i < 4; ++i) r.d[i] = 0.5f * (a.d[i] + b.d[i]); return r;
-}
-DEV D4 dclamp0(D4 a) {  // clamp(min=0): gradient passes where a >= 0
-  if (a.v >= 0.f) return a;
-  return dc(0.f);
-}
-DEV D4 dabs(D4 a) {
-  const float s = a.v > 0.f ? 1.f : (a.v < 0.f ? -1.f : 0.f);
-  D4 r; r.v = fabsf(a.v); for (int i = 0; i < 4; ++i) r.d[i] = s * a.d[i]; return r;
-}
-DEV D4 dfun(D4 a, float v, float dv) { D4 r; r.v = v; for (int i = 0; i < 4; ++i) r.d[i] = dv * a.d[i]; return r; }
-DEV D4 dexp(D4 a) { const float e = expf(a.v); return dfun(a, e, e); }
-DEV D4 dsqrt(D4 a) { const float s = powf(a.v, 0.5f); return dfun(a, s, 0.5f * powf(a.v, -0.5f)); }
-DEV D4 dcos(D4 a) { return dfun(a, cosf(a.v), -sinf(a.v)); }
-DEV D4 dasin(D4 a) { return dfun(a, asinf(a.v), 1.0f / sqrtf(1.0f - a.v * a.v)); }
-DEV D4 dsq(D4 a) { return dfun(a, a.v * a.v, 2.f * a.v); }
-DEV D4 dpow4(D4 a) { const float s = a.v * a.v; return dfun(a, s * s, 4.f * s * a.v); }
 
 // SIoU(b1, b2) for xywh boxes, utils/metrics.py:192-235; b1 carries the derivatives
 DEV D4 siou(D4 x1, D4 y1, D4 w1_, D4 h1_, float x2, float y2, float w2_, float h2_) {

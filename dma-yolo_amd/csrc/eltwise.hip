@@ -235,6 +235,37 @@ __global__ void resize_bwd_kernel(const T* __restrict__ dy, long dps, T* __restr
   }
 }
 
+// ---------------------------------------------------------------- space_to_depth (models/common.py:1451-1458)
+// y[b, h, w, q*C + c] = x[b, 2h + dy_q, 2w + dx_q, c], q = 0..3 <-> (dy, dx) = (0,0), (1,0), (0,1), (1,1)
+// (the cat order x[::2, ::2], x[1::2, ::2], x[::2, 1::2], x[1::2, 1::2]); backward is the inverse copy.
+template <typename T, int NV>
+__global__ void s2d_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps, int N, int H, int W, int C,
+                           int backward) {
+  const int OH = H / 2, OW = W / 2, CV = C / NV;
+  const long total = (long)N * OH * OW * 4 * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % CV) * NV;
+    long t = i / CV;
+    const int q = (int)(t % 4);
+    t /= 4;
+    const int w = (int)(t % OW);
+    t /= OW;
+    const int h = (int)(t % OH);
+    const int b = (int)(t / OH);
+    const int dy = q & 1, dx = q >> 1;
+    const long xi = (((long)b * H + 2 * h + dy) * W + 2 * w + dx) * xps + c;
+    const long yi = (((long)b * OH + h) * OW + w) * yps + q * C + c;
+    float v[NV];
+    if (backward) {
+      ldv<T, NV>(y + yi, v);
+      stv<T, NV>(const_cast<T*>(x) + xi, v);
+    } else {
+      ldv<T, NV>(x + xi, v);
+      stv<T, NV>(y + yi, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- channel-slice copy with BiFPN weight
 // scale = wvec ? wvec[idx] / (sum(wvec[0..nw)) + eps) : 1
 DEV float bifpn_scale(const float* wv, int idx, int nw, float eps) {
@@ -634,6 +665,14 @@ DMY_API int dmy_resize_bwd(int dtype, const void* dy, long dps, void* dx, long d
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
   DISPATCH_TV(dtype, v, resize_bwd_kernel<T, NV><<<egrid((long)N * IH * IW * C / NV), 256, 0, st>>>((const T*)dy, dps, (T*)dx, dxps, N, IH, IW, OH, OW, C));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long yps, int N, int H, int W, int C,
+                               int backward, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if ((H | W) & 1) return (int)hipErrorInvalidValue;  // the reference's cat needs even sizes
+  const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
+  DISPATCH_TV(dtype, v, s2d_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, N, H, W, C, backward));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long dps, long M, int C, const float* wv,

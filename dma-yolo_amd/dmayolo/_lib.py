@@ -64,6 +64,12 @@ SIGNATURES = {
                             I, P, P, P, P],
     'dmy_yolo_loss_finalize': [P, I, F, F, F, F, P, P, P],
     'dmy_loss_grad': [I, P, P, P, L, P],
+    # tal.hip
+    'dmy_tal_workspace_bytes': [I, I, I],
+    'dmy_tal_loss': [I, P, L, L, L, P, L, L, L, I, I, I, P, P, P, P, I, F, F, F, P, P, P, P, P],
+    'dmy_tal_flatten': [I, P, L, I, I, I, I, I, I, P, I, P],
+    'dmy_tal_detect_out': [I, P, I, I, I, P, P, P, P, P],
+    'dmy_space_to_depth': [I, P, L, P, L, I, I, I, I, I, P],
     # nms.hip
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
@@ -100,7 +106,7 @@ lib = _load()
 
 def call(name, *args):
     rc = getattr(lib, name)(*args)
-    if name.endswith(('_rows', '_blocks', '_groups')):
+    if name.endswith(('_rows', '_blocks', '_groups', '_bytes')):
         return rc
     if rc != 0:
         raise RuntimeError(f'{name} failed with hipError {rc}')

@@ -678,3 +678,57 @@ class SampleScaleFn(torch.autograd.Function):
         dx = torch.empty_like(dy, memory_format=CL)
         call('dmy_sample_scale', dcode(dy), ptr(dy), ptr(s), ptr(dx), dy.numel() // dy.shape[0], dy.numel(), stream())
         return dx, None
+
+
+# ------------------------------------------------------------------ space_to_depth / TDetect flatten
+
+class SpaceToDepthFn(torch.autograd.Function):
+    """models/common.py:1451-1458: cat(x[::2, ::2], x[1::2, ::2], x[::2, 1::2], x[1::2, 1::2]) on channels."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, 4 * C, H // 2, W // 2, x)
+        call('dmy_space_to_depth', dcode(x), ptr(x), xps, ptr(y), 4 * C, N, H, W, C, 0, stream())
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dy, dps = pixel_stride(dy)
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_space_to_depth', dcode(dy), ptr(dx), C, ptr(dy), dps, N, H, W, C, 1, stream())
+        return dx
+
+
+class FlattenLevelsFn(torch.autograd.Function):
+    """TDetect (models/detect_t.py:45-47): per-level NHWC head outputs [B, no, H, W] -> one
+    anchor-major [B, A, no] tensor (levels in order, anchors row-major within a level)."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        B, no = xs[0].shape[:2]
+        A = sum(x.shape[2] * x.shape[3] for x in xs)
+        F = torch.empty((B, A, no), dtype=xs[0].dtype, device=xs[0].device)
+        a0 = 0
+        geo = []
+        for x in xs:
+            x, xps = pixel_stride(x)
+            H, W = x.shape[2:]
+            call('dmy_tal_flatten', dcode(x), ptr(x), xps, B, H, W, A, a0, no, ptr(F), 0, stream())
+            geo.append((H, W, a0))
+            a0 += H * W
+        ctx.geo, ctx.B, ctx.no, ctx.A = geo, B, no, A
+        return F
+
+    @staticmethod
+    def backward(ctx, dF):
+        dF = dF.contiguous()
+        out = []
+        for H, W, a0 in ctx.geo:
+            dx = new_act(ctx.B, ctx.no, H, W, dF)
+            call('dmy_tal_flatten', dcode(dF), ptr(dx), ctx.no, ctx.B, H, W, ctx.A, a0, ctx.no, ptr(dF), 1, stream())
+            out.append(dx)
+        return tuple(out)

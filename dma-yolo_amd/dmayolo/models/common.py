@@ -17,7 +17,7 @@ from ..functional import ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GEL
 
 __all__ = ['autopad', 'Conv', 'Bottleneck', 'C3', 'SPPF', 'SPPFCSPC', 'SCConv', 'CoorAttention', 'CA',
            'CABottleneck', 'C3CA', 'Concat', 'AdConcat2', 'AdConcat3', 'Upsample', 'C3STR', 'SwinTransformerBlock',
-           'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath']
+           'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath', 'space_to_depth']
 
 
 def autopad(k, p=None):
@@ -262,6 +262,17 @@ class AdConcat3(AdConcat2):
     def forward(self, x):
         assert self.d == 1 and len(x) == 3
         return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
+
+
+class space_to_depth(nn.Module):
+    """models/common.py:1451-1458 (SPD: stride-free 2x downsampling into channels)."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def forward(self, x):
+        return Fn.SpaceToDepthFn.apply(x)
 
 
 class Upsample(nn.Upsample):

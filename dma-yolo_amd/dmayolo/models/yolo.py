@@ -16,7 +16,8 @@ import torch.nn as nn
 from .. import functional as Fn
 from ..functional import call, ptr, stream, dcode
 from .common import *  # noqa: F401,F403  (the YAML namespace)
-from .common import Conv, Upsample, SCConv, autopad
+from .common import Conv, Upsample, SCConv, autopad, space_to_depth
+from .tdetect import TDetect
 from ..utils.general import make_divisible
 from ..utils.torch_utils import initialize_weights, fuse_conv_and_bn
 
@@ -98,6 +99,8 @@ def _out_hw(m, hw):
     if isinstance(m, nn.Upsample):
         sf = m.scale_factor if isinstance(m.scale_factor, (int, float)) else m.scale_factor[0]
         return (int(hw[0] * sf), int(hw[1] * sf))
+    if isinstance(m, space_to_depth):
+        return (hw[0] // 2, hw[1] // 2)
     return hw
 
 
@@ -132,6 +135,13 @@ class Model(nn.Module):
             check_anchor_order(m)
             self.stride = m.stride
             self._initialize_biases()
+        elif isinstance(m, TDetect):  # models/yolo.py:173-180
+            s = 256
+            m.inplace = self.inplace
+            hw = self._probe_hw(s)
+            m.stride = torch.tensor([s / h for h, _ in hw], dtype=torch.float32)
+            self.stride = m.stride
+            m.bias_init()
         initialize_weights(self)
 
     def _probe_hw(self, s):
@@ -139,7 +149,7 @@ class Model(nn.Module):
         for m in self.model:
             if m.f != -1:
                 hw = ys[m.f] if isinstance(m.f, int) else [hw if j == -1 else ys[j] for j in m.f]
-            if isinstance(m, Detect):
+            if isinstance(m, (Detect, TDetect)):
                 return hw
             if isinstance(hw, list):
                 hw = hw[0]
@@ -196,6 +206,11 @@ class Model(nn.Module):
             m.grid = list(map(fn, m.grid))
             if isinstance(m.anchor_grid, list):
                 m.anchor_grid = list(map(fn, m.anchor_grid))
+        elif isinstance(m, TDetect):  # models/yolo.py:345-348; the stride list for the kernels stays on the host
+            m.stride_list = [float(v) for v in m.stride.cpu()] if m.stride.numel() else []
+            m.stride = fn(m.stride)
+            m.anchors = fn(m.anchors)
+            m.strides = fn(m.strides)
         return self
 
     def info(self, verbose=False, img_size=640):
@@ -211,6 +226,7 @@ def _namespace():
     from . import common as C
     ns = {k: getattr(C, k) for k in C.__all__}
     ns['Detect'] = Detect
+    ns['TDetect'] = TDetect
     ns['nn'] = types.SimpleNamespace(Upsample=Upsample, BatchNorm2d=nn.BatchNorm2d)
     return ns
 
@@ -251,6 +267,10 @@ def parse_model(d, ch):
             args.append([ch[x] for x in f])
             if isinstance(args[1], int):
                 args[1] = [list(range(args[1] * 2))] * len(f)
+        elif m is TDetect:
+            args.append([ch[x] for x in f])
+        elif m is space_to_depth:
+            c2 = 4 * ch[f]
         elif m is Upsample:
             c2 = ch[f]
         else:

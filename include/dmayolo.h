@@ -154,6 +154,23 @@ int dmy_adam(float* const* p, const float* const* g, float* const* m, float* con
 int dmy_ema(float* const* ema, const float* const* src, const long* n, const int* tid, const long* off, int nchunks,
             float decay, void* stream);
 
+
+/* ---- anchor-free TAL path: replaces models/detect_t.py:38-101 (TDetect outputs, DFL decode),
+ *      utils/tal.py:81-221 (ComputeLoss_TAL, BboxLoss, bbox2dist) and utils/tal_assign.py:54-189
+ *      (TaskAlignedAssigner); models/common.py:1451-1458 (space_to_depth).  H, W, stride are HOST
+ *      arrays of nl entries; box / cls are read through (batch, channel, anchor) element strides. */
+int dmy_tal_workspace_bytes(int B, int A, int cap);
+int dmy_tal_loss(int dtype, const void* box, long sbb, long sbc, long sba, const void* cls, long scb, long scc, long sca,
+                 int B, int nc, int nl, const int* H, const int* W, const float* stride, const float* targets, int nt,
+                 float alpha, float beta, float pos_weight, void* workspace, float* G, float* loss, float* items,
+                 void* stream);
+int dmy_tal_flatten(int dtype, const void* x, long xps, int B, int H, int W, int A, int a0, int no, void* F, int backward,
+                    void* stream);
+int dmy_tal_detect_out(int dtype, const void* F, int B, int nc, int nl, const int* H, const int* W, const float* stride,
+                       float* y, void* stream);
+int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long yps, int N, int H, int W, int C, int backward,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

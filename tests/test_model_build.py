@@ -47,3 +47,17 @@ def test_optimizer_groups_match_reference():
     assert [names[id(p)] for p in g0] == groups['g0']
     assert [names[id(p)] for p in g1] == groups['g1']
     assert [names[id(p)] for p in g2] == groups['g2']
+
+
+def test_caspd_tdetect_layout_matches_reference():
+    """CASPD_ODRTA (space_to_depth + C3CA + TDetect P2-P5): parameter count, state_dict shapes, strides."""
+    from dmayolo.models.yolo import Model
+    fx = Fixture('model_caspd_layout')
+    m = Model(os.path.join(YAMLS, 'CASPD_ODRTA.yaml'), nc=fx.meta['nc'])
+    sd = m.state_dict()
+    ref = fx.meta['shapes']
+    assert set(sd) == set(ref), set(sd) ^ set(ref)
+    for k, v in ref.items():
+        assert list(sd[k].shape) == v, k
+    assert sum(p.numel() for p in m.parameters()) == fx.meta['nparams']
+    assert [float(s) for s in m.stride] == fx.meta['stride']
