@@ -50,7 +50,7 @@ DEV float rcp_(float x) { return __builtin_amdgcn_rcpf(x); }
 DEV float sigmoidf_(float x) { return rcp_(1.0f + __expf(-x)); }
 
 // Activation codes shared with the host (dmayolo/_lib.py ACT_*).
-enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_HARDSWISH = 2, ACT_SIGMOID = 3, ACT_GELU = 4 };
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_HARDSWISH = 2, ACT_SIGMOID = 3, ACT_GELU = 4, ACT_RELU = 5 };
 
 DEV float act_fwd(int act, float u) {
   switch (act) {
@@ -58,6 +58,7 @@ DEV float act_fwd(int act, float u) {
     case ACT_HARDSWISH: return u * fminf(fmaxf(u + 3.0f, 0.0f), 6.0f) / 6.0f;
     case ACT_SIGMOID: return sigmoidf_(u);
     case ACT_GELU: return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f));
+    case ACT_RELU: return fmaxf(u, 0.0f);
     default: return u;
   }
 }
@@ -74,6 +75,7 @@ DEV float act_grad(int act, float u) {
       const float s = sigmoidf_(u);
       return s * (1.0f - s);
     }
+    case ACT_RELU: return u > 0.0f ? 1.0f : 0.0f;  // torch threshold_backward (result > 0)
     case ACT_GELU: {
       const float kA = 0.70710678118654752f, kB = 0.3989422804014327f;  // 1/sqrt2, 1/sqrt(2pi)
       return 0.5f * (1.0f + erff(u * kA)) + u * kB * expf(-0.5f * u * u);

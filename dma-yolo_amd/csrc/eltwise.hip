@@ -266,6 +266,198 @@ __global__ void s2d_kernel(const T* __restrict__ x, long xps, T* __restrict__ y,
   }
 }
 
+// ---------------------------------------------------------------- CBAM (models/common.py:260-310)
+// channel attention: [avg; max] global pools -> shared MLP (conv kernels) -> sigmoid(sum of halves);
+// spatial attention: out1 = x * ca, s2 = [mean_c out1, max_c out1] -> 7x7 conv + sigmoid (conv kernels)
+// -> out = out1 * sa.  Max-pool gradients go to the first maximum (torch's index semantics).
+template <typename T>
+__global__ void gpool_fwd_kernel(const T* __restrict__ x, long xps, int N, int HW, int C, T* __restrict__ out,
+                                 int* __restrict__ arg) {
+  const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), part = threadIdx.x >> 6;
+  __shared__ float ss[4][64], sm[4][64];
+  __shared__ int sa[4][64];
+  float s = 0.f, mx = -INFINITY;
+  int am = 0x7fffffff;
+  if (c < C) {
+    for (int p = part; p < HW; p += 4) {
+      const float v = to_f(x[((long)n * HW + p) * xps + c]);
+      s += v;
+      if (v > mx) { mx = v; am = p; }
+    }
+  }
+  ss[part][threadIdx.x & 63] = s;
+  sm[part][threadIdx.x & 63] = mx;
+  sa[part][threadIdx.x & 63] = am;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    const int l = threadIdx.x;
+    float t = 0.f, m = -INFINITY;
+    int a = 0x7fffffff;
+    for (int q = 0; q < 4; ++q) {
+      t += ss[q][l];
+      if (sm[q][l] > m || (sm[q][l] == m && sa[q][l] < a)) { m = sm[q][l]; a = sa[q][l]; }
+    }
+    out[(long)n * C + c] = from_f<T>(t / HW);
+    out[(long)(N + n) * C + c] = from_f<T>(m);
+    arg[(long)n * C + c] = a;
+  }
+}
+
+template <typename T>
+__global__ void gpool_bwd_kernel(const T* __restrict__ dz, const int* __restrict__ arg, T* __restrict__ dx, long dxps,
+                                 int accumulate, int N, int HW, int C) {
+  const long total = (long)N * HW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long t = i / C;
+    const int p = (int)(t % HW), n = (int)(t / HW);
+    float v = to_f(dz[(long)n * C + c]) / HW;
+    if (arg[(long)n * C + c] == p) v += to_f(dz[(long)(N + n) * C + c]);
+    T* o = dx + ((long)n * HW + p) * dxps + c;
+    if (accumulate) v += to_f(*o);
+    *o = from_f<T>(v);
+  }
+}
+
+// ca = sigmoid(z[:N] + z[N:]) (the two MLP branches); backward gives both halves the same gradient
+template <typename T>
+__global__ void halves_sigmoid_kernel(const T* __restrict__ z, int N, int C, T* __restrict__ ca, const T* __restrict__ dca,
+                                      T* __restrict__ dz) {
+  const long total = (long)N * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const float u = to_f(from_f<T>(to_f(z[i]) + to_f(z[i + total])));
+    const float s = sigmoidf_(u);
+    if (dca == nullptr) {
+      ca[i] = from_f<T>(s);
+    } else {
+      const float g = to_f(dca[i]) * s * (1.f - s);
+      dz[i] = from_f<T>(g);
+      dz[i + total] = from_f<T>(g);
+    }
+  }
+}
+
+// one wave per pixel: out1 = x * ca, s2 = (mean_c out1, max_c out1), am = first argmax channel
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) cbam_in_fwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ ca,
+                                                          int N, int HW, int C, T* __restrict__ out1,
+                                                          T* __restrict__ s2, int* __restrict__ am) {
+  const int lane = threadIdx.x & 63;
+  const long P = (long)N * HW;
+  for (long pix = blockIdx.x * 4L + (threadIdx.x >> 6); pix < P; pix += gridDim.x * 4L) {
+    const int n = (int)(pix / HW);
+    float s = 0.f, mx = -INFINITY;
+    int a = 0x7fffffff;
+    for (int c0 = lane * NV; c0 < C; c0 += 64 * NV) {
+      float xv[NV], cv[NV];
+      ldv<T, NV>(x + pix * xps + c0, xv);
+      ldv<T, NV>(ca + (long)n * C + c0, cv);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        xv[j] = to_f(from_f<T>(xv[j] * cv[j]));
+        s += xv[j];
+        if (xv[j] > mx) { mx = xv[j]; a = c0 + j; }
+      }
+      stv<T, NV>(out1 + pix * C + c0, xv);
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(mx, o, 64);
+      const int a2 = __shfl_xor(a, o, 64);
+      if (m2 > mx || (m2 == mx && a2 < a)) { mx = m2; a = a2; }
+    }
+    if (lane == 0) {
+      s2[pix * 2] = from_f<T>(s / C);
+      s2[pix * 2 + 1] = from_f<T>(mx);
+      am[pix] = a;
+    }
+  }
+}
+
+// backward: d_out1 total = d_out1 + d_mean / C + [c == am] d_max;  dx = total * ca;
+// dca[n][c] += sum over this wave's pixels of total * x  (fp32 atomics once per wave and channel)
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) cbam_in_bwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ ca,
+                                                          const T* __restrict__ dout1, long dps, const T* __restrict__ ds2,
+                                                          const int* __restrict__ am, int N, int HW, int C, int ppw,
+                                                          T* __restrict__ dx, long dxps, int accumulate,
+                                                          float* __restrict__ dca) {
+  const int lane = threadIdx.x & 63;
+  const long P = (long)N * HW;
+  const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const long p0 = w * ppw;
+  if (p0 >= P) return;
+  const long p1 = min(P, p0 + ppw);
+  for (int c0 = lane * NV; c0 < C; c0 += 64 * NV) {
+    float acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = 0.f;
+    int n = (int)(p0 / HW);
+    for (long pix = p0; pix < p1; ++pix) {
+      const int pn = (int)(pix / HW);
+      if (pn != n) {  // image boundary inside this wave's run: flush
+#pragma unroll
+        for (int j = 0; j < NV; ++j) { atomicAdd(dca + (long)n * C + c0 + j, acc[j]); acc[j] = 0.f; }
+        n = pn;
+      }
+      float xv[NV], cv[NV], gv[NV];
+      ldv<T, NV>(x + pix * xps + c0, xv);
+      ldv<T, NV>(ca + (long)n * C + c0, cv);
+      ldv<T, NV>(dout1 + pix * dps + c0, gv);
+      const float gm = to_f(ds2[pix * 2]) / C, gx = to_f(ds2[pix * 2 + 1]);
+      const int a = am[pix];
+      float o[NV];
+      if (accumulate) ldv<T, NV>(dx + pix * dxps + c0, o);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float t = gv[j] + gm + (c0 + j == a ? gx : 0.f);
+        acc[j] += t * xv[j];
+        o[j] = (accumulate ? o[j] : 0.f) + t * cv[j];
+      }
+      stv<T, NV>(dx + pix * dxps + c0, o);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) atomicAdd(dca + (long)n * C + c0 + j, acc[j]);
+  }
+}
+
+// out = out1 * sa (sa one value per pixel);  backward: d_out1 = d_out * sa, d_sa = sum_c d_out * out1
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) pixscale_kernel(const T* __restrict__ out1, const T* __restrict__ sa, long sps,
+                                                       int N, int HW, int C, T* __restrict__ out, long ops,
+                                                       const T* __restrict__ dout, long dps, T* __restrict__ dout1,
+                                                       T* __restrict__ dsa) {
+  const int lane = threadIdx.x & 63;
+  const long P = (long)N * HW;
+  for (long pix = blockIdx.x * 4L + (threadIdx.x >> 6); pix < P; pix += gridDim.x * 4L) {
+    const float sv = to_f(sa[pix * sps]);
+    float s = 0.f;
+    for (int c0 = lane * NV; c0 < C; c0 += 64 * NV) {
+      float a[NV];
+      ldv<T, NV>(out1 + pix * C + c0, a);
+      if (dout == nullptr) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) a[j] *= sv;
+        stv<T, NV>(out + pix * ops + c0, a);
+      } else {
+        float g[NV], d[NV];
+        ldv<T, NV>(dout + pix * dps + c0, g);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          s += g[j] * a[j];
+          d[j] = g[j] * sv;
+        }
+        stv<T, NV>(dout1 + pix * C + c0, d);
+      }
+    }
+    if (dout != nullptr) {
+      s = wave_sum(s);
+      if (lane == 0) dsa[pix] = from_f<T>(s);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- channel-slice copy with BiFPN weight
 // scale = wvec ? wvec[idx] / (sum(wvec[0..nw)) + eps) : 1
 DEV float bifpn_scale(const float* wv, int idx, int nw, float eps) {
@@ -673,6 +865,48 @@ DMY_API int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long
   if ((H | W) & 1) return (int)hipErrorInvalidValue;  // the reference's cat needs even sizes
   const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
   DISPATCH_TV(dtype, v, s2d_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, N, H, W, C, backward));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(N, ceil_div(C, 64));
+  DISPATCH_T(dtype, gpool_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)x, xps, N, HW, C, (T*)out, arg));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_gpool_bwd(int dtype, const void* dz, const int* arg, void* dx, long dxps, int accumulate, int N, int HW,
+                          int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, gpool_bwd_kernel<T><<<egrid((long)N * HW * C), 256, 0, st>>>((const T*)dz, arg, (T*)dx, dxps, accumulate, N, HW, C));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_halves_sigmoid(int dtype, const void* z, int N, int C, void* ca, const void* dca, void* dz, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, halves_sigmoid_kernel<T><<<egrid((long)N * C), 256, 0, st>>>((const T*)z, N, C, (T*)ca, (const T*)dca, (T*)dz));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_cbam_in_fwd(int dtype, const void* x, long xps, const void* ca, int N, int HW, int C, void* out1, void* s2,
+                            int* am, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const bool v = vec_ok(dtype, {C, xps}, {x, ca, out1});
+  DISPATCH_TV(dtype, v, cbam_in_fwd_kernel<T, NV><<<grid_cap(ceil_div((long)N * HW, 4), 8192), 256, 0, st>>>((const T*)x, xps, (const T*)ca, N, HW, C, (T*)out1, (T*)s2, am));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_cbam_in_bwd(int dtype, const void* x, long xps, const void* ca, const void* dout1, long dps,
+                            const void* ds2, const int* am, int N, int HW, int C, void* dx, long dxps, int accumulate,
+                            float* dca, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const bool v = vec_ok(dtype, {C, xps, dps, dxps}, {x, ca, dout1, dx});
+  const int ppw = 64;
+  const long waves = ceil_div((long)N * HW, ppw);
+  (void)hipMemsetAsync(dca, 0, sizeof(float) * (size_t)N * C, st);
+  DISPATCH_TV(dtype, v, cbam_in_bwd_kernel<T, NV><<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>((const T*)x, xps, (const T*)ca, (const T*)dout1, dps, (const T*)ds2, am, N, HW, C, ppw, (T*)dx, dxps, accumulate, dca));
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_pixscale(int dtype, const void* out1, const void* sa, long sps, int N, int HW, int C, void* out, long ops,
+                         const void* dout, long dps, void* dout1, void* dsa, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const bool v = vec_ok(dtype, {C, ops, dout ? dps : 0}, {out1, out, dout, dout1});
+  DISPATCH_TV(dtype, v, pixscale_kernel<T, NV><<<grid_cap(ceil_div((long)N * HW, 4), 8192), 256, 0, st>>>((const T*)out1, (const T*)sa, sps, N, HW, C, (T*)out, ops, (const T*)dout, dps, (T*)dout1, (T*)dsa));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long dps, long M, int C, const float* wv,

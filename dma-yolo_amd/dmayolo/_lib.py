@@ -70,6 +70,12 @@ SIGNATURES = {
     'dmy_tal_flatten': [I, P, L, I, I, I, I, I, I, P, I, P],
     'dmy_tal_detect_out': [I, P, I, I, I, P, P, P, P, P],
     'dmy_space_to_depth': [I, P, L, P, L, I, I, I, I, I, P],
+    'dmy_gpool_fwd': [I, P, L, I, I, I, P, P, P],
+    'dmy_gpool_bwd': [I, P, P, P, L, I, I, I, I, P],
+    'dmy_halves_sigmoid': [I, P, I, I, P, P, P, P],
+    'dmy_cbam_in_fwd': [I, P, L, P, I, I, I, P, P, P, P],
+    'dmy_cbam_in_bwd': [I, P, L, P, P, L, P, P, I, I, I, P, L, I, P, P],
+    'dmy_pixscale': [I, P, P, L, I, I, I, P, L, P, L, P, P, P],
     # nms.hip
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
@@ -128,4 +134,4 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU = 0, 1, 2, 3, 4
+ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU, ACT_RELU = 0, 1, 2, 3, 4, 5

@@ -8,7 +8,7 @@ hot path (torch is used for allocation and the current stream only).
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream, ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU  # noqa: F401
+from ._lib import call, ptr, stream, ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU, ACT_RELU  # noqa: F401
 
 DT = {torch.float32: 0, torch.bfloat16: 1}
 CL = torch.channels_last
@@ -732,3 +732,110 @@ class FlattenLevelsFn(torch.autograd.Function):
             call('dmy_tal_flatten', dcode(dF), ptr(dx), ctx.no, ctx.B, H, W, ctx.A, a0, ctx.no, ptr(dF), 1, stream())
             out.append(dx)
         return tuple(out)
+
+
+# ------------------------------------------------------------------ CBAM pieces (models/common.py:260-310)
+
+class GPoolFn(torch.autograd.Function):
+    """[N,C,H,W] -> [2N,C,1,1]: global average pool rows, then global max pool rows (first max)."""
+
+    @staticmethod
+    def forward(ctx, x, sink=None):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        z = new_act(2 * N, C, 1, 1, x)
+        arg = torch.empty((N, C), dtype=torch.int32, device=x.device)
+        call('dmy_gpool_fwd', dcode(x), ptr(x), xps, N, H * W, C, ptr(z), ptr(arg), stream())
+        ctx.save_for_backward(arg)
+        ctx.shape, ctx.sink = (N, C, H, W), sink
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dz = dz.contiguous()
+        buf, bps, acc = sink_target(ctx.sink, N, C, H, W, dz)
+        call('dmy_gpool_bwd', dcode(dz), ptr(dz), ptr(arg), ptr(buf), bps, acc, N, H * W, C, stream())
+        return sink_result(ctx.sink, buf), None
+
+
+class HalvesSigmoidFn(torch.autograd.Function):
+    """[2N,C,1,1] -> [N,C,1,1]: sigmoid(z[:N] + z[N:]) (CBAM channel attention: sigmoid(avgout + maxout))."""
+
+    @staticmethod
+    def forward(ctx, z):
+        z = z.contiguous()
+        N2, C = z.shape[:2]
+        ca = torch.empty((N2 // 2, C, 1, 1), dtype=z.dtype, device=z.device)
+        call('dmy_halves_sigmoid', dcode(z), ptr(z), N2 // 2, C, ptr(ca), None, None, stream())
+        ctx.save_for_backward(z)
+        return ca
+
+    @staticmethod
+    def backward(ctx, dca):
+        (z,) = ctx.saved_tensors
+        N2, C = z.shape[:2]
+        dca = dca.contiguous()
+        dz = torch.empty_like(z)
+        call('dmy_halves_sigmoid', dcode(z), ptr(z), N2 // 2, C, None, ptr(dca), ptr(dz), stream())
+        return dz
+
+
+class CBAMInFn(torch.autograd.Function):
+    """(x, ca) -> out1 = ca * x and s2 = cat(mean_c out1, max_c out1) (CBAM spatial-attention input)."""
+
+    @staticmethod
+    def forward(ctx, x, ca, sink=None):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        ca = ca.contiguous()
+        out1 = new_act(N, C, H, W, x)
+        s2 = new_act(N, 2, H, W, x)
+        am = torch.empty((N, H, W), dtype=torch.int32, device=x.device)
+        call('dmy_cbam_in_fwd', dcode(x), ptr(x), xps, ptr(ca), N, H * W, C, ptr(out1), ptr(s2), ptr(am), stream())
+        ctx.save_for_backward(x, ca, am)
+        ctx.xps, ctx.sink = xps, sink
+        return out1, s2
+
+    @staticmethod
+    def backward(ctx, dout1, ds2):
+        x, ca, am = ctx.saved_tensors
+        N, C, H, W = x.shape
+        if dout1 is None:
+            dout1 = torch.zeros_like(x)
+        dout1, dps = pixel_stride(dout1)
+        ds2 = torch.zeros((N, 2, H, W), dtype=x.dtype, device=x.device, memory_format=CL) if ds2 is None else \
+            ds2.contiguous(memory_format=CL)
+        buf, bps, acc = sink_target(ctx.sink, N, C, H, W, x)
+        dca = f32(N * C, x.device)
+        call('dmy_cbam_in_bwd', dcode(x), ptr(x), ctx.xps, ptr(ca), ptr(dout1), dps, ptr(ds2), ptr(am), N, H * W, C,
+             ptr(buf), bps, acc, ptr(dca), stream())
+        return sink_result(ctx.sink, buf), dca.view(N, C, 1, 1).to(ca.dtype), None
+
+
+class PixScaleFn(torch.autograd.Function):
+    """out = out1 * sa, sa one value per pixel [N,1,H,W] (CBAM: spatial_attention(out) * out)."""
+
+    @staticmethod
+    def forward(ctx, out1, sa):
+        out1 = out1.contiguous(memory_format=CL)
+        sa, sps = pixel_stride(sa)
+        N, C, H, W = out1.shape
+        out = new_act(N, C, H, W, out1)
+        call('dmy_pixscale', dcode(out1), ptr(out1), ptr(sa), sps, N, H * W, C, ptr(out), C, None, 0, None, None,
+             stream())
+        ctx.save_for_backward(out1, sa)
+        ctx.sps = sps
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out1, sa = ctx.saved_tensors
+        N, C, H, W = out1.shape
+        dout, dps = pixel_stride(dout)
+        dout1 = new_act(N, C, H, W, out1)
+        dsa = new_act(N, 1, H, W, out1)
+        call('dmy_pixscale', dcode(out1), ptr(out1), ptr(sa), ctx.sps, N, H * W, C, None, 0, ptr(dout), dps,
+             ptr(dout1), ptr(dsa), stream())
+        return dout1, dsa

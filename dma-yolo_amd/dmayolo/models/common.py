@@ -13,11 +13,12 @@ import torch
 import torch.nn as nn
 
 from .. import functional as Fn
-from ..functional import ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU
+from ..functional import ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GELU, ACT_RELU
 
 __all__ = ['autopad', 'Conv', 'Bottleneck', 'C3', 'SPPF', 'SPPFCSPC', 'SCConv', 'CoorAttention', 'CA',
            'CABottleneck', 'C3CA', 'Concat', 'AdConcat2', 'AdConcat3', 'Upsample', 'C3STR', 'SwinTransformerBlock',
-           'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath', 'space_to_depth']
+           'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath', 'space_to_depth', 'SPP', 'CBAM',
+           'ChannelAttentionModule', 'SpatialAttentionModule']
 
 
 def autopad(k, p=None):
@@ -38,6 +39,8 @@ def act_code(m):
         return ACT_SIGMOID
     if isinstance(m, nn.GELU):
         return ACT_GELU
+    if isinstance(m, nn.ReLU):
+        return ACT_RELU
     raise NotImplementedError(f'activation {type(m).__name__} has no gfx950 kernel')
 
 
@@ -262,6 +265,71 @@ class AdConcat3(AdConcat2):
     def forward(self, x):
         assert self.d == 1 and len(x) == 3
         return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
+
+
+class SPP(nn.Module):
+    """models/common.py:212-227: parallel max-pools (k = 5/9/13, 3/7/11, 3/5/7 in the config-5 YAML)."""
+
+    def __init__(self, c1, c2, k=(5, 9, 13)):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_ * (len(k) + 1), c2, 1, 1)
+        self.m = nn.ModuleList([nn.MaxPool2d(kernel_size=x, stride=1, padding=x // 2) for x in k])
+
+    def forward(self, x):
+        x = self.cv1(x)
+        sk = Fn.GradSink(len(self.m) + 1)  # x -> every pool and the concat
+        ys = [Fn.MaxPoolFn.apply(x, m.kernel_size, sk) for m in self.m]
+        return self.cv2(Fn.ConcatFn.apply(None, 0.0, (sk,) + (None,) * len(ys), x, *ys))
+
+
+class ChannelAttentionModule(nn.Module):
+    """models/common.py:260-285: sigmoid(MLP(avgpool x) + MLP(maxpool x)); both branches go through the
+    shared MLP in one [2N]-row pass (1x1 conv kernels), the halves are summed in the sigmoid kernel."""
+
+    def __init__(self, c1, reduction=16):
+        super().__init__()
+        mid = c1 // reduction
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.shared_MLP = nn.Sequential(nn.Linear(c1, mid), nn.ReLU(), nn.Linear(mid, c1))
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, x, sink=None):
+        l1, l2 = self.shared_MLP[0], self.shared_MLP[2]
+        mid, c1 = l1.weight.shape
+        z = Fn.GPoolFn.apply(x, sink)
+        h = Fn.conv_bn_act(z, l1.weight.view(mid, c1, 1, 1), l1.bias, None, 1, 0, ACT_RELU)
+        z2 = Fn.conv_bn_act(h, l2.weight.view(c1, mid, 1, 1), l2.bias, None, 1, 0, ACT_NONE)
+        return Fn.HalvesSigmoidFn.apply(z2)
+
+
+class SpatialAttentionModule(nn.Module):
+    """models/common.py:287-300."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv2d = nn.Conv2d(in_channels=2, out_channels=1, kernel_size=7, stride=1, padding=3)
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, s2):
+        return conv_forward(self.conv2d, None, self.sigmoid, s2)
+
+
+class CBAM(nn.Module):
+    """models/common.py:302-310: out = ca(x) * x;  out = sa(out) * out."""
+
+    def __init__(self, c1, c2):
+        super().__init__()
+        self.channel_attention = ChannelAttentionModule(c1)
+        self.spatial_attention = SpatialAttentionModule()
+
+    def forward(self, x):
+        sk = Fn.GradSink(2)  # x -> the pools and the channel scaling
+        ca = self.channel_attention(x, sk)
+        out1, s2 = Fn.CBAMInFn.apply(x, ca, sk)
+        return Fn.PixScaleFn.apply(out1, self.spatial_attention(s2))
 
 
 class space_to_depth(nn.Module):

@@ -240,7 +240,7 @@ def parse_model(d, ch):
     no = na * (nc + 5)
     ev = dict(ns, nc=nc, anchors=anchors)
     chan_mods = (C.Conv, C.Bottleneck, C.SPPF, C.C3, C.C3STR, C.CoorAttention, C.CABottleneck, C.C3CA, C.SPPFCSPC,
-                 C.SCConv)
+                 C.SCConv, C.SPP, C.CBAM)
     rep_mods = (C.C3, C.C3STR, C.C3CA)
     layers, save, c2 = [], [], ch[-1]
     for i, (f, n, m, args) in enumerate(d['backbone'] + d['head']):

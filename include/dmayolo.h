@@ -171,6 +171,20 @@ int dmy_tal_detect_out(int dtype, const void* F, int B, int nc, int nl, const in
 int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long yps, int N, int H, int W, int C, int backward,
                        void* stream);
 
+
+/* ---- config-5 modules: CBAM (models/common.py:260-310) channel / spatial attention pieces; SPP
+ *      (common.py:212-227) reuses dmy_maxpool_* with k = 3..13. */
+int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, void* stream);
+int dmy_gpool_bwd(int dtype, const void* dz, const int* arg, void* dx, long dxps, int accumulate, int N, int HW, int C,
+                  void* stream);
+int dmy_halves_sigmoid(int dtype, const void* z, int N, int C, void* ca, const void* dca, void* dz, void* stream);
+int dmy_cbam_in_fwd(int dtype, const void* x, long xps, const void* ca, int N, int HW, int C, void* out1, void* s2,
+                    int* am, void* stream);
+int dmy_cbam_in_bwd(int dtype, const void* x, long xps, const void* ca, const void* dout1, long dps, const void* ds2,
+                    const int* am, int N, int HW, int C, void* dx, long dxps, int accumulate, float* dca, void* stream);
+int dmy_pixscale(int dtype, const void* out1, const void* sa, long sps, int N, int HW, int C, void* out, long ops,
+                 const void* dout, long dps, void* dout1, void* dsa, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,63 @@ class SPPF(nn.Module):
         return self.cv2(torch.cat([a, b, c, self.m(c)], 1))
 
 
+class SPP(nn.Module):
+    """models/common.py:212-227: parallel max-pools (k odd, stride 1, pad k//2) of cv1(x), concat, cv2."""
+
+    def __init__(self, c1, c2, k=(5, 9, 13)):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c_ * (len(k) + 1), c2, 1, 1)
+        self.m = nn.ModuleList([nn.MaxPool2d(kernel_size=x, stride=1, padding=x // 2) for x in k])
+
+    def forward(self, x):
+        x = self.cv1(x)
+        return self.cv2(torch.cat([x] + [m(x) for m in self.m], 1))
+
+
+class ChannelAttentionModule(nn.Module):
+    """models/common.py:260-285: sigmoid(MLP(avgpool x) + MLP(maxpool x)), MLP = Linear-ReLU-Linear, r = 16."""
+
+    def __init__(self, c1, reduction=16):
+        super().__init__()
+        mid = c1 // reduction
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.shared_MLP = nn.Sequential(nn.Linear(c1, mid), nn.ReLU(), nn.Linear(mid, c1))
+
+    def forward(self, x):
+        b = x.shape[0]
+        a = self.shared_MLP(self.avg_pool(x).view(b, -1))
+        m = self.shared_MLP(self.max_pool(x).view(b, -1))
+        return torch.sigmoid(a + m)[:, :, None, None]
+
+
+class SpatialAttentionModule(nn.Module):
+    """models/common.py:287-300: sigmoid(conv7x7(cat(mean_c x, max_c x)))."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv2d = nn.Conv2d(2, 1, kernel_size=7, stride=1, padding=3)
+
+    def forward(self, x):
+        s = torch.cat([x.mean(1, keepdim=True), x.max(1, keepdim=True)[0]], 1)
+        return torch.sigmoid(self.conv2d(s))
+
+
+class CBAM(nn.Module):
+    """models/common.py:302-310."""
+
+    def __init__(self, c1, c2):
+        super().__init__()
+        self.channel_attention = ChannelAttentionModule(c1)
+        self.spatial_attention = SpatialAttentionModule()
+
+    def forward(self, x):
+        out = self.channel_attention(x) * x
+        return self.spatial_attention(out) * out
+
+
 class SPPFCSPC(nn.Module):
     """models/common.py:1257-1276."""
 
@@ -371,7 +428,7 @@ def make_divisible(x, d):
 
 
 _CHANNEL_MODS = ('Conv', 'Bottleneck', 'SPPF', 'C3', 'C3STR', 'CoorAttention', 'CA', 'CABottleneck', 'C3CA',
-                 'SPPFCSPC', 'SCConv')
+                 'SPPFCSPC', 'SCConv', 'SPP', 'CBAM')
 _REPEAT_MODS = ('C3', 'C3STR', 'C3CA')
 
 

@@ -13,6 +13,7 @@ def product_modules():
         'CoorAttention': P.CoorAttention, 'C3CA': P.C3CA, 'SPPF': P.SPPF, 'SPPFCSPC': P.SPPFCSPC,
         'Upsample': P.Upsample, 'AdConcat2': P.AdConcat2, 'AdConcat3': P.AdConcat3, 'Concat': P.Concat,
         'SwinTransformerLayer': lambda c, h, ws, sh: P.SwinTransformerLayer(c, h, ws, sh), 'C3STR': P.C3STR,
+        'SPP': lambda c1, c2, k: P.SPP(c1, c2, tuple(k)), 'CBAM': P.CBAM,
     }
 
 

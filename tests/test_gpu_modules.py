@@ -27,7 +27,7 @@ def test_module_vs_oracle_bf16(name):
     _, ref = run_case(name, ORACLE_MODS, 'cpu')
     # max-pool chains route the gradient through argmax; bf16 rounding of the pooled activations
     # creates ties that legitimately move it to a neighbouring pixel -> looser input-grad bound
-    gtol = 0.3 if name.startswith('sppf') else 6e-2
+    gtol = 0.3 if name.startswith(('spp', 'cbam')) else 6e-2
     for a, b in zip(res['out'], ref['out']):
         assert rel_err(a, b) < 3e-2, rel_err(a, b)
     for a, b in zip(res['gin'], ref['gin']):

@@ -12,11 +12,12 @@ MODS = {
     'CoorAttention': onn.CoorAttention, 'C3CA': onn.C3CA, 'SPPF': onn.SPPF, 'SPPFCSPC': onn.SPPFCSPC,
     'Upsample': torch.nn.Upsample, 'AdConcat2': onn.AdConcat2, 'AdConcat3': onn.AdConcat3, 'Concat': onn.Concat,
     'SwinTransformerLayer': lambda c, h, ws, sh: onn.SwinTransformerLayer(c, h, ws, sh), 'C3STR': onn.C3STR,
+    'SPP': lambda c1, c2, k: onn.SPP(c1, c2, tuple(k)), 'CBAM': onn.CBAM,
 }
 
 MODULE_CASES = [n for n in golden_names('') if n.split('_')[0] in (
     'conv', 'bottleneck', 'c3', 'scconv', 'ca', 'c3ca', 'sppf', 'sppfcspc', 'upsample', 'adconcat2',
-    'adconcat3', 'concat', 'swin', 'c3str') and n != 'conv_fuse']
+    'adconcat3', 'concat', 'swin', 'c3str', 'spp', 'cbam') and n != 'conv_fuse']
 
 
 def run_module_case(name, build=None, device='cpu', dtype=torch.float32):

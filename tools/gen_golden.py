@@ -193,6 +193,13 @@ def gen_modules():
         mask = m.create_mask(x, hh, ww)
         np.savez_compressed(os.path.join(OUT, f'swinmask_{tag}.npz'), meta=json.dumps(dict(H=hh, W=ww)),
                             mask=npy(mask))
+    # 8. config-5 modules (yolov5l-xs-tr-cbam-spp-bifpn.yaml): SPP variants, CBAM
+    for (k, tag) in [((5, 9, 13), 'k5913'), ((3, 5, 7), 'k357')]:
+        torch.manual_seed(17)
+        module_case(f'spp_{tag}', C.SPP(32, 32, k), [rnd(2, 32, 11, 9, seed=18)], dict(module='SPP', args=[32, 32, list(k)]))
+    for (c, hw, tag) in [(32, (10, 12), 'c32'), (64, (7, 5), 'c64')]:
+        torch.manual_seed(19)
+        module_case(f'cbam_{tag}', C.CBAM(c, c), [rnd(2, c, *hw, seed=20)], dict(module='CBAM', args=[c, c]))
     torch.manual_seed(8)
     module_case('c3str', C.C3STR(64, 64, 3, False), [rnd(1, 64, 16, 16, seed=15, scale=0.5)],
                 dict(module='C3STR', args=[64, 64, 3, False]))
