@@ -5,6 +5,7 @@
 //   CoorAttention pooling / re-weighting (:1183-1207), input normalisation (train.py:402).
 #include "common.h"
 #include <initializer_list>
+#include <type_traits>
 
 namespace {
 
@@ -35,71 +36,115 @@ DEV void vidx(long i, int H, int W, int CV, int NV, int& b, int& h, int& w, int&
 }
 
 // ---------------------------------------------------------------- max-pool (k odd, stride 1, pad k/2)
-// Writes the first-max window offset (row-major scan, like ATen's CPU kernel) for the backward.
-template <typename T, int NV>
-__global__ void maxpool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps,
-                                   uint8_t* __restrict__ arg, int N, int H, int W, int C, int k) {
+// ATen's max_pool2d rule (CPU and CUDA kernels alike): scan the window row-major, update when
+// `v > best || isnan(v)`, start from -inf with the index of the first in-image tap.  The window
+// offset of the winner (dh * k + dw) is written for the backward.  KS > 0: compile-time window,
+// every tap is loaded branch-free (out-of-image taps read the centre pixel and are masked), so the
+// loads of a window issue back to back; KS = 0: runtime window (k > 13).
+template <typename T, int NV, int KS>
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps,
+                                                          uint8_t* __restrict__ arg, int N, int H, int W, int C, int kr) {
+  const int k = KS > 0 ? KS : kr;
   const int CV = C / NV;
   const long total = (long)N * H * W * CV;
   const int p = k / 2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int b, h, w, c;
     vidx(i, H, W, CV, NV, b, h, w, c);
+    const int h0 = h - p, w0 = w - p;
+    const int first = ((h0 < 0 ? 0 : h0) - h0) * k + ((w0 < 0 ? 0 : w0) - w0);
     float best[NV];
     int bi[NV];
-    bool nan[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) { best[j] = -INFINITY; bi[j] = 0; nan[j] = false; }
-    for (int dh = 0; dh < k; ++dh) {
-      const int hh = h - p + dh;
-      if (hh < 0 || hh >= H) continue;
-      for (int dw = 0; dw < k; ++dw) {
-        const int ww = w - p + dw;
-        if (ww < 0 || ww >= W) continue;
-        float v[NV];
-        ldv<T, NV>(x + (((long)b * H + hh) * W + ww) * xps + c, v);
+    for (int j = 0; j < NV; ++j) { best[j] = -INFINITY; bi[j] = first; }
+    const T* xb = x + (long)b * H * W * xps + c;
+    if constexpr (KS > 0) {
+      // one window row per batch: KS independent loads in flight, 32-bit offsets inside the image
+      const int ixps = (int)xps;
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          if (!nan[j] && (v[j] > best[j] || isnan(v[j]))) {
-            best[j] = v[j];
-            bi[j] = dh * k + dw;
-            nan[j] = isnan(v[j]);
+      for (int dh = 0; dh < KS; ++dh) {
+        const int hh = h0 + dh;
+        const bool hok = (unsigned)hh < (unsigned)H;
+        float v[KS][NV];
+#pragma unroll
+        for (int dw = 0; dw < KS; ++dw) {
+          const int ww = w0 + dw;
+          const bool ok = hok && (unsigned)ww < (unsigned)W;
+          ldv<T, NV>(xb + ((ok ? hh : h) * W + (ok ? ww : w)) * ixps, v[dw]);
+        }
+#pragma unroll
+        for (int dw = 0; dw < KS; ++dw) {
+          const int ww = w0 + dw;
+          const bool ok = hok && (unsigned)ww < (unsigned)W;
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            // bitwise (not short-circuit) so the selects stay branch-free
+            const float vv = ok ? v[dw][j] : -INFINITY;
+            const unsigned up = (unsigned)(vv > best[j]) | (unsigned)__builtin_isnan(vv);
+            best[j] = up ? vv : best[j];
+            bi[j] = up ? dh * KS + dw : bi[j];
+          }
+        }
+      }
+    }
+    if constexpr (KS == 0) {
+      for (int dh = 0; dh < k; ++dh) {
+        const int hh = h0 + dh;
+        if ((unsigned)hh >= (unsigned)H) continue;
+        for (int dw = 0; dw < k; ++dw) {
+          const int ww = w0 + dw;
+          if ((unsigned)ww >= (unsigned)W) continue;
+          float v[NV];
+          ldv<T, NV>(xb + ((long)hh * W + ww) * xps, v);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            const bool up = v[j] > best[j] || isnan(v[j]);
+            best[j] = up ? v[j] : best[j];
+            bi[j] = up ? dh * k + dw : bi[j];
           }
         }
       }
     }
     const long pix = ((long)b * H + h) * W + w;
     stv<T, NV>(y + pix * yps + c, best);
+    // one packed store of the NV argmax bytes
+    uint8_t a[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) arg[pix * C + c + j] = (uint8_t)bi[j];
+    for (int j = 0; j < NV; ++j) a[j] = (uint8_t)bi[j];
+    if constexpr (NV == 8) *reinterpret_cast<uint2*>(arg + pix * C + c) = *reinterpret_cast<const uint2*>(a);
+    else if constexpr (NV == 4) *reinterpret_cast<uint32_t*>(arg + pix * C + c) = *reinterpret_cast<const uint32_t*>(a);
+    else
+#pragma unroll
+      for (int j = 0; j < NV; ++j) arg[pix * C + c + j] = a[j];
   }
 }
 
-// dx[p] = sum of dy[q] over windows q whose argmax is p (gather: deterministic, no atomics)
+// dx[p] = sum of dy[q] over windows q whose argmax is p (gather: deterministic, no atomics); only the
+// dy vectors that route to p are loaded.
 template <typename T, int NV>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, long dps, const uint8_t* __restrict__ arg,
-                                   T* __restrict__ dx, long dxps, int accumulate, int N, int H, int W, int C, int k) {
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const T* __restrict__ dy, long dps, const uint8_t* __restrict__ arg,
+                                                          T* __restrict__ dx, long dxps, int accumulate, int N, int H, int W,
+                                                          int C, int kr) {
+  const int k = kr;
   const int CV = C / NV;
   const long total = (long)N * H * W * CV;
   const int p = k / 2;
+  using AW = typename std::conditional<NV == 8, uint2, typename std::conditional<NV == 4, uint32_t, uint8_t>::type>::type;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int b, h, w, c;
     vidx(i, H, W, CV, NV, b, h, w, c);
     float s[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) s[j] = 0.f;
+    const long img = (long)b * H * W;
     for (int oh = h - p; oh <= h + p; ++oh) {
       if (oh < 0 || oh >= H) continue;
       for (int ow = w - p; ow <= w + p; ++ow) {
         if (ow < 0 || ow >= W) continue;
-        const long q = ((long)b * H + oh) * W + ow;
+        const long q = img + (long)oh * W + ow;
         const int want = (h - oh + p) * k + (w - ow + p);
         uint8_t a[NV];
-        if constexpr (NV == 8) *reinterpret_cast<uint2*>(a) = *reinterpret_cast<const uint2*>(arg + q * C + c);
-        else if constexpr (NV == 4) *reinterpret_cast<uint32_t*>(a) = *reinterpret_cast<const uint32_t*>(arg + q * C + c);
-        else
-#pragma unroll
-          for (int j = 0; j < NV; ++j) a[j] = arg[q * C + c + j];
+        *reinterpret_cast<AW*>(a) = *reinterpret_cast<const AW*>(arg + q * C + c);
         bool any = false;
 #pragma unroll
         for (int j = 0; j < NV; ++j) any |= a[j] == want;
@@ -821,13 +866,26 @@ DMY_API int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yp
                             int W, int C, int k, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
-  DISPATCH_TV(dtype, v, maxpool_fwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, arg, N, H, W, C, k));
+  if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;  // uint8 window offsets
+  const int g = egrid((long)N * H * W * C / (v ? (dtype ? 8 : 4) : 1));
+#define MP_FWD(KS) DISPATCH_TV(dtype, v, maxpool_fwd_kernel<T, NV, KS><<<g, 256, 0, st>>>((const T*)x, xps, (T*)y, yps, arg, N, H, W, C, k))
+  switch ((long)H * W * xps < (1L << 31) ? k : 0) {  // compile-time windows use 32-bit in-image offsets
+    case 3: MP_FWD(3); break;
+    case 5: MP_FWD(5); break;
+    case 7: MP_FWD(7); break;
+    case 9: MP_FWD(9); break;
+    case 11: MP_FWD(11); break;
+    case 13: MP_FWD(13); break;
+    default: MP_FWD(0); break;
+  }
+#undef MP_FWD
   return (int)hipGetLastError();
 }
 DMY_API int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned char* arg, void* dx, long dxps,
                             int accumulate, int N, int H, int W, int C, int k, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
+  if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;
   DISPATCH_TV(dtype, v, maxpool_bwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)dy, dps, arg, (T*)dx, dxps, accumulate, N, H, W, C, k));
   return (int)hipGetLastError();
 }

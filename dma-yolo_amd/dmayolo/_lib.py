@@ -76,6 +76,11 @@ SIGNATURES = {
     'dmy_cbam_in_fwd': [I, P, L, P, I, I, I, P, P, P, P],
     'dmy_cbam_in_bwd': [I, P, L, P, P, L, P, P, I, I, I, P, L, I, P, P],
     'dmy_pixscale': [I, P, P, L, I, I, I, P, L, P, L, P, P, P],
+    # mha.hip
+    'dmy_mha_fwd': [I, P, L, P, L, P, L, P, L, P, I, I, I, I, F, P],
+    'dmy_mha_fwd_ref': [I, P, L, P, L, P, L, P, L, P, I, I, I, I, F, P],
+    'dmy_mha_bwd': [I, P, L, P, L, P, L, P, P, L, P, P, P, P, P, I, I, I, I, F, P],
+    'dmy_dropout': [I, P, L, P, L, L, I, F, ctypes.c_ulonglong, P],
     # nms.hip
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],

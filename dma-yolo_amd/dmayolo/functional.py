@@ -660,6 +660,71 @@ class WinAttnFn(torch.autograd.Function):
         return dqkv, dtab, None, None, None
 
 
+class MHAFn(torch.autograd.Function):
+    """Global multi-head attention core of nn.MultiheadAttention (common.py:323, C3TR): q, k, v are the
+    in-projected NHWC token tensors [N, c, H, W] (tokens = the H*W pixels of one image); returns
+    softmax(q k^T / sqrt(d)) v per head, [N, c, H, W].  Kernels: csrc/mha.hip (flash-style, nothing
+    L x L is stored; the backward recomputes P from the saved log-sum-exp)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, nh):
+        q, qps = pixel_stride(q)
+        k, kps = pixel_stride(k)
+        v, vps = pixel_stride(v)
+        N, C, H, W = q.shape
+        assert C % nh == 0 and k.shape == q.shape and v.shape == q.shape
+        d, L = C // nh, H * W
+        o = new_act(N, C, H, W, q)
+        lse = f32(N * nh * L, q.device)
+        call('dmy_mha_fwd', dcode(q), ptr(q), qps, ptr(k), kps, ptr(v), vps, ptr(o), C, ptr(lse), N, L, nh, d,
+             float(d) ** -0.5, stream())
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.ps, ctx.nh = (qps, kps, vps), nh
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        qps, kps, vps = ctx.ps
+        N, C, H, W = q.shape
+        nh = ctx.nh
+        d, L = C // nh, H * W
+        do = do.to(q.dtype).contiguous(memory_format=CL)
+        dq, dk, dv = new_act(N, C, H, W, q), new_act(N, C, H, W, q), new_act(N, C, H, W, q)
+        Dq = f32(N * nh * L, q.device)
+        call('dmy_mha_bwd', dcode(q), ptr(q), qps, ptr(k), kps, ptr(v), vps, ptr(o), ptr(do), C, ptr(lse), ptr(Dq),
+             ptr(dq), ptr(dk), ptr(dv), N, L, nh, d, float(d) ** -0.5, stream())
+        return dq, dk, dv, None
+
+
+def _seed():
+    """a fresh 63-bit dropout seed from torch's CPU generator (no device sync)"""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64))
+
+
+class DropoutFn(torch.autograd.Function):
+    """nn.Dropout(p) in train mode (common.py:328): y = x * keep / (1 - p); the keep mask is a counter
+    hash of (seed, element index), regenerated in the backward."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        x, xps = pixel_stride(x)
+        N, C, H, W = x.shape
+        y = new_act(N, C, H, W, x)
+        seed = _seed()
+        call('dmy_dropout', dcode(x), ptr(x), xps, ptr(y), C, N * H * W, C, float(p), seed, stream())
+        ctx.p, ctx.seed = p, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy, dps = pixel_stride(dy)
+        N, C, H, W = dy.shape
+        dx = new_act(N, C, H, W, dy)
+        call('dmy_dropout', dcode(dy), ptr(dy), dps, ptr(dx), C, N * H * W, C, float(ctx.p), ctx.seed, stream())
+        return dx, None
+
+
 class SampleScaleFn(torch.autograd.Function):
     """y = x * s[b] (DropPath with a pre-drawn per-sample keep mask, common.py:386-403)."""
 

@@ -18,7 +18,7 @@ from ..functional import ACT_NONE, ACT_SILU, ACT_HARDSWISH, ACT_SIGMOID, ACT_GEL
 __all__ = ['autopad', 'Conv', 'Bottleneck', 'C3', 'SPPF', 'SPPFCSPC', 'SCConv', 'CoorAttention', 'CA',
            'CABottleneck', 'C3CA', 'Concat', 'AdConcat2', 'AdConcat3', 'Upsample', 'C3STR', 'SwinTransformerBlock',
            'SwinTransformerLayer', 'WindowAttention', 'Mlp', 'DropPath', 'space_to_depth', 'SPP', 'CBAM',
-           'ChannelAttentionModule', 'SpatialAttentionModule']
+           'ChannelAttentionModule', 'SpatialAttentionModule', 'C3TR', 'TransformerBlock', 'TransformerLayer']
 
 
 def autopad(k, p=None):
@@ -368,3 +368,84 @@ class C3STR(C3):
         super().__init__(c1, c2, n, shortcut, g, e)
         c_ = int(c2 * e)
         self.m = SwinTransformerBlock(c_, c_, c_ // 32, n)
+
+
+# ------------------------------------------------------------------ C3TR (config 5: global MHSA over P5 tokens)
+
+class TransformerLayer(nn.Module):
+    """models/common.py:312-336: x + Dropout(MHA(q(LN1 x), k(LN1 x), v(LN1 x))); x + Dropout(fc2(Dropout(
+    ReLU(fc1(LN2 x))))).  `ma` is the real nn.MultiheadAttention (state_dict keys ma.in_proj_weight /
+    in_proj_bias / out_proj.*; train.py's optimizer grouping skips in_proj_*); its
+    projections run on the implicit-GEMM kernels and the attention core on csrc/mha.hip.  Tokens are
+    the pixels of the NHWC activation, so the reference's [HW, b, c] sequence-first transposes are free."""
+
+    def __init__(self, c, num_heads):
+        super().__init__()
+        self.ln1 = nn.LayerNorm(c)
+        self.q = nn.Linear(c, c, bias=False)
+        self.k = nn.Linear(c, c, bias=False)
+        self.v = nn.Linear(c, c, bias=False)
+        self.ma = nn.MultiheadAttention(embed_dim=c, num_heads=num_heads)
+        self.ln2 = nn.LayerNorm(c)
+        self.fc1 = nn.Linear(c, 4 * c, bias=False)
+        self.fc2 = nn.Linear(4 * c, c, bias=False)
+        self.dropout = nn.Dropout(0.1)
+        self.act = nn.ReLU(True)
+
+    @staticmethod
+    def _lin(x, w, b=None, act=ACT_NONE, **kw):
+        return Fn.conv_bn_act(x, w.view(w.shape[0], w.shape[1], 1, 1), b, None, 1, 0, act, **kw)
+
+    def forward(self, x):
+        c = x.shape[1]
+        ma = self.ma
+        drop = self.training and self.dropout.p > 0
+        p = self.dropout.p
+        s1, su, s2 = Fn.GradSink(2), Fn.GradSink(3), Fn.GradSink(2)  # x -> ln1 + residual; u -> q/k/v; x2 -> ln2 + residual
+        u = Fn.LayerNormFn.apply(x, self.ln1.weight, self.ln1.bias, self.ln1.eps, s1)
+        W, bi = ma.in_proj_weight, ma.in_proj_bias
+        q = self._lin(self._lin(u, self.q.weight, xsink=su), W[:c], bi[:c])
+        k = self._lin(self._lin(u, self.k.weight, xsink=su), W[c:2 * c], bi[c:2 * c])
+        v = self._lin(self._lin(u, self.v.weight, xsink=su), W[2 * c:], bi[2 * c:])
+        o = Fn.MHAFn.apply(q, k, v, ma.num_heads)
+        if drop:
+            x = Fn.AddFn.apply(x, Fn.DropoutFn.apply(self._lin(o, ma.out_proj.weight, ma.out_proj.bias), p), s1)
+        else:
+            x = self._lin(o, ma.out_proj.weight, ma.out_proj.bias, res=x, rsink=s1)
+        u2 = Fn.LayerNormFn.apply(x, self.ln2.weight, self.ln2.bias, self.ln2.eps, s2)
+        h = self._lin(u2, self.fc1.weight, act=ACT_RELU)
+        if drop:
+            return Fn.AddFn.apply(x, Fn.DropoutFn.apply(self._lin(Fn.DropoutFn.apply(h, p), self.fc2.weight), p), s2)
+        return self._lin(h, self.fc2.weight, res=x, rsink=s2)
+
+
+class TransformerBlock(nn.Module):
+    """models/common.py:338-355: (optional Conv) -> p + linear(p) (learned position term, residual fused
+    into the GEMM epilogue) -> n TransformerLayers; tokens stay in the NHWC activation."""
+
+    def __init__(self, c1, c2, num_heads, num_layers):
+        super().__init__()
+        self.conv = None
+        if c1 != c2:
+            self.conv = Conv(c1, c2)
+        self.linear = nn.Linear(c2, c2)
+        self.tr = nn.Sequential(*(TransformerLayer(c2, num_heads) for _ in range(num_layers)))
+        self.c2 = c2
+
+    def forward(self, x):
+        if self.conv is not None:
+            x = self.conv(x)
+        sk = Fn.GradSink(2)  # p -> linear + residual
+        w = self.linear.weight
+        p = Fn.conv_bn_act(x, w.view(self.c2, self.c2, 1, 1), self.linear.bias, None, 1, 0, ACT_NONE, res=x,
+                           xsink=sk, rsink=sk)
+        return self.tr(p)
+
+
+class C3TR(C3):
+    """models/common.py:184-189: C3 whose bottleneck stack is TransformerBlock(c_, c_, 4 heads, n)."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = TransformerBlock(c_, c_, 4, n)

@@ -239,9 +239,9 @@ def parse_model(d, ch):
     na = (len(anchors[0]) // 2) if isinstance(anchors, list) else anchors
     no = na * (nc + 5)
     ev = dict(ns, nc=nc, anchors=anchors)
-    chan_mods = (C.Conv, C.Bottleneck, C.SPPF, C.C3, C.C3STR, C.CoorAttention, C.CABottleneck, C.C3CA, C.SPPFCSPC,
-                 C.SCConv, C.SPP, C.CBAM)
-    rep_mods = (C.C3, C.C3STR, C.C3CA)
+    chan_mods = (C.Conv, C.Bottleneck, C.SPPF, C.C3, C.C3TR, C.C3STR, C.CoorAttention, C.CABottleneck, C.C3CA,
+                 C.SPPFCSPC, C.SCConv, C.SPP, C.CBAM)
+    rep_mods = (C.C3, C.C3TR, C.C3STR, C.C3CA)
     layers, save, c2 = [], [], ch[-1]
     for i, (f, n, m, args) in enumerate(d['backbone'] + d['head']):
         m = eval(m, ev) if isinstance(m, str) else m

@@ -185,6 +185,25 @@ int dmy_cbam_in_bwd(int dtype, const void* x, long xps, const void* ca, const vo
 int dmy_pixscale(int dtype, const void* out1, const void* sa, long sps, int N, int HW, int C, void* out, long ops,
                  const void* dout, long dps, void* dout1, void* dsa, void* stream);
 
+/* ---- config-5 C3TR (models/common.py:184-189, 312-355): the attention core of the
+ *      nn.MultiheadAttention (common.py:323; torch multi_head_attention_forward: softmax(q k^T / sqrt(d)) v
+ *      per head, after the in-projection) over the H*W tokens of each image, and the TransformerLayer
+ *      nn.Dropout(0.1) (common.py:328).  q/k/v/o are NHWC token rows [B*L][ps], head h = columns
+ *      [h d, h d + d); lse2 = fp32 [B][nh][L] (log2-domain log-sum-exp, saved for the backward);
+ *      Dq = fp32 workspace [B][nh][L]; dq/dk/dv use the token stride `ops`.  d <= 128; bf16 with
+ *      d in {32, 64, 128} runs on MFMA, everything else on the fp32-math generic kernels.
+ *      dmy_mha_fwd_ref always runs the generic kernel (test reference for the MFMA path). */
+int dmy_mha_fwd(int dtype, const void* q, long qps, const void* k, long kps, const void* v, long vps, void* o, long ops,
+                float* lse2, int B, int L, int nh, int d, float scale, void* stream);
+int dmy_mha_fwd_ref(int dtype, const void* q, long qps, const void* k, long kps, const void* v, long vps, void* o,
+                    long ops, float* lse2, int B, int L, int nh, int d, float scale, void* stream);
+int dmy_mha_bwd(int dtype, const void* q, long qps, const void* k, long kps, const void* v, long vps, const void* o,
+                const void* dout, long ops, const float* lse2, float* Dq, void* dq, void* dk, void* dv, int B, int L,
+                int nh, int d, float scale, void* stream);
+/* y[m][c] = x[m][c] * (u(seed, m * C + c) >= p) / (1 - p); the same call with the same seed on dy is the backward */
+int dmy_dropout(int dtype, const void* x, long xps, void* y, long yps, long M, int C, float p, unsigned long long seed,
+                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -392,6 +392,81 @@ class C3STR(C3):
         self.m = SwinTransformerBlock(h, h, h // 32, n)
 
 
+# ---------------------------------------------------------------- C3TR (config 5: global MHSA over P5 tokens)
+
+class TransformerLayer(nn.Module):
+    """models/common.py:312-336: x + Dropout(MHA(q(LN1 x), k(LN1 x), v(LN1 x))), then
+    x + Dropout(fc2(Dropout(ReLU(fc1(LN2 x))))).  The nn.MultiheadAttention (common.py:323) is
+    restated with explicit math (torch/nn/functional.py multi_head_attention_forward, need_weights
+    path: in-projection, q scaled by head_dim^-1/2, softmax(q k^T), @ v, out-projection); the module
+    is kept only as the holder of in_proj_weight / in_proj_bias / out_proj (state_dict keys)."""
+
+    def __init__(self, c, num_heads):
+        super().__init__()
+        self.ln1 = nn.LayerNorm(c)
+        self.q = nn.Linear(c, c, bias=False)
+        self.k = nn.Linear(c, c, bias=False)
+        self.v = nn.Linear(c, c, bias=False)
+        self.ma = nn.MultiheadAttention(embed_dim=c, num_heads=num_heads)
+        self.ln2 = nn.LayerNorm(c)
+        self.fc1 = nn.Linear(c, 4 * c, bias=False)
+        self.fc2 = nn.Linear(4 * c, c, bias=False)
+        self.dropout = nn.Dropout(0.1)
+        self.act = nn.ReLU(True)
+        self.num_heads = num_heads
+
+    def mha(self, q, k, v):
+        """[L, B, c] sequence-first in, [L, B, c] out."""
+        L, B, c = q.shape
+        h = self.num_heads
+        d = c // h
+        W, b = self.ma.in_proj_weight, self.ma.in_proj_bias
+        q = F.linear(q, W[:c], b[:c])
+        k = F.linear(k, W[c:2 * c], b[c:2 * c])
+        v = F.linear(v, W[2 * c:], b[2 * c:])
+        q = q.reshape(L, B * h, d).transpose(0, 1) * (1.0 / math.sqrt(d))
+        k = k.reshape(L, B * h, d).transpose(0, 1)
+        v = v.reshape(L, B * h, d).transpose(0, 1)
+        a = torch.softmax(q @ k.transpose(1, 2), dim=-1)
+        o = (a @ v).transpose(0, 1).reshape(L, B, c)
+        return F.linear(o, self.ma.out_proj.weight, self.ma.out_proj.bias)
+
+    def forward(self, x):
+        x_ = self.ln1(x)
+        x = self.dropout(self.mha(self.q(x_), self.k(x_), self.v(x_))) + x
+        x_ = self.ln2(x)
+        x_ = self.fc2(self.dropout(self.act(self.fc1(x_))))
+        return x + self.dropout(x_)
+
+
+class TransformerBlock(nn.Module):
+    """models/common.py:338-355: tokens = pixels in (H, W) row-major order, sequence-first [HW, B, c];
+    learned position term p + linear(p); output back to [B, c, H, W]."""
+
+    def __init__(self, c1, c2, num_heads, num_layers):
+        super().__init__()
+        self.conv = Conv(c1, c2) if c1 != c2 else None
+        self.linear = nn.Linear(c2, c2)
+        self.tr = nn.Sequential(*(TransformerLayer(c2, num_heads) for _ in range(num_layers)))
+        self.c2 = c2
+
+    def forward(self, x):
+        if self.conv is not None:
+            x = self.conv(x)
+        b, _, h, w = x.shape
+        p = x.flatten(2).permute(2, 0, 1)
+        return self.tr(p + self.linear(p)).permute(1, 2, 0).reshape(b, self.c2, h, w)
+
+
+class C3TR(C3):
+    """models/common.py:184-189: C3 whose bottleneck stack is a TransformerBlock(c_, c_, 4 heads, n)."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        h = int(c2 * e)
+        self.m = TransformerBlock(h, h, 4, n)
+
+
 # ---------------------------------------------------------------- Detect / Model
 
 class Detect(nn.Module):
@@ -427,9 +502,9 @@ def make_divisible(x, d):
     return math.ceil(x / d) * d
 
 
-_CHANNEL_MODS = ('Conv', 'Bottleneck', 'SPPF', 'C3', 'C3STR', 'CoorAttention', 'CA', 'CABottleneck', 'C3CA',
+_CHANNEL_MODS = ('Conv', 'Bottleneck', 'SPPF', 'C3', 'C3TR', 'C3STR', 'CoorAttention', 'CA', 'CABottleneck', 'C3CA',
                  'SPPFCSPC', 'SCConv', 'SPP', 'CBAM')
-_REPEAT_MODS = ('C3', 'C3STR', 'C3CA')
+_REPEAT_MODS = ('C3', 'C3TR', 'C3STR', 'C3CA')
 
 
 def _eval_arg(a, env):
@@ -484,7 +559,7 @@ def parse_model(d, ch):
 class Model(nn.Module):
     """models/yolo.py:117-239 (forward path only; weights come from state_dict transfer)."""
 
-    def __init__(self, cfg, ch=3, nc=None, stride=(8., 16., 32.)):
+    def __init__(self, cfg, ch=3, nc=None, stride=None):
         super().__init__()
         import copy
         self.yaml = copy.deepcopy(cfg)
@@ -492,6 +567,8 @@ class Model(nn.Module):
             self.yaml['nc'] = nc
         self.model, self.save = parse_model(copy.deepcopy(self.yaml), [ch])
         det = self.model[-1]
+        if stride is None:  # P3-P5 heads (8, 16, 32); the config-5 head adds P2 (4)
+            stride = (4., 8., 16., 32.)[-det.nl:]
         det.stride = torch.tensor(stride)
         self.stride = det.stride
 

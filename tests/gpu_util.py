@@ -13,7 +13,7 @@ def product_modules():
         'CoorAttention': P.CoorAttention, 'C3CA': P.C3CA, 'SPPF': P.SPPF, 'SPPFCSPC': P.SPPFCSPC,
         'Upsample': P.Upsample, 'AdConcat2': P.AdConcat2, 'AdConcat3': P.AdConcat3, 'Concat': P.Concat,
         'SwinTransformerLayer': lambda c, h, ws, sh: P.SwinTransformerLayer(c, h, ws, sh), 'C3STR': P.C3STR,
-        'SPP': lambda c1, c2, k: P.SPP(c1, c2, tuple(k)), 'CBAM': P.CBAM,
+        'SPP': lambda c1, c2, k: P.SPP(c1, c2, tuple(k)), 'CBAM': P.CBAM, 'C3TR': P.C3TR,
     }
 
 
@@ -28,6 +28,8 @@ def run_case(name, mods, device, dtype=torch.float32, inputs=None, sd=None):
             m.drop_prob = 0.0
         if type(m).__name__ == 'SwinTransformerLayer':
             m.drop_path = torch.nn.Identity()
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0  # fixtures were captured with the TransformerLayer dropout off
     load_sd(mod, sd if sd is not None else fx.group('sd'))
     mod = mod.to(device)
     xs = inputs if inputs is not None else fx.seq('in')

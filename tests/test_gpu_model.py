@@ -15,10 +15,12 @@ def _model(fx, dtype=torch.float32):
     for mod in m.modules():
         if type(mod).__name__ == 'SwinTransformerLayer':
             mod.drop_path = torch.nn.Identity()
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
     return m.cuda()
 
 
-@pytest.mark.parametrize('name', ['model_v5s', 'model_dma'])
+@pytest.mark.parametrize('name', ['model_v5s', 'model_dma', 'model_c5'])
 def test_model_train_eval_fp32(name):
     fx = Fixture(name)
     m = _model(fx)

@@ -11,7 +11,7 @@ from golden_util import Fixture
 YAMLS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'dma-yolo_amd', 'dmayolo', 'configs')
 
 
-@pytest.mark.parametrize('name', ['model_v5s', 'model_dma'])
+@pytest.mark.parametrize('name', ['model_v5s', 'model_dma', 'model_c5'])
 def test_state_dict_matches_reference(name):
     from dmayolo.models.yolo import Model
     fx = Fixture(name)
@@ -61,3 +61,31 @@ def test_caspd_tdetect_layout_matches_reference():
         assert list(sd[k].shape) == v, k
     assert sum(p.numel() for p in m.parameters()) == fx.meta['nparams']
     assert [float(s) for s in m.stride] == fx.meta['stride']
+
+
+def test_config5_layout_matches_reference():
+    """yolov5l-xs-tr-cbam-spp-bifpn.yaml (C3TR + CBAM + SPP, 4-level Detect with `anchors: 4`): parameter
+    count, state_dict shapes, strides and the placeholder anchors (models/yolo.py:432-436)."""
+    from dmayolo.models.yolo import Model
+    fx = Fixture('model_c5_layout')
+    m = Model(os.path.join(YAMLS, 'yolov5l-xs-tr-cbam-spp-bifpn.yaml'), nc=fx.meta['nc'])
+    sd = m.state_dict()
+    ref = fx.meta['shapes']
+    assert set(sd) == set(ref), set(sd) ^ set(ref)
+    for k, v in ref.items():
+        assert list(sd[k].shape) == v, k
+    assert sum(p.numel() for p in m.parameters()) == fx.meta['nparams'] == 60401284
+    assert [float(s) for s in m.stride] == fx.meta['stride']
+    assert m.model[-1].anchors.tolist() == fx.meta['anchors']
+
+
+def test_config5_in_proj_never_optimized():
+    """train.py:197-214 grouping collects .weight/.bias attributes only: the 12 MHA in_proj params
+    (4,727,808 values) get gradients but never enter the optimizer."""
+    from dmayolo.models.yolo import Model
+    from dmayolo.optim import param_groups
+    m = Model(os.path.join(YAMLS, 'yolov5l-xs-tr-cbam-spp-bifpn.yaml'), nc=3)
+    grouped = {id(p) for g in param_groups(m) for p in g}
+    missing = [(k, p.numel()) for k, p in m.named_parameters() if id(p) not in grouped]
+    assert len(missing) == 12 and all('in_proj' in k for k, _ in missing), missing
+    assert sum(n for _, n in missing) == 4727808

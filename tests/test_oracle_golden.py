@@ -12,12 +12,12 @@ MODS = {
     'CoorAttention': onn.CoorAttention, 'C3CA': onn.C3CA, 'SPPF': onn.SPPF, 'SPPFCSPC': onn.SPPFCSPC,
     'Upsample': torch.nn.Upsample, 'AdConcat2': onn.AdConcat2, 'AdConcat3': onn.AdConcat3, 'Concat': onn.Concat,
     'SwinTransformerLayer': lambda c, h, ws, sh: onn.SwinTransformerLayer(c, h, ws, sh), 'C3STR': onn.C3STR,
-    'SPP': lambda c1, c2, k: onn.SPP(c1, c2, tuple(k)), 'CBAM': onn.CBAM,
+    'SPP': lambda c1, c2, k: onn.SPP(c1, c2, tuple(k)), 'CBAM': onn.CBAM, 'C3TR': onn.C3TR,
 }
 
 MODULE_CASES = [n for n in golden_names('') if n.split('_')[0] in (
     'conv', 'bottleneck', 'c3', 'scconv', 'ca', 'c3ca', 'sppf', 'sppfcspc', 'upsample', 'adconcat2',
-    'adconcat3', 'concat', 'swin', 'c3str', 'spp', 'cbam') and n != 'conv_fuse']
+    'adconcat3', 'concat', 'swin', 'c3str', 'spp', 'cbam', 'c3tr') and n != 'conv_fuse']
 
 
 def run_module_case(name, build=None, device='cpu', dtype=torch.float32):
@@ -26,6 +26,9 @@ def run_module_case(name, build=None, device='cpu', dtype=torch.float32):
     meta = fx.meta
     mod = (build or (lambda m: MODS[m['module']](*m['args'])))(meta)
     onn.bn_defaults(mod)
+    for m in mod.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0  # the fixtures were captured with dropout off (tools/gen_golden.py randomize_bn)
     load_sd(mod, fx.group('sd'))
     mod = mod.to(device)
     ins = [x.to(device, dtype).requires_grad_(True) for x in fx.seq('in')]
@@ -152,7 +155,7 @@ def test_oracle_nms(name):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('name', ['model_v5s', 'model_dma'])
+@pytest.mark.parametrize('name', ['model_v5s', 'model_dma', 'model_c5'])
 def test_oracle_model(name):
     fx = Fixture(name)
     meta = fx.meta
@@ -162,6 +165,8 @@ def test_oracle_model(name):
     for mod in m.modules():
         if isinstance(mod, onn.SwinTransformerLayer):
             mod.drop_prob = 0.0
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
     x = fx.t('in.0').requires_grad_(False)
     m.train()
     outs = m(x)

@@ -65,6 +65,8 @@ def randomize_bn(mod, gen):
                 m.w.copy_(torch.rand(m.w.shape, generator=gen) + 0.5)
         if isinstance(m, C.DropPath):
             m.drop_prob = 0.0  # deterministic: SURVEY §0.6 (DropPath forced off in fixtures)
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0  # TransformerLayer dropout (common.py:328): deterministic fixtures
 
 
 def module_case(name, mod, inputs, meta, seed=0, eval_too=True, list_input=False):
@@ -607,6 +609,64 @@ def gen_tal():
                                              stride=[float(s_) for s_ in model.stride],
                                              shapes={k: list(v.shape) for k, v in sd.items()})))
     print('wrote model_caspd_layout', sum(p.numel() for p in model.parameters()))
+
+
+def gen_c5():
+    """Config-5 (yolov5l-xs-tr-cbam-spp-bifpn.yaml) extras: C3TR (global MHSA, common.py:184-189, 312-355)
+    at a small head dim (4) and at head dim 32, and a whole small-width config-5 model (4-level Detect
+    with the `anchors: 4` placeholder anchors, yolo.py:432-436)."""
+    torch.manual_seed(21)
+    module_case('c3tr_a', C.C3TR(32, 32, 2), [rnd(2, 32, 5, 7, seed=22)], dict(module='C3TR', args=[32, 32, 2]))
+    torch.manual_seed(23)
+    module_case('c3tr_b', C.C3TR(256, 256, 1, False), [rnd(2, 256, 9, 10, seed=24, scale=0.5)],
+                dict(module='C3TR', args=[256, 256, 1, False]))
+    torch.manual_seed(25)
+    yml = small_yaml('/root/reference/models/yolov5l-xs-tr-cbam-spp-bifpn.yaml', 0.125, 0.33)
+    model = Y.Model(deepcopy(yml), nc=3)
+    gen = torch.Generator().manual_seed(26)
+    randomize_bn(model, gen)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            if v.dtype.is_floating_point:
+                v.copy_(v.half().float())
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    x = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(27))
+    model.train()
+    outs = model(x)
+    gups = [torch.randn(o.shape, generator=gen) * 0.1 for o in outs]
+    loss = sum((o * g).sum() for o, g in zip(outs, gups))
+    loss.backward()
+    d = {'meta': json.dumps(dict(yaml=yml, nc=3, img=128)), 'in.0': npy(x)}
+    for k, v in sd0.items():
+        d[f'sd.{k}'] = v.half().numpy() if v.dtype.is_floating_point else npy(v)
+    for i, (o, g) in enumerate(zip(outs, gups)):
+        d[f'out.{i}'] = npy(o)
+        d[f'gup.{i}'] = npy(g)
+    params = dict(model.named_parameters())
+    for k in list(params)[:6] + list(params)[-6:]:
+        d[f'gp.{k}'] = npy(params[k].grad)
+    d['gnorm'] = np.array([float(p.grad.norm()) if p.grad is not None else 0.0 for p in params.values()],
+                          dtype=np.float64)
+    d['pnames'] = np.array(list(params.keys()))
+    model.load_state_dict(sd0)
+    model.eval()
+    with torch.no_grad():
+        z, _ = model(x)
+    d['eout.0'] = npy(z)
+    np.savez_compressed(os.path.join(OUT, 'model_c5.npz'), **d)
+    print('wrote model_c5', sum(v.nbytes for k, v in d.items() if k != 'meta') / 1e6, 'MB',
+          sum(p.numel() for p in model.parameters()), 'params')
+    # full-size parameter layout (nc=3): never-optimized in_proj params, shapes, strides
+    torch.manual_seed(28)
+    full = Y.Model('/root/reference/models/yolov5l-xs-tr-cbam-spp-bifpn.yaml', nc=3)
+    sd = full.state_dict()
+    np.savez_compressed(os.path.join(OUT, 'model_c5_layout.npz'),
+                        meta=json.dumps(dict(yaml='yolov5l-xs-tr-cbam-spp-bifpn.yaml', nc=3,
+                                             nparams=sum(p.numel() for p in full.parameters()),
+                                             stride=[float(s_) for s_ in full.stride],
+                                             anchors=full.model[-1].anchors.tolist(),
+                                             shapes={k: list(v.shape) for k, v in sd.items()})))
+    print('wrote model_c5_layout', sum(p.numel() for p in full.parameters()))
 
 
 if __name__ == '__main__':
