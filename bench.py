@@ -27,6 +27,8 @@ CONFIGS = {
     'v5s-640': ('yolov5s.yaml', 10, 640, 64, 'visdrone'),
     'dma-640': ('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 10, 640, 32, 'visdrone'),
     'dma-1536': ('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 10, 1536, 32, 'visdrone'),
+    'dmaca-1536': ('yolov5l-ca-sppfcspc-bifpn.yaml', 10, 1536, 32, 'visdrone'),  # C3CA sibling
+    'c5-1920': ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 3, 1920, 8, 'visdrone'),  # config 5 (UAVDT nc=3)
 }
 PEAK = {torch.bfloat16: 2500.0, torch.float32: 157.3}  # dense TFLOP/s (MI355X_MICROARCH.md)
 
@@ -54,7 +56,7 @@ def build(cfg, dtype, device):
     yml, nc, img, _, _ = cfg
     torch.manual_seed(0)
     m = Model(os.path.join(CDIR, yml), nc=nc, act_dtype=dtype).to(device)
-    m.hyp = scaled_hyp(HYP_VISDRONE, nc, img)
+    m.hyp = scaled_hyp(HYP_VISDRONE, nc, img, m.model[-1].nl)
     return m
 
 
@@ -88,8 +90,8 @@ def cpu_baseline(cfg, seconds):
     for mod in m.modules():
         if isinstance(mod, onn.SwinTransformerLayer):
             mod.drop_prob = 0.0
-    hyp = scaled_hyp(HYP_VISDRONE, nc, img)
     det = m.model[-1]
+    hyp = scaled_hyp(HYP_VISDRONE, nc, img, det.nl)
     anchors = det.anchors / det.stride.view(-1, 1, 1)
     opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.937, nesterov=True)
     x = images(1, img).float() / 255

@@ -1051,6 +1051,147 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
     if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
   }
 }
+// Narrow-layer weight-grad (out channels <= 64): block tile BM (out channels, 32 or 64) x BN
+// ((kh, kw, ci) columns, 128 or 256), NW = BN / 64 waves side by side, each BM x 64.  Same k-major
+// swizzled LDS images as conv_wgrad_v3 (kmaj_off<BM> / kmaj_off<BN>), filled by LDS-DMA: a 1-KiB
+// piece covers 1024 / rowbytes pixel rows, lane l writes row (l / slots), physical slot (l % slots),
+// i.e. the logical chunk (slot ^ key(row)) & (slots - 1).
+template <int ROW> DEV int kmaj_chunk(int row, int slot) {
+  constexpr int RB = ROW * 2;
+  int key;
+  if constexpr (RB >= 256) key = 2 * ((row & 3) | (((row >> 3) & 1) << 2));
+  else key = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+  return (slot ^ key) & (ROW / 8 - 1);
+}
+
+template <int BM, int BN>
+struct WgradLdsN {
+  static constexpr int NW = BN / 64;
+  static constexpr int RA = BM * 2, RB = BN * 2;
+  static constexpr int SA = RA / 16, SB = RB / 16;
+  static constexpr int PAW = 64 * RA / 1024 / NW, PBW = 64 * RB / 1024 / NW;
+  static constexpr int RPA = 1024 / RA, RPB = 1024 / RB;
+  static constexpr int A_BYTES = 64 * RA, STAGE = 64 * (RA + RB);
+  static_assert(PAW >= 1 && PBW >= 1 && PAW * NW * 1024 == A_BYTES, "tile");
+  const bf16* x; const bf16* dy; Geom g; long NP;
+  long apix[PAW]; int aco[PAW];
+  long bpix[PBW]; int bb[PBW], boh[PBW], bow[PBW], bkh[PBW], bkw[PBW], bci[PBW]; bool bok[PBW];
+  DEV WgradLdsN(const bf16* x_, const bf16* dy_, const Geom& g_, int m0, int n0, int kt0, int wid, int lane)
+      : x(x_), dy(dy_), g(g_) {
+    NP = (long)g.N * g.OH * g.OW;
+    const int Ntot = g.KH * g.KW * g.C;
+#pragma unroll
+    for (int j = 0; j < PAW; ++j) {
+      const int r = (wid * PAW + j) * RPA + lane / SA;
+      apix[j] = (long)kt0 * 64 + r;
+      const int co = m0 + 8 * kmaj_chunk<BM>(r, lane % SA);
+      aco[j] = co < g.K ? co : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < PBW; ++j) {
+      const int r = (wid * PBW + j) * RPB + lane / SB;
+      bpix[j] = (long)kt0 * 64 + r;
+      const long pp = bpix[j] < NP ? bpix[j] : 0;
+      bow[j] = (int)(pp % g.OW);
+      const long t = pp / g.OW;
+      boh[j] = (int)(t % g.OH);
+      bb[j] = (int)(t / g.OH);
+      const int n = n0 + 8 * kmaj_chunk<BN>(r, lane % SB);
+      bok[j] = n < Ntot;
+      bci[j] = n % g.C;
+      const int u = n / g.C;
+      bkw[j] = u % g.KW;
+      bkh[j] = u / g.KW;
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+    const bf16* zero = reinterpret_cast<const bf16*>(g_zero_page);
+#pragma unroll
+    for (int j = 0; j < PAW; ++j) {
+      const bf16* sa = (apix[j] < NP && aco[j] >= 0) ? dy + apix[j] * g.yps + aco[j] : zero;
+      glds16(sa, stage + (wid * PAW + j) * 1024);
+      apix[j] += 64;
+    }
+#pragma unroll
+    for (int j = 0; j < PBW; ++j) {
+      const int ih = boh[j] * g.S - g.P + bkh[j], iw = bow[j] * g.S - g.P + bkw[j];
+      const bool ok = bpix[j] < NP && bok[j] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const bf16* sb = ok ? x + (((long)bb[j] * g.H + ih) * g.W + iw) * g.xps + bci[j] : zero;
+      glds16(sb, stage + A_BYTES + (wid * PBW + j) * 1024);
+      bpix[j] += 64;
+      bow[j] += 64;
+      while (bow[j] >= g.OW) {
+        bow[j] -= g.OW;
+        if (++boh[j] == g.OH) { boh[j] = 0; ++bb[j]; }
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int NS>
+__global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                    float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn) {
+  using LD = WgradLdsN<BM, BN>;
+  constexpr int STAGE = LD::STAGE, TM = BM / 16, PER = LD::PAW + LD::PBW;
+  constexpr int LDSB = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int nk_all = (int)((NP + 63) / 64);
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
+  f32x4 acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    LD ld(x, dy, g, m0, n0, kt0, wid, lane);
+    ld.issue(smem, wid);
+    if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+#pragma unroll
+      for (int ks = 0; ks < 64; ks += 32) {
+        bf16x8 a[TM], b[4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = frag_k<BM>(As, i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag_k<BN>(Bs, wid * 64 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int RS = BN + 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(i * 16 + 4 * (lane >> 4) + r) * RS + wid * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int Ntot = g.KH * g.KW * g.C;
+  for (int e = threadIdx.x; e < BM * BN; e += BN) {
+    const int row = e / BN, c = e % BN;
+    const int m = m0 + row, n = n0 + c;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+  }
+}
 }  // namespace v3
 
 // ---------------------------------------------------------------- host dispatch
@@ -1228,13 +1369,64 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   return (int)hipGetLastError();
 }
 
+// narrow layers (K <= 64): BM = 32 / 64 out-channel tiles, BN = 128 / 256 column tiles
+template <int BM, int BN>
+int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int Ntot = g.KH * g.KW * g.C;
+  const int gm = ceil_div(g.K, BM), gn = ceil_div(Ntot, BN);
+  const int nk = ceil_div(NP, 64);
+  const int tiles = gm * gn;
+  int maxs = nk / 8;
+  if (maxs < 1) maxs = 1;
+  int splits = 1;
+  if (wgrad_target() > 0) {
+    splits = (wgrad_target() + tiles / 2) / tiles;
+    if (splits < 1) splits = 1;
+  } else {
+    // same cost model as launch_wgrad_v3 with the tile's share of a 128 x 128 step and atomics
+    const double R = 2.0 * num_cus() * (128.0 * 128.0) / (BM * BN) * 0.5;
+    const double step = 1.9 * (BM * BN) / (128.0 * 128.0) + 0.25;
+    double best = 1e300;
+    for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
+      const double blocks = (double)tiles * sp;
+      const double t = ceil(blocks / R) * ceil_div(nk, sp) * step + blocks * 0.0504 * (BM * BN) / (128.0 * 128.0);
+      if (t < best) { best = t; splits = sp; }
+    }
+  }
+  if (splits > maxs) splits = maxs;
+  const int per = ceil_div(nk, splits);
+  splits = ceil_div(nk, per);
+  const dim3 grid((unsigned)tiles, splits);
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  constexpr int NS = 3 * v3::WgradLdsN<BM, BN>::STAGE <= 80 * 1024 ? 3 : 2;  // keep 2 blocks per CU
+  v3::conv_wgrad_v3n<BM, BN, NS><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  return (int)hipGetLastError();
+}
+
+inline int wgrad_narrow_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_WGRAD_NARROW");
+    return e ? atoi(e) : 1;
+  }();
+  return t;
+}
+
 template <typename T>
 int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     const long NP = (long)g.N * g.OH * g.OW;
-    if (g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy) &&
-        g.K > 64 && g.KH * g.KW * g.C > 64 && NP >= 16384)
+    const int Ntot = g.KH * g.KW * g.C;
+    const bool vec = g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy);
+    if (vec && g.K > 64 && Ntot > 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
+    if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && wgrad_narrow_mode()) {
+      const bool wide = Ntot >= 512 || Ntot % 256 == 0;
+      if (g.K <= 32) return wide ? launch_wgrad_v3n<32, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                                 : launch_wgrad_v3n<32, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
+      return wide ? launch_wgrad_v3n<64, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                  : launch_wgrad_v3n<64, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
+    }
   }
   if (g.K > 64 && g.KH * g.KW * g.C > 64) return launch_wgrad<T, 128, 128>((const T*)x, (const T*)dy, dw, g, st);
   return launch_wgrad<T, 64, 64>((const T*)x, (const T*)dy, dw, g, st);

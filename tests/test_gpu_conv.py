@@ -11,7 +11,10 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 128, 3, 1),
           (16, 128, 40, 40, 256, 1, 1), (16, 64, 64, 64, 128, 3, 2), (12, 96, 37, 45, 136, 3, 1),
           (9, 256, 48, 50, 384, 1, 1), (8, 8, 192, 192, 64, 6, 2), (8, 8, 192, 192, 128, 6, 2),
-          (4, 40, 96, 70, 200, 3, 1)]
+          (4, 40, 96, 70, 200, 3, 1),
+          # narrow layers (K <= 64) on the LDS-DMA weight-grad tiles (BM 32/64 x BN 128/256), ragged K / columns
+          (16, 32, 64, 64, 32, 3, 1), (4, 64, 80, 80, 64, 3, 1), (16, 256, 40, 40, 64, 1, 1),
+          (8, 8, 192, 192, 32, 6, 2), (8, 136, 60, 50, 40, 1, 1), (8, 32, 96, 96, 64, 3, 2)]
 
 
 def _rel(a, b):
