@@ -1406,8 +1406,10 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hi
 
 inline int wgrad_narrow_mode() {
   static int t = [] {
+    // off by default: measured slower than the register-staged v2 64x64 tiles on the yolov5s narrow
+    // layers (tools/gpu/tune_narrow.sh); kept selectable (and parity-tested) for tuning
     const char* e = getenv("DMY_WGRAD_NARROW");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return t;
 }

@@ -167,6 +167,153 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- max-pool, LDS-tiled (16-B channel vectors)
+// One workgroup = a TH x TW tile of outputs x one 16-B channel vector of one image.  The input tile
+// with its (K-1) halo is staged in LDS once; the window max is separable: a row pass (max over dw
+// per (input row, output col), first-valid start, ATen update rule) then a column pass over dh
+// (start = first valid row's row winner) gives exactly the row-major scan's winner (NaN: the last
+// one, as in ATen).  Backward: the window arguments and dy of every output that can route into the
+// tile are staged in LDS and each input pixel gathers its contributions (deterministic, no atomics).
+constexpr int MP_TH = 16, MP_TW = 32;
+
+template <typename T, int K>
+__global__ void __launch_bounds__(256) maxpool_fwd_lds(const T* __restrict__ x, long xps, T* __restrict__ y, long yps,
+                                                       uint8_t* __restrict__ arg, int H, int W, int C) {
+  constexpr int NV = Traits<T>::VW, P = K / 2, IH = MP_TH + K - 1, IW = MP_TW + K - 1;
+  __shared__ uint4 xin[IH * IW];
+  __shared__ uint4 rm[IH * MP_TW];
+  __shared__ uint2 ra[IH * MP_TW];
+  const int CV = C / NV;
+  const int b = blockIdx.z / CV, c = (blockIdx.z % CV) * NV;
+  const int h0 = blockIdx.y * MP_TH, w0 = blockIdx.x * MP_TW;
+  const T* xb = x + (long)b * H * W * xps + c;
+  for (int e = threadIdx.x; e < IH * IW; e += 256) {
+    const int hh = h0 - P + e / IW, ww = w0 - P + e % IW;
+    xin[e] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                 ? *reinterpret_cast<const uint4*>(xb + ((long)hh * W + ww) * xps) : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  // row pass: rm[r][w] = max over dw of input (row r, col w + dw)
+  const int wlo = w0 - P;  // image col of tile col 0 of xin
+  for (int e = threadIdx.x; e < IH * MP_TW; e += 256) {
+    const int r = e / MP_TW, w = e % MP_TW;
+    const int c0 = wlo + w;  // image col of tap dw = 0
+    const int first = c0 < 0 ? -c0 : 0;
+    float best[NV];
+    uint8_t bi[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) { best[j] = -INFINITY; bi[j] = (uint8_t)first; }
+#pragma unroll
+    for (int dw = 0; dw < K; ++dw) {
+      const bool ok = (unsigned)(c0 + dw) < (unsigned)W;
+      float v[NV];
+      unpack<T>(xin[r * IW + w + dw], v);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float vv = ok ? v[j] : -INFINITY;
+        const unsigned up = (unsigned)(vv > best[j]) | (unsigned)__builtin_isnan(vv);
+        best[j] = up ? vv : best[j];
+        bi[j] = up ? (uint8_t)dw : bi[j];
+      }
+    }
+    rm[e] = pack<T>(best);
+    ra[e] = *reinterpret_cast<const uint2*>(bi);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < MP_TH * MP_TW; e += 256) {
+    const int h = e / MP_TW, w = e % MP_TW;
+    const int oh = h0 + h, ow = w0 + w;
+    if (oh >= H || ow >= W) continue;
+    const int r0 = oh - P;  // image row of tap dh = 0 (= tile row h of xin / rm)
+    const int first = r0 < 0 ? -r0 : 0;
+    float best[NV];
+    int bi[NV];
+    {
+      const uint8_t* fa = reinterpret_cast<const uint8_t*>(&ra[(h + first) * MP_TW + w]);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) { best[j] = -INFINITY; bi[j] = first * K + fa[j]; }
+    }
+#pragma unroll
+    for (int dh = 0; dh < K; ++dh) {
+      const bool ok = (unsigned)(r0 + dh) < (unsigned)H;
+      float v[NV];
+      unpack<T>(rm[(h + dh) * MP_TW + w], v);
+      const uint2 a2 = ra[(h + dh) * MP_TW + w];
+      const uint8_t* a = reinterpret_cast<const uint8_t*>(&a2);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const float vv = ok ? v[j] : -INFINITY;
+        const unsigned up = (unsigned)(vv > best[j]) | (unsigned)__builtin_isnan(vv);
+        best[j] = up ? vv : best[j];
+        bi[j] = up ? dh * K + a[j] : bi[j];
+      }
+    }
+    const long pix = ((long)b * H + oh) * W + ow;
+    *reinterpret_cast<uint4*>(y + pix * yps + c) = pack<T>(best);
+    uint8_t ab[8];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) ab[j] = (uint8_t)bi[j];
+    if constexpr (NV == 8) *reinterpret_cast<uint2*>(arg + pix * C + c) = *reinterpret_cast<const uint2*>(ab);
+    else *reinterpret_cast<uint32_t*>(arg + pix * C + c) = *reinterpret_cast<const uint32_t*>(ab);
+  }
+}
+
+template <typename T, int K>
+__global__ void __launch_bounds__(256) maxpool_bwd_lds(const T* __restrict__ dy, long dps, const uint8_t* __restrict__ arg,
+                                                       T* __restrict__ dx, long dxps, int accumulate, int H, int W, int C) {
+  constexpr int NV = Traits<T>::VW, P = K / 2, IH = MP_TH + K - 1, IW = MP_TW + K - 1;
+  using AW = typename std::conditional<NV == 8, uint2, uint32_t>::type;
+  __shared__ uint4 gs[IH * IW];
+  __shared__ AW as_[IH * IW];
+  const int CV = C / NV;
+  const int b = blockIdx.z / CV, c = (blockIdx.z % CV) * NV;
+  const int h0 = blockIdx.y * MP_TH, w0 = blockIdx.x * MP_TW;
+  // outputs q in [h0 - P, h0 + TH - 1 + P] x [w0 - P, w0 + TW - 1 + P]; out-of-image ones never route
+  for (int e = threadIdx.x; e < IH * IW; e += 256) {
+    const int qh = h0 - P + e / IW, qw = w0 - P + e % IW;
+    const bool ok = (unsigned)qh < (unsigned)H && (unsigned)qw < (unsigned)W;
+    const long q = ((long)b * H + qh) * W + qw;
+    gs[e] = ok ? *reinterpret_cast<const uint4*>(dy + q * dps + c) : make_uint4(0, 0, 0, 0);
+    as_[e] = ok ? *reinterpret_cast<const AW*>(arg + q * C + c) : AW{0xFFFFFFFFu};
+    if constexpr (NV == 8) { if (!ok) as_[e] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu); }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < MP_TH * MP_TW; e += 256) {
+    const int h = e / MP_TW, w = e % MP_TW;
+    const int ih = h0 + h, iw = w0 + w;
+    if (ih >= H || iw >= W) continue;
+    float s[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] = 0.f;
+    // output q = (ih + P - dh, iw + P - dw) routes to p iff its window offset == dh * K + dw
+#pragma unroll
+    for (int dh = 0; dh < K; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < K; ++dw) {
+        const int slot = (h + K - 1 - dh) * IW + (w + K - 1 - dw);
+        const AW a2 = as_[slot];
+        const uint8_t* a = reinterpret_cast<const uint8_t*>(&a2);
+        const uint8_t want = (uint8_t)(dh * K + dw);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) any |= a[j] == want;
+        if (!any) continue;
+        float d[NV];
+        unpack<T>(gs[slot], d);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) s[j] += a[j] == want ? d[j] : 0.f;
+      }
+    T* o = dx + (((long)b * H + ih) * W + iw) * dxps + c;
+    if (accumulate) {
+      float d[NV];
+      unpack<T>(*reinterpret_cast<const uint4*>(o), d);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) s[j] += d[j];
+    }
+    *reinterpret_cast<uint4*>(o) = pack<T>(s);
+  }
+}
+
 // ---------------------------------------------------------------- avg-pool r x r, stride r, floor mode
 template <typename T, int NV>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, int N, int H, int W, int C,
@@ -315,52 +462,109 @@ __global__ void s2d_kernel(const T* __restrict__ x, long xps, T* __restrict__ y,
 // channel attention: [avg; max] global pools -> shared MLP (conv kernels) -> sigmoid(sum of halves);
 // spatial attention: out1 = x * ca, s2 = [mean_c out1, max_c out1] -> 7x7 conv + sigmoid (conv kernels)
 // -> out = out1 * sa.  Max-pool gradients go to the first maximum (torch's index semantics).
-template <typename T>
-__global__ void gpool_fwd_kernel(const T* __restrict__ x, long xps, int N, int HW, int C, T* __restrict__ out,
-                                 int* __restrict__ arg) {
-  const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), part = threadIdx.x >> 6;
-  __shared__ float ss[4][64], sm[4][64];
-  __shared__ int sa[4][64];
-  float s = 0.f, mx = -INFINITY;
-  int am = 0x7fffffff;
+// Stage 1: grid (S pixel chunks, N, channel groups).  A workgroup is L lanes across NV-wide channel
+// vectors x (256 / L) pixel parts; each lane scans its pixels in increasing order (first max wins),
+// the parts merge in LDS (equal max -> smaller pixel), and the chunk's (sum, max, argmax) partials go
+// to the fp32/int workspace [3][S][N][C].  Stage 2 folds the S chunks in order, so the result is
+// deterministic and the argmax is the first maximum in pixel order (AdaptiveMaxPool2d's rule).
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) gpool_part_kernel(const T* __restrict__ x, long xps, int N, int HW, int C, int L,
+                                                         int chunk, float* __restrict__ ws) {
+  const int S = gridDim.x, s = blockIdx.x, n = blockIdx.y;
+  const int lane = threadIdx.x % L, part = threadIdx.x / L, parts = 256 / L;
+  const int c = (blockIdx.z * L + lane) * NV;
+  __shared__ float ss[256 * NV], sm[256 * NV];
+  __shared__ int sa[256 * NV];
+  float sum[NV], mx[NV];
+  int am[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) { sum[j] = 0.f; mx[j] = -INFINITY; am[j] = 0x7fffffff; }
+  const int p0 = s * chunk, p1 = min(HW, p0 + chunk);
   if (c < C) {
-    for (int p = part; p < HW; p += 4) {
-      const float v = to_f(x[((long)n * HW + p) * xps + c]);
-      s += v;
-      if (v > mx) { mx = v; am = p; }
+    const T* xb = x + (long)n * HW * xps + c;
+    for (int p = p0 + part; p < p1; p += parts) {
+      float v[NV];
+      ldv<T, NV>(xb + (long)p * xps, v);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        sum[j] += v[j];
+        const bool up = v[j] > mx[j];
+        mx[j] = up ? v[j] : mx[j];
+        am[j] = up ? p : am[j];
+      }
     }
   }
-  ss[part][threadIdx.x & 63] = s;
-  sm[part][threadIdx.x & 63] = mx;
-  sa[part][threadIdx.x & 63] = am;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    ss[threadIdx.x * NV + j] = sum[j];
+    sm[threadIdx.x * NV + j] = mx[j];
+    sa[threadIdx.x * NV + j] = am[j];
+  }
   __syncthreads();
   if (part == 0 && c < C) {
-    const int l = threadIdx.x;
-    float t = 0.f, m = -INFINITY;
-    int a = 0x7fffffff;
-    for (int q = 0; q < 4; ++q) {
-      t += ss[q][l];
-      if (sm[q][l] > m || (sm[q][l] == m && sa[q][l] < a)) { m = sm[q][l]; a = sa[q][l]; }
+    const long plane = (long)S * N * C;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float t = 0.f, m = -INFINITY;
+      int a = 0x7fffffff;
+      for (int q = 0; q < parts; ++q) {
+        const int e = (q * L + lane) * NV + j;
+        t += ss[e];
+        if (sm[e] > m || (sm[e] == m && sa[e] < a)) { m = sm[e]; a = sa[e]; }
+      }
+      const long o = ((long)s * N + n) * C + c + j;
+      ws[o] = t;
+      ws[plane + o] = m;
+      reinterpret_cast<int*>(ws)[2 * plane + o] = a;
     }
-    out[(long)n * C + c] = from_f<T>(t / HW);
-    out[(long)(N + n) * C + c] = from_f<T>(m);
-    arg[(long)n * C + c] = a;
   }
 }
 
 template <typename T>
+__global__ void gpool_final_kernel(const float* __restrict__ ws, int S, int N, int HW, int C, T* __restrict__ out,
+                                   int* __restrict__ arg) {
+  const long NC = (long)N * C, plane = (long)S * NC;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < NC; i += (long)gridDim.x * blockDim.x) {
+    float t = 0.f, m = -INFINITY;
+    int a = 0x7fffffff;
+    for (int s = 0; s < S; ++s) {
+      const long o = s * NC + i;
+      t += ws[o];
+      const float mm = ws[plane + o];
+      const int aa = reinterpret_cast<const int*>(ws)[2 * plane + o];
+      if (mm > m || (mm == m && aa < a)) { m = mm; a = aa; }
+    }
+    if (a == 0x7fffffff) a = 0;  // all -inf: the first pixel (ATen starts from index 0)
+    const int n = (int)(i / C), c = (int)(i % C);
+    out[(long)n * C + c] = from_f<T>(t / HW);
+    out[(long)(N + n) * C + c] = from_f<T>(m);
+    arg[i] = a;
+  }
+}
+
+template <typename T, int NV>
 __global__ void gpool_bwd_kernel(const T* __restrict__ dz, const int* __restrict__ arg, T* __restrict__ dx, long dxps,
                                  int accumulate, int N, int HW, int C) {
-  const long total = (long)N * HW * C;
+  const int CV = C / NV;
+  const long total = (long)N * HW * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long t = i / C;
+    const int c = (int)(i % CV) * NV;
+    const long t = i / CV;
     const int p = (int)(t % HW), n = (int)(t / HW);
-    float v = to_f(dz[(long)n * C + c]) / HW;
-    if (arg[(long)n * C + c] == p) v += to_f(dz[(long)(N + n) * C + c]);
+    float v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      v[j] = to_f(dz[(long)n * C + c + j]) / HW;
+      if (arg[(long)n * C + c + j] == p) v[j] += to_f(dz[(long)(N + n) * C + c + j]);
+    }
     T* o = dx + ((long)n * HW + p) * dxps + c;
-    if (accumulate) v += to_f(*o);
-    *o = from_f<T>(v);
+    if (accumulate) {
+      float d[NV];
+      ldv<T, NV>(o, d);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += d[j];
+    }
+    stv<T, NV>(o, v);
   }
 }
 
@@ -867,6 +1071,21 @@ DMY_API int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yp
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
   if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;  // uint8 window offsets
+  if (v && N * (C / (dtype ? 8 : 4)) < 65536 && k >= 3 && k <= 13) {
+    const dim3 gl(ceil_div(W, MP_TW), ceil_div(H, MP_TH), N * (C / (dtype ? 8 : 4)));
+#define MP_LDS(KS) if (dtype) maxpool_fwd_lds<bf16, KS><<<gl, 256, 0, st>>>((const bf16*)x, xps, (bf16*)y, yps, arg, H, W, C); \
+                   else maxpool_fwd_lds<float, KS><<<gl, 256, 0, st>>>((const float*)x, xps, (float*)y, yps, arg, H, W, C)
+    switch (k) {
+      case 3: MP_LDS(3); break;
+      case 5: MP_LDS(5); break;
+      case 7: MP_LDS(7); break;
+      case 9: MP_LDS(9); break;
+      case 11: MP_LDS(11); break;
+      default: MP_LDS(13); break;
+    }
+#undef MP_LDS
+    return (int)hipGetLastError();
+  }
   const int g = egrid((long)N * H * W * C / (v ? (dtype ? 8 : 4) : 1));
 #define MP_FWD(KS) DISPATCH_TV(dtype, v, maxpool_fwd_kernel<T, NV, KS><<<g, 256, 0, st>>>((const T*)x, xps, (T*)y, yps, arg, N, H, W, C, k))
   switch ((long)H * W * xps < (1L << 31) ? k : 0) {  // compile-time windows use 32-bit in-image offsets
@@ -886,6 +1105,21 @@ DMY_API int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned 
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
   if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;
+  if (v && N * (C / (dtype ? 8 : 4)) < 65536 && k >= 3 && k <= 13) {
+    const dim3 gl(ceil_div(W, MP_TW), ceil_div(H, MP_TH), N * (C / (dtype ? 8 : 4)));
+#define MP_LDS(KS) if (dtype) maxpool_bwd_lds<bf16, KS><<<gl, 256, 0, st>>>((const bf16*)dy, dps, arg, (bf16*)dx, dxps, accumulate, H, W, C); \
+                   else maxpool_bwd_lds<float, KS><<<gl, 256, 0, st>>>((const float*)dy, dps, arg, (float*)dx, dxps, accumulate, H, W, C)
+    switch (k) {
+      case 3: MP_LDS(3); break;
+      case 5: MP_LDS(5); break;
+      case 7: MP_LDS(7); break;
+      case 9: MP_LDS(9); break;
+      case 11: MP_LDS(11); break;
+      default: MP_LDS(13); break;
+    }
+#undef MP_LDS
+    return (int)hipGetLastError();
+  }
   DISPATCH_TV(dtype, v, maxpool_bwd_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)dy, dps, arg, (T*)dx, dxps, accumulate, N, H, W, C, k));
   return (int)hipGetLastError();
 }
@@ -925,16 +1159,46 @@ DMY_API int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long
   DISPATCH_TV(dtype, v, s2d_kernel<T, NV><<<egrid((long)N * H * W * C / NV), 256, 0, st>>>((const T*)x, xps, (T*)y, yps, N, H, W, C, backward));
   return (int)hipGetLastError();
 }
-DMY_API int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, void* stream) {
+namespace {
+// pixel chunks of the global pool: about 2048 workgroups over (chunks x N x channel groups), >= 64
+// pixels per chunk
+struct GPoolPlan {
+  int L, groups, S, chunk;
+  GPoolPlan(int N, int HW, int C, int NV) {
+    const int CV = ceil_div(C, NV);
+    L = 1;
+    while (L < CV && L < 256) L <<= 1;
+    groups = ceil_div(CV, L);
+    const long per = (long)N * groups;
+    const long by_work = ceil_div((long)HW, 64L), by_grid = 2048L / (per > 0 ? per : 1L);
+    S = (int)(by_work < by_grid ? by_work : by_grid);
+    if (S < 1) S = 1;
+    chunk = ceil_div(HW, S);
+    S = ceil_div(HW, chunk);
+  }
+};
+}  // namespace
+
+DMY_API long dmy_gpool_ws_bytes(int dtype, int N, int HW, int C) {
+  const GPoolPlan pl(N, HW, C, dtype ? 8 : 4);  // the vector plan has at least as many chunks as the scalar one
+  const GPoolPlan ps(N, HW, C, 1);
+  return 3L * (pl.S > ps.S ? pl.S : ps.S) * N * C * 4;
+}
+DMY_API int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, float* ws,
+                          void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(N, ceil_div(C, 64));
-  DISPATCH_T(dtype, gpool_fwd_kernel<T><<<grid, 256, 0, st>>>((const T*)x, xps, N, HW, C, (T*)out, arg));
+  const bool v = vec_ok(dtype, {C, xps}, {x});
+  const GPoolPlan pl(N, HW, C, (int)vw_of(dtype, v));
+  const dim3 grid(pl.S, N, pl.groups);
+  DISPATCH_TV(dtype, v, gpool_part_kernel<T, NV><<<grid, 256, 0, st>>>((const T*)x, xps, N, HW, C, pl.L, pl.chunk, ws));
+  DISPATCH_T(dtype, gpool_final_kernel<T><<<egrid((long)N * C), 256, 0, st>>>(ws, pl.S, N, HW, C, (T*)out, arg));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_gpool_bwd(int dtype, const void* dz, const int* arg, void* dx, long dxps, int accumulate, int N, int HW,
                           int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, gpool_bwd_kernel<T><<<egrid((long)N * HW * C), 256, 0, st>>>((const T*)dz, arg, (T*)dx, dxps, accumulate, N, HW, C));
+  const bool v = vec_ok(dtype, {C, dxps}, {dx});
+  DISPATCH_TV(dtype, v, gpool_bwd_kernel<T, NV><<<egrid((long)N * HW * C / NV), 256, 0, st>>>((const T*)dz, arg, (T*)dx, dxps, accumulate, N, HW, C));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_halves_sigmoid(int dtype, const void* z, int N, int C, void* ca, const void* dca, void* dz, void* stream) {

@@ -70,7 +70,8 @@ SIGNATURES = {
     'dmy_tal_flatten': [I, P, L, I, I, I, I, I, I, P, I, P],
     'dmy_tal_detect_out': [I, P, I, I, I, P, P, P, P, P],
     'dmy_space_to_depth': [I, P, L, P, L, I, I, I, I, I, P],
-    'dmy_gpool_fwd': [I, P, L, I, I, I, P, P, P],
+    'dmy_gpool_ws_bytes': [I, I, I, I],
+    'dmy_gpool_fwd': [I, P, L, I, I, I, P, P, P, P],
     'dmy_gpool_bwd': [I, P, P, P, L, I, I, I, I, P],
     'dmy_halves_sigmoid': [I, P, I, I, P, P, P, P],
     'dmy_cbam_in_fwd': [I, P, L, P, I, I, I, P, P, P, P],
@@ -108,7 +109,7 @@ def _load():
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError = stale build: fail loudly
         fn.argtypes = argt
-        fn.restype = ctypes.c_int
+        fn.restype = ctypes.c_long if name.endswith('_bytes') else ctypes.c_int
     return lib
 
 

@@ -810,7 +810,8 @@ class GPoolFn(torch.autograd.Function):
         N, C, H, W = x.shape
         z = new_act(2 * N, C, 1, 1, x)
         arg = torch.empty((N, C), dtype=torch.int32, device=x.device)
-        call('dmy_gpool_fwd', dcode(x), ptr(x), xps, N, H * W, C, ptr(z), ptr(arg), stream())
+        ws = torch.empty(call('dmy_gpool_ws_bytes', dcode(x), N, H * W, C) // 4, dtype=torch.float32, device=x.device)
+        call('dmy_gpool_fwd', dcode(x), ptr(x), xps, N, H * W, C, ptr(z), ptr(arg), ptr(ws), stream())
         ctx.save_for_backward(arg)
         ctx.shape, ctx.sink = (N, C, H, W), sink
         return z

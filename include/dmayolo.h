@@ -174,7 +174,11 @@ int dmy_space_to_depth(int dtype, const void* x, long xps, void* y, long yps, in
 
 /* ---- config-5 modules: CBAM (models/common.py:260-310) channel / spatial attention pieces; SPP
  *      (common.py:212-227) reuses dmy_maxpool_* with k = 3..13. */
-int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, void* stream);
+/* global avg + max pool (CBAM ChannelAttentionModule avg_pool / max_pool, common.py:266-267):
+ * out [2N][C] = (means; maxima), arg [N][C] = first argmax pixel.  ws: dmy_gpool_ws_bytes() of fp32 scratch. */
+long dmy_gpool_ws_bytes(int dtype, int N, int HW, int C);
+int dmy_gpool_fwd(int dtype, const void* x, long xps, int N, int HW, int C, void* out, int* arg, float* ws,
+                  void* stream);
 int dmy_gpool_bwd(int dtype, const void* dz, const int* arg, void* dx, long dxps, int accumulate, int N, int HW, int C,
                   void* stream);
 int dmy_halves_sigmoid(int dtype, const void* z, int N, int C, void* ca, const void* dca, void* dz, void* stream);
