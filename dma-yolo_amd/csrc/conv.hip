@@ -798,7 +798,118 @@ struct FwdLds {
   }
 };
 
+// Buffer-descriptor form of FwdLds for gathered tensors whose channel count is a multiple of BK
+// (every K step then lies inside one tap, so the tap (kh, kw) and the channel base ci0 are uniform).
+// Sources are 32-bit byte offsets against buffer descriptors: an out-of-image tap, a row past M or a
+// column past K gets an offset beyond the descriptor's record count and the hardware's range check
+// returns zeros (no zero page, no 64-bit address arithmetic).  Per K step a lane spends one add, two
+// compares and a select per A piece and one add per B piece; the pixel bases are built once.
+constexpr unsigned kBufOob = 0xFFFFFFF0u;  // >= every record count used (checked on the host)
+
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+DEV void blds16(__amdgpu_buffer_rsrc_t r, unsigned off, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0, 0, 0);
+}
+
+template <int BM, int BN, int NS, bool P1, bool DG>
+struct FwdLdsB {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __amdgpu_buffer_rsrc_t rx, rw;
+  int H, W, C, KW, xps;
+  int kh, kw, ci0, kpos;            // uniform cursor of the next K step
+  int kl;                           // this lane's (swizzled) 16-B chunk within the step, in elements
+  int pix[C3_::APW], ih0[C3_::APW], iw0[C3_::APW];
+  bool aval[C3_::APW];
+  unsigned boff[C3_::BPW];
+  DEV FwdLdsB(const bf16* x, const bf16* w, const Geom& g, long M, long m0, int n0, int wid, int lane, unsigned xbytes,
+              unsigned wbytes)
+      : H(g.H), W(g.W), C(g.C), KW(g.KW), xps((int)g.xps), kh(0), kw(0), ci0(0), kpos(0) {
+    rx = make_rsrc(x, xbytes);
+    rw = make_rsrc(w, wbytes);
+    const int Ktot = g.KH * g.KW * g.C;
+    kl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      const long m = m0 + (wid * C3_::APW + j) * 8 + (lane >> 3);
+      aval[j] = m < M;
+      const int mm = (int)(aval[j] ? m : 0);
+      const int ow = mm % g.OW, t = mm / g.OW, oh = t % g.OH, b = t / g.OH;
+      if (P1) { pix[j] = mm * xps; ih0[j] = 0; iw0[j] = 0; }
+      else {
+        ih0[j] = DG ? oh + g.P : oh * g.S - g.P;
+        iw0[j] = DG ? ow + g.P : ow * g.S - g.P;
+        pix[j] = ((b * g.H + ih0[j]) * g.W + iw0[j]) * xps;  // may be negative; valid taps land >= 0
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j) {
+      const int n = n0 + (wid * C3_::BPW + j) * 8 + (lane >> 3);
+      boff[j] = n < g.K ? (unsigned)(n * Ktot + kl) * 2u : kBufOob;
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+    const int dh = DG ? -kh : kh, dw = DG ? -kw : kw;
+    const int delta = P1 ? kpos + kl : (dh * W + dw) * xps + ci0 + kl;
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      bool ok = aval[j];
+      if (!P1) ok = ok && (unsigned)(ih0[j] + dh) < (unsigned)H && (unsigned)(iw0[j] + dw) < (unsigned)W;
+      blds16(rx, ok ? (unsigned)(pix[j] + delta) * 2u : kBufOob, stage + (wid * C3_::APW + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j)
+      blds16(rw, boff[j] == kBufOob ? kBufOob : boff[j] + (unsigned)kpos * 2u,
+             stage + C3_::A_BYTES + (wid * C3_::BPW + j) * 1024);
+    kpos += BK;
+    if (!P1) {
+      ci0 += BK;
+      if (ci0 == C) {
+        ci0 = 0;
+        if (++kw == KW) { kw = 0; ++kh; }
+      }
+    }
+  }
+};
+
 template <int N> DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// Main loop with the whole K step's fragments read up front (64 VGPRs), the next stage's LDS-DMA
+// issued while those reads are in flight, then the step's 32 MFMAs back to back.
+template <int BM, int BN, int NS, bool IF, class LD>
+DEV void mainloop4(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int lane) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  constexpr int PER = C3_::APW + C3_::BPW;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  ld.issue(smem, wid);
+  if (NS == 3 && nk > 1) ld.issue(smem + C3_::STAGE, wid);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (IF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
+    const bf16* Bs = As + BM * BK;
+    bf16x8 a[2][4], b[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[h][i] = frag_sw(As, wm * 64 + i * 16, h * 32, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[h][j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!IF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+  }
+}
 
 template <int BM, int BN, int NS, class LD>
 DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int lane) {
@@ -831,11 +942,12 @@ DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
 
 // Forward (DG = false) or stride-1 data-grad (DG = true; `g` is the GEMM view built by the host:
 // rows = input pixels, columns = input channels, gather = dy) with the BN-partial / accumulate epilogue.
-template <int BM, int BN, int NS, bool P1, bool DG>
+template <int BM, int BN, int NS, bool P1, bool DG, int BUF>
 __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
                                                             float* __restrict__ psum, float* __restrict__ psq,
-                                                            int accumulate, Geom g, int gm, int gn) {
+                                                            int accumulate, Geom g, int gm, int gn, unsigned xbytes,
+                                                            unsigned wbytes) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -844,14 +956,19 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   const long M = (long)g.N * g.OH * g.OW;
   const long m0 = (long)tm * BM;
   const int n0 = tn * BN;
-  FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
-  mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  if constexpr (BUF > 0) {
+    FwdLdsB<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+    mainloop4<BM, BN, NS, BUF == 2>(ld, nk, smem, acc, wid, lane);
+  } else {
+    FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
+    mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  }
   __syncthreads();
   // epilogue: (+bias) -> bf16 tile in LDS [BM][BN+8] + BN partials.  Partial rows follow the v2
   // numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
@@ -987,9 +1104,92 @@ struct WgradLds {
   }
 };
 
-template <int NS>
+// Buffer-descriptor form of WgradLds: every address is a 32-bit element offset advanced by adds only
+// (the per-pixel 64-bit products of WgradLds cost 32 quarter-rate v_mul_lo_u32 per K step).  Per
+// piece the lane tracks its pixel (pix, oh, ow), ih/iw = oh*S - P / ow*S - P and the element bases
+// dyb = pix * yps and xb = ((b H + ih) W + iw) xps; a 64-pixel step adds fixed deltas and walks the
+// row / image wraps.  Invalid sources get kBufOob (range-checked to zero by the hardware).
+struct WgradLdsB {
+  static constexpr int PPW = 4;
+  __amdgpu_buffer_rsrc_t rx, rdy;
+  int NP, OW, OH, H, W, S;
+  int dyStep, xStep, xWrapOW, xRow, xImg;   // uniform element deltas
+  int co[2], tap[2], bkh[2], bkw[2];        // per lane half: dy column / x tap offset, tap
+  bool cok[2], bok[2];
+  int pix[PPW], oh[PPW], ow[PPW], ih[PPW], iw[PPW], dyb[PPW], xb[PPW];
+  DEV WgradLdsB(const bf16* x, const bf16* dy, const Geom& g, int m0, int n0, int kt0, int wid, int lane,
+                unsigned xbytes, unsigned dybytes)
+      : OW(g.OW), OH(g.OH), H(g.H), W(g.W), S(g.S) {
+    rx = make_rsrc(x, xbytes);
+    rdy = make_rsrc(dy, dybytes);
+    NP = g.N * g.OH * g.OW;
+    const int Ntot = g.KH * g.KW * g.C, xps = (int)g.xps, yps = (int)g.yps;
+    dyStep = 64 * yps;
+    xStep = 64 * g.S * xps;
+    xWrapOW = g.OW * g.S * xps;
+    xRow = g.S * g.W * xps;
+    xImg = (g.H - g.OH * g.S) * g.W * xps;
+    const int q = lane >> 4, sl = lane & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = sl ^ (2 * (q | (h << 2)));
+      co[h] = m0 + c * 8;
+      cok[h] = co[h] < g.K;
+      const int n = n0 + c * 8;
+      bok[h] = n < Ntot;
+      const int nn = bok[h] ? n : 0;
+      const int ci = nn % g.C, t = nn / g.C;
+      bkw[h] = t % g.KW;
+      bkh[h] = t / g.KW;
+      tap[h] = (bkh[h] * g.W + bkw[h]) * xps + ci;
+    }
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      pix[j] = kt0 * 64 + (wid * PPW + j) * 4 + q;
+      const int pp = pix[j] < NP ? pix[j] : 0;
+      ow[j] = pp % g.OW;
+      const int t = pp / g.OW;
+      oh[j] = t % g.OH;
+      const int b = t / g.OH;
+      ih[j] = oh[j] * g.S - g.P;
+      iw[j] = ow[j] * g.S - g.P;
+      dyb[j] = pix[j] * yps;
+      xb[j] = ((b * g.H + ih[j]) * g.W + iw[j]) * xps;
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int piece = wid * PPW + j;
+      const int h = (j >> 1) & 1;  // bit 3 of the pixel row 4 piece + q (wid * PPW is a multiple of 4)
+      const bool pin = pix[j] < NP;
+      blds16(rdy, (pin && cok[h]) ? (unsigned)(dyb[j] + co[h]) * 2u : kBufOob, stage + piece * 1024);
+      const bool okb = pin && bok[h] && (unsigned)(ih[j] + bkh[h]) < (unsigned)H && (unsigned)(iw[j] + bkw[h]) < (unsigned)W;
+      blds16(rx, okb ? (unsigned)(xb[j] + tap[h]) * 2u : kBufOob, stage + 16384 + piece * 1024);
+      pix[j] += 64;
+      dyb[j] += dyStep;
+      ow[j] += 64;
+      iw[j] += 64 * S;
+      xb[j] += xStep;
+      while (ow[j] >= OW) {
+        ow[j] -= OW;
+        iw[j] -= OW * S;
+        xb[j] += xRow - xWrapOW;
+        ih[j] += S;
+        if (++oh[j] == OH) {
+          oh[j] = 0;
+          ih[j] -= OH * S;
+          xb[j] += xImg;
+        }
+      }
+    }
+  }
+};
+
+template <int NS, int BUF>
 __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                     float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn) {
+                                                     float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn,
+                                                     unsigned xbytes, unsigned dybytes) {
   constexpr int BM = 128, BN = 128, STAGE = 32768;
   constexpr int LDS = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
@@ -1007,7 +1207,38 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk > 0) {
+  if (nk > 0 && BUF > 0) {
+    // fragments of the whole step first, then the next stage's DMA while they land, then 32 MFMAs
+    WgradLdsB ld(x, dy, g, m0, n0, kt0, wid, lane, xbytes, dybytes);
+    ld.issue(smem, wid);
+    if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (NS == 3 && kt + 1 < nk) vm_wait<8>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      if (BUF == 2 && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = As + 64 * BM;
+      bf16x8 a[2][4], b[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[h][i] = frag_k<BM>(As, wm * 64 + i * 16, h * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[h][j] = frag_k<BN>(Bs, wn * 64 + j * 16, h * 32, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (BUF == 1 && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+    }
+  } else if (nk > 0) {
     WgradLds<NS> ld(x, dy, g, m0, n0, kt0, wid, lane);
     ld.issue(smem, wid);
     if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
@@ -1276,21 +1507,44 @@ inline bool v3_ok(int C, long xps, int K, long yps, const void* x, const void* w
 
 // gv = GEMM view (rows N*OH*OW, columns K, gather tensor H x W x C with stride xps); BN partials need
 // 64-row wave rows, numbered 4 per 256-row tile (= dmy_conv_fwd_partial_rows when K > 64)
+inline int conv_buf_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_CONV_BUF");
+    return e ? atoi(e) : 1;
+  }();
+  return t;
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
-#define V3_LAUNCH(BM, BN, NS)                                                                                      \
-  {                                                                                                                \
-    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
-    const unsigned grid = (unsigned)gm * gn;                                                                       \
-    if (p1) v3::conv_fwd_v3<BM, BN, NS, true, DG><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn); \
-    else v3::conv_fwd_v3<BM, BN, NS, false, DG><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn); \
+  // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
+  const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
+  const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
+  const unsigned xbytes = buf ? (unsigned)xb : 0u, wbytes = buf ? (unsigned)wb : 0u;
+#define V3_GO(BM, BN, NS, P1_, BUF_) \
+  v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes)
+#define V3_LAUNCH(BM, BN, NS)                                \
+  {                                                          \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN); \
+    const unsigned grid = (unsigned)gm * gn;                 \
+    if (buf && conv_buf_mode() == 2) {                       \
+      if (p1) V3_GO(BM, BN, NS, true, 2);                    \
+      else V3_GO(BM, BN, NS, false, 2);                      \
+    } else if (buf) {                                        \
+      if (p1) V3_GO(BM, BN, NS, true, 1);                    \
+      else V3_GO(BM, BN, NS, false, 1);                      \
+    } else {                                                 \
+      if (p1) V3_GO(BM, BN, NS, true, 0);                    \
+      else V3_GO(BM, BN, NS, false, 0);                      \
+    }                                                        \
   }
   if (gv.K > 64) V3_LAUNCH(256, 128, 3)
   else V3_LAUNCH(256, 64, 2)
 #undef V3_LAUNCH
+#undef V3_GO
   return (int)hipGetLastError();
 }
 
@@ -1365,7 +1619,14 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)gm * gn, splits);
   (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
-  v3::conv_wgrad_v3<2><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
+  const bool buf = conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
+  if (buf && conv_buf_mode() == 2)
+    v3::conv_wgrad_v3<2, 2><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  else if (buf)
+    v3::conv_wgrad_v3<2, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  else
+    v3::conv_wgrad_v3<2, 0><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
   return (int)hipGetLastError();
 }
 
