@@ -1359,9 +1359,92 @@ struct WgradLdsN {
   }
 };
 
-template <int BM, int BN, int NS>
+// Buffer-descriptor form of WgradLdsN (same LDS images): 32-bit element offsets advanced by adds
+// (see WgradLdsB).  A piece j: pixel row r, dy column co; B piece j: pixel row r, column n -> tap.
+template <int BM, int BN>
+struct WgradLdsNB {
+  using L = WgradLdsN<BM, BN>;
+  static constexpr int PAW = L::PAW, PBW = L::PBW, A_BYTES = L::A_BYTES;
+  __amdgpu_buffer_rsrc_t rx, rdy;
+  int NP, OW, OH, H, W, S, dyStep, xStep, xWrapOW, xRow, xImg;
+  int apix[PAW], adyb[PAW];
+  int bpix[PBW], boh[PBW], bow[PBW], bih[PBW], biw[PBW], bxb[PBW], bkh[PBW], bkw[PBW], btap[PBW];
+  DEV WgradLdsNB(const bf16* x, const bf16* dy, const Geom& g, int m0, int n0, int kt0, int wid, int lane,
+                 unsigned xbytes, unsigned dybytes)
+      : OW(g.OW), OH(g.OH), H(g.H), W(g.W), S(g.S) {
+    rx = make_rsrc(x, xbytes);
+    rdy = make_rsrc(dy, dybytes);
+    NP = g.N * g.OH * g.OW;
+    const int Ntot = g.KH * g.KW * g.C, xps = (int)g.xps, yps = (int)g.yps;
+    dyStep = 64 * yps;
+    xStep = 64 * g.S * xps;
+    xWrapOW = g.OW * g.S * xps;
+    xRow = g.S * g.W * xps;
+    xImg = (g.H - g.OH * g.S) * g.W * xps;
+#pragma unroll
+    for (int j = 0; j < PAW; ++j) {
+      const int r = (wid * PAW + j) * L::RPA + lane / L::SA;
+      apix[j] = kt0 * 64 + r;
+      const int co = m0 + 8 * kmaj_chunk<BM>(r, lane % L::SA);
+      // an out-of-range column never becomes valid: fold it into the pixel bound
+      adyb[j] = apix[j] * yps + co;
+      if (co >= g.K) apix[j] = 0x40000000;
+    }
+#pragma unroll
+    for (int j = 0; j < PBW; ++j) {
+      const int r = (wid * PBW + j) * L::RPB + lane / L::SB;
+      bpix[j] = kt0 * 64 + r;
+      const int pp = bpix[j] < NP ? bpix[j] : 0;
+      bow[j] = pp % g.OW;
+      const int t = pp / g.OW;
+      boh[j] = t % g.OH;
+      const int b = t / g.OH;
+      bih[j] = boh[j] * g.S - g.P;
+      biw[j] = bow[j] * g.S - g.P;
+      bxb[j] = ((b * g.H + bih[j]) * g.W + biw[j]) * xps;
+      const int n = n0 + 8 * kmaj_chunk<BN>(r, lane % L::SB);
+      const int nn = n < Ntot ? n : 0;
+      const int ci = nn % g.C, u = nn / g.C;
+      bkw[j] = u % g.KW;
+      bkh[j] = u / g.KW;
+      btap[j] = (bkh[j] * g.W + bkw[j]) * xps + ci;
+      if (n >= Ntot) bkh[j] = 0x40000000;  // never in-image
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+#pragma unroll
+    for (int j = 0; j < PAW; ++j) {
+      blds16(rdy, apix[j] < NP ? (unsigned)adyb[j] * 2u : kBufOob, stage + (wid * PAW + j) * 1024);
+      apix[j] += 64;
+      adyb[j] += dyStep;
+    }
+#pragma unroll
+    for (int j = 0; j < PBW; ++j) {
+      const bool ok = bpix[j] < NP && (unsigned)(bih[j] + bkh[j]) < (unsigned)H && (unsigned)(biw[j] + bkw[j]) < (unsigned)W;
+      blds16(rx, ok ? (unsigned)(bxb[j] + btap[j]) * 2u : kBufOob, stage + A_BYTES + (wid * PBW + j) * 1024);
+      bpix[j] += 64;
+      bow[j] += 64;
+      biw[j] += 64 * S;
+      bxb[j] += xStep;
+      while (bow[j] >= OW) {
+        bow[j] -= OW;
+        biw[j] -= OW * S;
+        bxb[j] += xRow - xWrapOW;
+        bih[j] += S;
+        if (++boh[j] == OH) {
+          boh[j] = 0;
+          bih[j] -= OH * S;
+          bxb[j] += xImg;
+        }
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int NS, bool BUF>
 __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                    float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn) {
+                                                    float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn,
+                                                    unsigned xbytes, unsigned dybytes) {
   using LD = WgradLdsN<BM, BN>;
   constexpr int STAGE = LD::STAGE, TM = BM / 16, PER = LD::PAW + LD::PBW;
   constexpr int LDSB = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
@@ -1379,7 +1462,36 @@ __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x,
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk > 0) {
+  if (nk > 0 && BUF) {
+    WgradLdsNB<BM, BN> ld(x, dy, g, m0, n0, kt0, wid, lane, xbytes, dybytes);
+    ld.issue(smem, wid);
+    if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+      bf16x8 a[2][TM], b[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[h][i] = frag_k<BM>(As, i * 16, h * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[h][j] = frag_k<BN>(Bs, wid * 64 + j * 16, h * 32, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+    }
+  } else if (nk > 0) {
     LD ld(x, dy, g, m0, n0, kt0, wid, lane);
     ld.issue(smem, wid);
     if (NS == 3 && nk > 1) ld.issue(smem + STAGE, wid);
@@ -1661,18 +1773,29 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hi
   const dim3 grid((unsigned)tiles, splits);
   (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   constexpr int NS = 3 * v3::WgradLdsN<BM, BN>::STAGE <= 80 * 1024 ? 3 : 2;  // keep 2 blocks per CU
-  v3::conv_wgrad_v3n<BM, BN, NS><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
+  if (conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob)
+    v3::conv_wgrad_v3n<BM, BN, NS, true><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  else
+    v3::conv_wgrad_v3n<BM, BN, NS, false><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
   return (int)hipGetLastError();
 }
 
+// weight-grad of layers with <= 64 output channels: 0 = v2 register-staged 64 x 64 tiles, 1 = the
+// narrow LDS-DMA tiles (BM 32/64), 2 = the 128 x 128 LDS-DMA tile (half its rows idle at K = 64),
+// 3 = auto (default): narrow tiles past 8 M pixels at K = 64, the 128 tile otherwise (tools/gpu/ab_conv.sh:
+// 64 ch @768^2 x 32 narrow 483 / 128-tile 394 / v2 257 TFLOP/s; @384^2 280 / 384 / 261; yolov5s layers 128-tile best)
 inline int wgrad_narrow_mode() {
   static int t = [] {
-    // off by default: measured slower than the register-staged v2 64x64 tiles on the yolov5s narrow
-    // layers (tools/gpu/tune_narrow.sh); kept selectable (and parity-tested) for tuning
     const char* e = getenv("DMY_WGRAD_NARROW");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 3;
   }();
   return t;
+}
+inline int wgrad_narrow_for(const Geom& g, long NP) {
+  const int m = wgrad_narrow_mode();
+  if (m != 3) return m;
+  return (g.K == 64 && NP >= 8L * 1024 * 1024) ? 1 : 2;
 }
 
 template <typename T>
@@ -1681,9 +1804,10 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const long NP = (long)g.N * g.OH * g.OW;
     const int Ntot = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy);
-    if (vec && g.K > 64 && Ntot > 64 && NP >= 16384)
+    const int nm = wgrad_narrow_for(g, NP);
+    if (vec && (g.K > 64 || nm == 2) && Ntot > 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
-    if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && wgrad_narrow_mode()) {
+    if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && nm == 1) {
       const bool wide = Ntot >= 512 || Ntot % 256 == 0;
       if (g.K <= 32) return wide ? launch_wgrad_v3n<32, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
                                  : launch_wgrad_v3n<32, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
