@@ -1614,7 +1614,7 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
 // v3 (LDS-DMA) kernels apply to bf16 with 16-B vectors everywhere and enough rows to fill the chip
 inline bool v3_ok(int C, long xps, int K, long yps, const void* x, const void* w, const void* y, long M) {
   return C % 8 == 0 && xps % 8 == 0 && K % 8 == 0 && yps % 8 == 0 && aligned16(x) && aligned16(w) && aligned16(y) &&
-         M >= 16384 && K >= 64;
+         M >= 16384 && K >= 32;
 }
 
 // gv = GEMM view (rows N*OH*OW, columns K, gather tensor H x W x C with stride xps); BN partials need
@@ -1805,7 +1805,7 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const int Ntot = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy);
     const int nm = wgrad_narrow_for(g, NP);
-    if (vec && (g.K > 64 || nm == 2) && Ntot > 64 && NP >= 16384)
+    if (vec && (g.K > 64 || nm == 2) && Ntot >= 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && nm == 1) {
       const bool wide = Ntot >= 512 || Ntot % 256 == 0;
