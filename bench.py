@@ -192,9 +192,19 @@ def main():
     dom = max(ks, key=lambda k: ks[k]['seconds'])
     d = ks[dom]
     achieved = d['flops'] / d['launches'] / (d['seconds'] / d['launches']) / 1e12
+    # traffic: HBM bytes per launch of the same kernel family from the committed rocprofv3 --pmc passes
+    # (FETCH_SIZE / WRITE_SIZE in separate runs of this bench command, tools/gpu/pmc.sh + tools/pmc_traffic.py)
+    traffic, tsrc = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tpath):
+        tr = json.load(open(tpath)).get(a.config, {}).get(dom)
+        if tr:
+            traffic, tsrc = round(tr['bytes_per_launch']), 'profiles/pmc_traffic.json: ' + tr['source']
     roof = dict(bound='mfma', kernel=f'dmy_{dom} (implicit-GEMM, all launches of the timed region)',
                 achieved=round(achieved, 2), peak=PEAK[dtype], unit='TFLOP/s', frac=round(achieved / PEAK[dtype], 4),
-                traffic=None, launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
+                traffic=traffic, traffic_unit='bytes/launch (HBM, PMC)', traffic_source=tsrc,
+                algorithmic_bytes_per_launch=round(d['bytes'] / d['launches']),
+                launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
                 kernels={k: dict(launches=v['launches'], ms=round(v['seconds'] * 1e3 / a.steps, 3),
                                  tflops=round(v['flops'] / v['seconds'] / 1e12, 2)) for k, v in ks.items()},
                 conv_share_of_step=round(sum(v['seconds'] for v in ks.values()) / el, 3))

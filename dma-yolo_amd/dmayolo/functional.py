@@ -141,43 +141,47 @@ class KernelTimer:
     """Live per-launch timing of the implicit-GEMM conv kernels with HIP events on the launch
     stream (bench.py roofline).  Off by default; zero overhead when disabled."""
     enabled = False
-    records = []  # (kind, algorithmic_flops, start_event, end_event, shape tag)
+    records = []  # (kind, algorithmic_flops, algorithmic_bytes, start_event, end_event, shape tag)
 
     @classmethod
-    def run(cls, kind, flops, name, *args, tag=None):
+    def run(cls, kind, flops, name, *args, tag=None, nbytes=0.0):
+        """nbytes: algorithmic HBM bytes of the launch (operands read once, result written once)"""
         if not cls.enabled:
             return call(name, *args)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         call(name, *args)
         e1.record()
-        cls.records.append((kind, flops, e0, e1, tag))
+        cls.records.append((kind, flops, nbytes, e0, e1, tag))
 
     @classmethod
     def summary(cls, detail=None):
         """per-kind totals; when `detail` is a dict it also receives per-(kind, shape) totals"""
         torch.cuda.synchronize()
         out = {}
-        for kind, fl, e0, e1, tag in cls.records:
+        for kind, fl, nb, e0, e1, tag in cls.records:
             t = e0.elapsed_time(e1) * 1e-3
-            d = out.setdefault(kind, [0, 0.0, 0.0])
+            d = out.setdefault(kind, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += fl
             d[2] += t
+            d[3] += nb
             if detail is not None:
-                d = detail.setdefault((kind, tag), [0, 0.0, 0.0])
+                d = detail.setdefault((kind, tag), [0, 0.0, 0.0, 0.0])
                 d[0] += 1
                 d[1] += fl
                 d[2] += t
+                d[3] += nb
         cls.records = []
-        return {k: dict(launches=v[0], flops=v[1], seconds=v[2]) for k, v in out.items()}
+        return {k: dict(launches=v[0], flops=v[1], seconds=v[2], bytes=v[3]) for k, v in out.items()}
 
 
 def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
     N, C, H, W = x.shape
+    es = x.element_size()
     KernelTimer.run('conv_fwd', 2.0 * N * OH * OW * K * C * k * k, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf),
                     ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(),
-                    tag=(N, C, H, W, K, k, s))
+                    tag=(N, C, H, W, K, k, s), nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -307,12 +311,14 @@ class ConvBNActFn(torch.autograd.Function):
                 raise NotImplementedError('input gradient of a channel-padded stem conv')
             buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
             KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf),
-                            acc, N, H, W, C, bps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s))
+                            acc, N, H, W, C, bps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
+                            nbytes=z.element_size() * (M * K + K * C * k * k + (1 + acc) * N * H * W * C))
             dx = sink_result(ctx.xsink, buf)
         if ctx.needs_input_grad[1]:
             dwo = f32(K * Cp * k * k, dev)
             KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
-                            H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s))
+                            H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
+                            nbytes=z.element_size() * (N * H * W * Cp + M * K) + 4 * K * Cp * k * k)
             dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
             call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
         dres = None
