@@ -1627,6 +1627,16 @@ inline int conv_buf_mode() {
   return t;
 }
 
+// tile of the 1x1 (pure GEMM) layers: 0 = 256 x 128, 3 stages; 1 = 128 x 128, 2 stages (2 blocks / CU);
+// 2 = 128 x 128, 3 stages
+inline int p1_tile_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_P1_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  return t;
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st) {
@@ -1653,7 +1663,10 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
   }
-  if (gv.K > 64) V3_LAUNCH(256, 128, 3)
+  const int pt = p1 ? p1_tile_mode() : 0;
+  if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
+  else if (gv.K > 64 && pt == 2) V3_LAUNCH(128, 128, 3)
+  else if (gv.K > 64) V3_LAUNCH(256, 128, 3)
   else V3_LAUNCH(256, 64, 2)
 #undef V3_LAUNCH
 #undef V3_GO
@@ -1733,7 +1746,13 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   const bool buf = conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
-  if (buf && conv_buf_mode() == 2)
+  static const int ns3 = [] {
+    const char* e = getenv("DMY_WGRAD_NS");
+    return e ? atoi(e) == 3 : 0;
+  }();
+  if (buf && ns3)
+    v3::conv_wgrad_v3<3, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  else if (buf && conv_buf_mode() == 2)
     v3::conv_wgrad_v3<2, 2><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   else if (buf)
     v3::conv_wgrad_v3<2, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);

@@ -17,6 +17,9 @@ SETS = {
             (32, 512, 96, 96, 512, 3, 1), (32, 512, 192, 192, 128, 1, 1)],
     'narrow': [(64, 8, 640, 640, 32, 6, 2), (64, 64, 80, 80, 64, 3, 1), (64, 32, 160, 160, 32, 3, 1),
                (64, 32, 320, 320, 64, 3, 2), (64, 256, 80, 80, 64, 1, 1), (64, 64, 160, 160, 32, 1, 1)],
+    'p1': [(32, 256, 96, 96, 256, 1, 1), (32, 512, 192, 192, 128, 1, 1), (32, 1024, 96, 96, 256, 1, 1),
+           (32, 256, 192, 192, 128, 1, 1), (32, 1024, 48, 48, 512, 1, 1), (32, 512, 96, 96, 512, 1, 1),
+           (64, 256, 40, 40, 128, 1, 1), (64, 512, 20, 20, 256, 1, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
 }
