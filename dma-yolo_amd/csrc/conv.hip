@@ -813,22 +813,36 @@ DEV void blds16(__amdgpu_buffer_rsrc_t r, unsigned off, char* lds_wave_base) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0, 0, 0);
 }
 
-template <int BM, int BN, int NS, bool P1, bool DG>
+// Stride-2 data-grad parity class (a, b) (S2): rows are the input pixels (2 i2 + a, 2 j2 + b); only the
+// taps of matching parity (kh = a + P mod 2, kw = b + P mod 2, stepping by 2) reach them, from dy pixel
+// (i2 + (a + P - kh) / 2, j2 + (b + P - kw) / 2).  The GEMM view g has (H, W, C) = dy, (OH, OW) = the
+// class's rows, K = input channels; S2Cls carries the class and dx's spatial size for the epilogue.
+struct S2Cls {
+  int a, b, HX, WX;
+};
+
+template <int BM, int BN, int NS, bool P1, bool DG, bool S2 = false>
 struct FwdLdsB {
   using C3_ = Cfg3<BM, BN, NS>;
   __amdgpu_buffer_rsrc_t rx, rw;
   int H, W, C, KW, xps;
   int kh, kw, ci0, kpos;            // uniform cursor of the next K step
+  int kw0, ca, cb, P;               // S2: first kw of the class's parity, class, pad
   int kl;                           // this lane's (swizzled) 16-B chunk within the step, in elements
   int pix[C3_::APW], ih0[C3_::APW], iw0[C3_::APW];
   bool aval[C3_::APW];
   unsigned boff[C3_::BPW];
   DEV FwdLdsB(const bf16* x, const bf16* w, const Geom& g, long M, long m0, int n0, int wid, int lane, unsigned xbytes,
-              unsigned wbytes)
+              unsigned wbytes, S2Cls cls = S2Cls{0, 0, 0, 0})
       : H(g.H), W(g.W), C(g.C), KW(g.KW), xps((int)g.xps), kh(0), kw(0), ci0(0), kpos(0) {
     rx = make_rsrc(x, xbytes);
     rw = make_rsrc(w, wbytes);
     const int Ktot = g.KH * g.KW * g.C;
+    P = g.P;
+    ca = cls.a;
+    cb = cls.b;
+    kw0 = (cls.b + g.P) & 1;
+    if (S2) { kh = (cls.a + g.P) & 1; kw = kw0; }
     kl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
 #pragma unroll
     for (int j = 0; j < C3_::APW; ++j) {
@@ -838,8 +852,8 @@ struct FwdLdsB {
       const int ow = mm % g.OW, t = mm / g.OW, oh = t % g.OH, b = t / g.OH;
       if (P1) { pix[j] = mm * xps; ih0[j] = 0; iw0[j] = 0; }
       else {
-        ih0[j] = DG ? oh + g.P : oh * g.S - g.P;
-        iw0[j] = DG ? ow + g.P : ow * g.S - g.P;
+        ih0[j] = S2 ? oh : DG ? oh + g.P : oh * g.S - g.P;
+        iw0[j] = S2 ? ow : DG ? ow + g.P : ow * g.S - g.P;
         pix[j] = ((b * g.H + ih0[j]) * g.W + iw0[j]) * xps;  // may be negative; valid taps land >= 0
       }
     }
@@ -850,8 +864,9 @@ struct FwdLdsB {
     }
   }
   DEV void issue(char* stage, int wid) {
-    const int dh = DG ? -kh : kh, dw = DG ? -kw : kw;
+    const int dh = S2 ? (ca + P - kh) >> 1 : DG ? -kh : kh, dw = S2 ? (cb + P - kw) >> 1 : DG ? -kw : kw;
     const int delta = P1 ? kpos + kl : (dh * W + dw) * xps + ci0 + kl;
+    const int bk = S2 ? (kh * KW + kw) * C + ci0 : kpos;  // this step's column of the (kh, kw, c) weight rows
 #pragma unroll
     for (int j = 0; j < C3_::APW; ++j) {
       bool ok = aval[j];
@@ -860,14 +875,20 @@ struct FwdLdsB {
     }
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j)
-      blds16(rw, boff[j] == kBufOob ? kBufOob : boff[j] + (unsigned)kpos * 2u,
+      blds16(rw, boff[j] == kBufOob ? kBufOob : boff[j] + (unsigned)bk * 2u,
              stage + C3_::A_BYTES + (wid * C3_::BPW + j) * 1024);
     kpos += BK;
     if (!P1) {
       ci0 += BK;
       if (ci0 == C) {
         ci0 = 0;
-        if (++kw == KW) { kw = 0; ++kh; }
+        if (S2) {
+          kw += 2;
+          if (kw >= KW) { kw = kw0; kh += 2; }
+        } else if (++kw == KW) {
+          kw = 0;
+          ++kh;
+        }
       }
     }
   }
@@ -947,7 +968,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
                                                             float* __restrict__ psum, float* __restrict__ psq,
                                                             int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                            unsigned wbytes) {
+                                                            unsigned wbytes, S2Cls cls) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -961,8 +982,14 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
-  if constexpr (BUF > 0) {
+  // BUF: 0 = FwdLds, 1 = buffer loader (fragments first), 2 = buffer loader (DMA first), 3 = buffer loader,
+  // stride-2 data-grad parity class `cls` (only the class's taps: ceil((KH - kh0) / 2) x ceil((KW - kw0) / 2))
+  const int nk = BUF == 3 ? ((g.KH - ((cls.a + g.P) & 1) + 1) / 2) * ((g.KW - ((cls.b + g.P) & 1) + 1) / 2) * (g.C / BK)
+                          : (g.KH * g.KW * g.C + BK - 1) / BK;
+  if constexpr (BUF == 3) {
+    FwdLdsB<BM, BN, NS, false, true, true> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes, cls);
+    mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+  } else if constexpr (BUF > 0) {
     FwdLdsB<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
     mainloop4<BM, BN, NS, BUF == 2>(ld, nk, smem, acc, wid, lane);
   } else {
@@ -1027,7 +1054,14 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
     const int n = n0 + cv * 8;
     if (m >= M || n >= g.K) continue;
     uint4 v = *reinterpret_cast<const uint4*>(ct + row * RS + cv * 8);
-    uint4* dst = reinterpret_cast<uint4*>(y + m * g.yps + n);
+    long pix = m;
+    if (BUF == 3) {  // class row (b, i2, j2) -> dx pixel (b, 2 i2 + a, 2 j2 + b)
+      const int j2 = (int)(m % g.OW);
+      const long t = m / g.OW;
+      const int i2 = (int)(t % g.OH), bb = (int)(t / g.OH);
+      pix = ((long)bb * cls.HX + 2 * i2 + cls.a) * cls.WX + 2 * j2 + cls.b;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + n);
     if (accumulate) {
       float a[8], b[8];
       unpack<bf16>(v, a);
@@ -1646,8 +1680,9 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
   const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
   const unsigned xbytes = buf ? (unsigned)xb : 0u, wbytes = buf ? (unsigned)wb : 0u;
-#define V3_GO(BM, BN, NS, P1_, BUF_) \
-  v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes)
+#define V3_GO(BM, BN, NS, P1_, BUF_)                                                                          \
+  v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
+                                                                          wbytes, v3::S2Cls{0, 0, 0, 0})
 #define V3_LAUNCH(BM, BN, NS)                                \
   {                                                          \
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN); \
@@ -1684,10 +1719,44 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
   return launch_fwd<T, 64, 64>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
 }
+// stride-2 data-grad on the v3 buffer loader: one launch per output-parity class (a, b), each a GEMM
+// over the class's input pixels and only the taps of matching parity (FwdLdsB S2 mode)
+inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const void* dx) {
+  if (g.S != 2 || !conv_buf_mode() || g.K % 64 != 0 || g.KH < 2 || g.KW < 2) return false;
+  const long Mmin = (long)g.N * (g.H / 2) * (g.W / 2);
+  const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
+  return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
+}
+inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc, const Geom& g, hipStream_t st) {
+  const unsigned xbytes = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
+  const unsigned wbytes = (unsigned)(2.0 * g.C * g.KH * g.KW * g.K);
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      const int H2 = (g.H - a + 1) / 2, W2 = (g.W - b + 1) / 2;
+      if (H2 <= 0 || W2 <= 0) continue;
+      // GEMM view: gather dy (OH x OW x K, stride yps), rows = the class's (N, H2, W2), columns = C
+      const Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 2, g.P, H2, W2, g.xps);
+      const long M = (long)g.N * H2 * W2;
+      const v3::S2Cls cls{a, b, g.H, g.W};
+      if (g.C > 64) {
+        const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
+        v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls);
+      } else {
+        const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 64);
+        v3::conv_fwd_v3<256, 64, 2, false, true, 3><<<(unsigned)gm * gn, 256, 0, st>>>(
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls);
+      }
+    }
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st) {
   const long M = (long)g.N * g.H * g.W / (g.S == 2 ? 4 : 1);
   if constexpr (sizeof(T) == 2) {
+    if (dgrad_s2_v3_ok(g, dy, wt, dx))
+      return launch_dgrad_s2_v3((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, g, st);
     if (g.S == 1 && g.OH == g.H + 2 * g.P - g.KH + 1 && g.OW == g.W + 2 * g.P - g.KW + 1 &&
         v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M)) {
       // GEMM view: rows = input pixels (N, H, W), columns = C, gather dy (OH x OW x K, stride yps)

@@ -430,14 +430,22 @@ __global__ void __launch_bounds__(256) winattn_bwd_kernel(const T* __restrict__ 
 }
 
 // table grad [225][nh] = sum over window groups
-__global__ void dtab_reduce_kernel(const float* __restrict__ part, int ngroups, int nh, float* __restrict__ dtab) {
+// one workgroup per table entry: 256 lanes stride over the groups, fixed-order fp64 tree in LDS
+__global__ void __launch_bounds__(256) dtab_reduce_kernel(const float* __restrict__ part, int ngroups, int nh,
+                                                          float* __restrict__ dtab) {
   const int ntab = (2 * WS - 1) * (2 * WS - 1);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ntab * nh) return;
+  const int e = blockIdx.x;
   const int idx = e / nh, h = e % nh;
+  __shared__ double red[256];
   double s = 0.0;
-  for (int gi = 0; gi < ngroups; ++gi) s += part[((long)gi * nh + h) * ntab + idx];
-  dtab[e] = (float)s;
+  for (int gi = threadIdx.x; gi < ngroups; gi += 256) s += part[((long)gi * nh + h) * ntab + idx];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dtab[e] = (float)red[0];
 }
 
 // per-sample scale (DropPath, common.py:386-403): y = x * sc[b]  (sc = floor(keep + u) / keep)
@@ -645,6 +653,15 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
   bf16* Ds = Vs + MATQ;  // dO
   bf16* Ps = Ds + MATQ;  // P, then dS
   const int w0 = blockIdx.x * wpb, w1 = min(nwin, w0 + wpb);
+  // dS summed per (q, k) position over this wave's windows in registers; binned into the bias-table
+  // gradient once per workgroup (the bin depends on (q, k) only, not on the window)
+  float dsacc[4][4][4];
+#pragma unroll
+  for (int bq = 0; bq < 4; ++bq)
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dsacc[bq][bk][r] = 0.f;
   for (int base = w0; base < w1; base += NW) {
     const int wid = base + w;
     const bool live = wid < w1;
@@ -695,15 +712,13 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
         }
         rs += __shfl_xor(rs, 16, 64);
         rs += __shfl_xor(rs, 32, 64);
-        const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
 #pragma unroll
         for (int bk = 0; bk < 4; ++bk)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float ds = P[bq][bk][r] * (dp[bk][r] - rs);
             P[bq][bk][r] = ds;
-            const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
-            atomicAdd(&dtab[(ri - rj + WS - 1) * (2 * WS - 1) + (ci - cj + WS - 1)], ds);
+            dsacc[bq][bk][r] += ds;
           }
       }
     }
@@ -738,6 +753,17 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
       store_tok(Ks, dqkv, 3L * g.C, (long)g.C + head * HD, p, lane);
       store_tok(Vs, dqkv, 3L * g.C, 2L * g.C + head * HD, p, lane);
     }
+  }
+#pragma unroll
+  for (int bq = 0; bq < 4; ++bq) {
+    const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
+        atomicAdd(&dtab[(ri - rj + WS - 1) * (2 * WS - 1) + (ci - cj + WS - 1)], dsacc[bq][bk][r]);
+      }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < NTAB; e += blockDim.x) dtab_part[((long)blockIdx.x * g.nh + head) * NTAB + e] = dtab[e];
@@ -847,7 +873,7 @@ DMY_API int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const 
   if (dtype) winattn_bwd_mfma<2><<<grid, 128, 0, st>>>((const bf16*)qkv, (const bf16*)dout, table, (bf16*)dqkv, dtab_part, nwin, wpb, g);
   else winattn_bwd_kernel<float><<<grid, 256, 0, st>>>((const float*)qkv, (const float*)dout, table, (float*)dqkv, dtab_part, nwin, wpb, g);
   const int ntab = (2 * WS - 1) * (2 * WS - 1) * nh;
-  dtab_reduce_kernel<<<ceil_div(ntab, 256), 256, 0, st>>>(dtab_part, groups, nh, dtab);
+  dtab_reduce_kernel<<<ntab, 256, 0, st>>>(dtab_part, groups, nh, dtab);
   return (int)hipGetLastError();
 }
 

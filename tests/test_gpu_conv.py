@@ -16,7 +16,9 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           (16, 32, 64, 64, 32, 3, 1), (4, 64, 80, 80, 64, 3, 1), (16, 256, 40, 40, 64, 1, 1),
           (8, 8, 192, 192, 32, 6, 2), (8, 136, 60, 50, 40, 1, 1), (8, 32, 96, 96, 64, 3, 2),
           # buffer-descriptor v3 loader (C % 64 == 0): ragged M and K, 3 K steps per tap, stride 2
-          (11, 128, 37, 45, 200, 3, 1), (6, 192, 52, 60, 136, 3, 1), (4, 64, 130, 122, 256, 3, 2)]
+          (11, 128, 37, 45, 200, 3, 1), (6, 192, 52, 60, 136, 3, 1), (4, 64, 130, 122, 256, 3, 2),
+          # stride-2 data-grad on the buffer loader, one launch per parity class: odd sizes, 3 K steps per tap
+          (12, 64, 75, 91, 128, 3, 2), (8, 128, 101, 99, 192, 3, 2)]
 
 
 def _rel(a, b):
