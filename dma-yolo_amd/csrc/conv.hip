@@ -628,13 +628,16 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const T* __restrict__ x,
   using TT = Tile<T, BM, BN, true, true>;
   __shared__ __attribute__((aligned(16))) char smem[TT::LDS_BYTES];
   T* lds = reinterpret_cast<T*>(smem);
-  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  // (tile, split) from the linear dispatch id: consecutive logical ids share an XCD, so all tiles of
+  // a split (which read the same pixel chunk) run on one XCD and share its L2
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
   const int tm = tile / gn, tn = tile % gn;
   const int m0 = tm * BM, n0 = tn * BN;
   WgradLoader<T, BM, BN, VECA, VECB> ld(x, dy, g, m0, n0);
   const long NP = (long)g.N * g.OH * g.OW;
   const int nk = (int)((NP + TT::BK - 1) / TT::BK);
-  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt0 = split * kt_per_split;
   const int kt1 = min(nk, kt0 + kt_per_split);
   f32x4 acc[TT::TM][TT::TN];
   zero_acc<BM, BN>(acc);
@@ -1229,12 +1232,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  // (tile, split) from the linear dispatch id: consecutive logical ids share an XCD, so all tiles of
+  // a split (which read the same pixel chunk) run on one XCD and share its L2
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
   const int tm = tile / gn, tn = tile % gn;
   const int m0 = tm * BM, n0 = tn * BN;
   const long NP = (long)g.N * g.OH * g.OW;
   const int nk_all = (int)((NP + 63) / 64);
-  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt0 = split * kt_per_split;
   const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
   f32x4 acc[4][4];
 #pragma unroll
@@ -1484,12 +1490,15 @@ __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x,
   constexpr int LDSB = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDSB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  // (tile, split) from the linear dispatch id: consecutive logical ids share an XCD, so all tiles of
+  // a split (which read the same pixel chunk) run on one XCD and share its L2
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
   const int tm = tile / gn, tn = tile % gn;
   const int m0 = tm * BM, n0 = tn * BN;
   const long NP = (long)g.N * g.OH * g.OW;
   const int nk_all = (int)((NP + 63) / 64);
-  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt0 = split * kt_per_split;
   const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
   f32x4 acc[TM][4];
 #pragma unroll
