@@ -1401,10 +1401,11 @@ struct WgradLdsN {
 
 // Buffer-descriptor form of WgradLdsN (same LDS images): 32-bit element offsets advanced by adds
 // (see WgradLdsB).  A piece j: pixel row r, dy column co; B piece j: pixel row r, column n -> tap.
-template <int BM, int BN>
+template <int BM, int BN, int NWV = BN / 64>
 struct WgradLdsNB {
-  using L = WgradLdsN<BM, BN>;
-  static constexpr int PAW = L::PAW, PBW = L::PBW, A_BYTES = L::A_BYTES;
+  using L = WgradLdsN<BM, BN>;  // LDS image layout (row bytes, slots, rows per piece); NWV waves share the pieces
+  static constexpr int PAW = 64 * L::RA / 1024 / NWV, PBW = 64 * L::RB / 1024 / NWV, A_BYTES = L::A_BYTES;
+  static_assert(PAW >= 1 && PBW >= 1 && PAW * NWV * 1024 == A_BYTES, "pieces");
   __amdgpu_buffer_rsrc_t rx, rdy;
   int NP, OW, OH, H, W, S, dyStep, xStep, xWrapOW, xRow, xImg;
   int apix[PAW], adyb[PAW];
@@ -1573,6 +1574,85 @@ __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x,
   __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
   for (int e = threadIdx.x; e < BM * BN; e += BN) {
+    const int row = e / BN, c = e % BN;
+    const int m = m0 + row, n = n0 + c;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+  }
+}
+// Weight-grad v4: 8 waves (BM / 64 x BN / 64, each 64 x 64), BM x BN = 128 x 256 or 256 x 128, a
+// 3-stage LDS-DMA ring (48 KiB stages, one block per CU, 2 waves per SIMD) with a counted
+// vmcnt(pieces per wave) so one stage stays in flight across each barrier -- the forward kernel's
+// structure; the narrow-tile buffer loader with the pieces shared by all 8 waves.
+template <int BM, int BN>
+__global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                     float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn,
+                                                     unsigned xbytes, unsigned dybytes) {
+  constexpr int WM = BM / 64, NS = 3;
+  static_assert(WM * (BN / 64) == 8, "8 waves");
+  using LD = WgradLdsNB<BM, BN, 8>;
+  constexpr int STAGE = WgradLdsN<BM, BN>::STAGE, PER = LD::PAW + LD::PBW;
+  constexpr int CT = BM * (BN + 4) * 4;
+  constexpr int LDSB = NS * STAGE > CT ? NS * STAGE : CT;
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int nk_all = (int)((NP + 63) / 64);
+  const int kt0 = split * kt_per_split;
+  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    LD ld(x, dy, g, m0, n0, kt0, wid, lane, xbytes, dybytes);
+    ld.issue(smem, wid);
+    if (nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) vm_wait<PER>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+      bf16x8 a[2][4], b[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[h][i] = frag_k<BM>(As, wm * 64 + i * 16, h * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[h][j] = frag_k<BN>(Bs, wn * 64 + j * 16, h * 32, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+    }
+  }
+  vm_wait<0>();
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int RS = BN + 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int Ntot = g.KH * g.KW * g.C;
+  for (int e = threadIdx.x; e < BM * BN; e += 512) {
     const int row = e / BN, c = e % BN;
     const int m = m0 + row, n = n0 + c;
     if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
@@ -1839,6 +1919,49 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   return (int)hipGetLastError();
 }
 
+// wgrad v4 tiles (0 = off): 1 = 128 x 256, 2 = 256 x 128, 3 = auto (default): 256 x 128 when K_out >= 256,
+// else the v3 128 x 128 kernel (tools/gpu/ab_conv.sh, profiles/r01/ab_wgrad_v4.log: +7-11 % at K_out >= 256,
+// the 256-row tile is half idle and the 128 x 256 one no faster at K_out = 128)
+inline int wgrad_v4_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_WGRAD_V4");
+    return e ? atoi(e) : 3;
+  }();
+  return t;
+}
+template <int BM, int BN>
+int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int Ntot = g.KH * g.KW * g.C;
+  const int gm = ceil_div(g.K, BM), gn = ceil_div(Ntot, BN);
+  const int nk = ceil_div(NP, 64);
+  const int tiles = gm * gn;
+  int maxs = nk / 8;
+  if (maxs < 1) maxs = 1;
+  int splits = 1;
+  if (wgrad_target() > 0) {
+    splits = (wgrad_target() + tiles / 2) / tiles;
+    if (splits < 1) splits = 1;
+  } else {
+    // launch_wgrad_v3's model with one resident block per CU, twice the tile per K step and atomics
+    const double R = num_cus();
+    double best = 1e300;
+    for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
+      const double blocks = (double)tiles * sp;
+      const double t = ceil(blocks / R) * ceil_div(nk, sp) * 1.9 * 2 * 0.5 + blocks * 0.0504 * 2;
+      if (t < best) { best = t; splits = sp; }
+    }
+  }
+  if (splits > maxs) splits = maxs;
+  const int per = ceil_div(nk, splits);
+  splits = ceil_div(nk, per);
+  const dim3 grid((unsigned)tiles, splits);
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
+  v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  return (int)hipGetLastError();
+}
+
 // narrow layers (K <= 64): BM = 32 / 64 out-channel tiles, BN = 128 / 256 column tiles
 template <int BM, int BN>
 int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
@@ -1902,6 +2025,13 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const int Ntot = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy);
     const int nm = wgrad_narrow_for(g, NP);
+    const int v4 = wgrad_v4_mode();
+    const double xb4 = 2.0 * ((double)g.N * g.H * g.W * g.xps), db4 = 2.0 * ((double)NP * g.yps);
+    if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
+        db4 < (double)v3::kBufOob) {
+      if (v4 == 2 || (v4 == 3 && g.K >= 256)) return launch_wgrad_v4<256, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
+      if (v4 == 1) return launch_wgrad_v4<128, 256>((const bf16*)x, (const bf16*)dy, dw, g, st);
+    }
     if (vec && (g.K > 64 || nm == 2) && Ntot >= 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && nm == 1) {
