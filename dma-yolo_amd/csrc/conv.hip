@@ -22,6 +22,12 @@
 #include <cstdlib>
 #include <cmath>
 
+// s_setprio(1) around the MFMA cluster of the LDS-DMA main loops (cdna_hip_programming.md §5.5 T5);
+// compile-time A/B switch, off unless measured faster
+#ifndef DMY_SETPRIO
+#define DMY_SETPRIO 0
+#endif
+
 namespace {
 
 constexpr int NT = 256;  // 4 waves, 2x2 over the block tile
@@ -926,12 +932,14 @@ DEV void mainloop4(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
     __builtin_amdgcn_sched_barrier(0);
     if (!IF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+    if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -1270,6 +1278,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
       __builtin_amdgcn_sched_barrier(0);
       if (BUF == 1 && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1277,6 +1286,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   } else if (nk > 0) {
     WgradLds<NS> ld(x, dy, g, m0, n0, kt0, wid, lane);
@@ -1630,6 +1640,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
       __builtin_amdgcn_sched_barrier(0);
       if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1637,6 +1648,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   vm_wait<0>();
