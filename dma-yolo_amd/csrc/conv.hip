@@ -169,7 +169,16 @@ struct Geom {
   int K, KH, KW, S, P;  // out channels, kernel, stride, pad
   int OH, OW;           // output spatial
   long xps, yps;        // pixel strides of x and y (elements)
+  int oihw;             // weight-grad: write [K][C][KH][KW] (torch OIHW) instead of the GEMM view [K][KH][KW][C]
+  int zeroed;           // weight-grad: the output is already zero (caller-cleared arena): no memset
 };
+
+// weight-grad GEMM column n = (kh * KW + kw) * C + c -> its offset inside one output row of dw
+DEV long wgrad_col(const Geom& g, int n) {
+  if (!g.oihw) return n;
+  const int taps = g.KH * g.KW;
+  return (long)(n % g.C) * taps + n / g.C;
+}
 
 // parity class of a stride-2 data-grad (blockIdx.y): output pixels with (ih%2, iw%2) == (a, b)
 struct Parity {
@@ -662,10 +671,12 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const T* __restrict__ x,
         ct[(wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r) * RS + wn * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
+  static_assert((NT) % BN == 0, "epilogue column must be fixed per thread");
+  const int c = threadIdx.x % BN, n = n0 + c;
+  const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += NT) {
-    const int row = e / BN, c = e % BN;
-    const int m = m0 + row, n = n0 + c;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+    const int row = e / BN, m = m0 + row;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 
@@ -685,6 +696,35 @@ __global__ void wprep_kernel(const float* __restrict__ w, T* __restrict__ wf, T*
     const float v = c < C ? w[(((long)k * C + c) * KH + kh) * KW + kw] : 0.f;
     if (wf) wf[i] = from_f<T>(v);
     if (wt && c < C) wt[(((long)c * KH + kh) * KW + kw) * K + k] = from_f<T>(v);
+  }
+}
+
+// Stem k6 s2 p2 weights as the equivalent k3 s1 p1 conv over the space-to-depth image (dmy_image_s2d):
+// ws[k][ky][kx][(dy * 2 + dx) * C + c] = w[k][c][2 ky + dy][2 kx + dx], channels [4C, Cs) zero
+template <typename T>
+__global__ void wprep_s2d_kernel(const float* __restrict__ w, T* __restrict__ ws, int K, int C, int Cs) {
+  const long total = (long)K * 9 * Cs;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % Cs);
+    const long t = i / Cs;
+    const int tap = (int)(t % 9), k = (int)(t / 9);
+    const int ky = tap / 3, kx = tap % 3;
+    float v = 0.f;
+    if (ch < 4 * C) {
+      const int q = ch / C, c = ch - q * C;
+      v = w[(((long)k * C + c) * 6 + 2 * ky + (q >> 1)) * 6 + 2 * kx + (q & 1)];
+    }
+    ws[i] = from_f<T>(v);
+  }
+}
+
+// weight-grad of the s2d view [K][3][3][Cs] (GEMM order) -> the stem's OIHW [K][C][6][6] gradient
+__global__ void wgrad_s2d_to_oihw_kernel(const float* __restrict__ src, float* __restrict__ dst, int K, int C, int Cs) {
+  const long total = (long)K * C * 36;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int kw = (int)(i % 6), kh = (int)(i / 6 % 6), c = (int)(i / 36 % C), k = (int)(i / (36L * C));
+    const int tap = (kh >> 1) * 3 + (kw >> 1), q = (kh & 1) * 2 + (kw & 1);
+    dst[i] = src[((long)k * 9 + tap) * Cs + q * C + c];
   }
 }
 
@@ -1326,10 +1366,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
         ct[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
+  static_assert((256) % BN == 0, "epilogue column must be fixed per thread");
+  const int c = threadIdx.x % BN, n = n0 + c;
+  const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += 256) {
-    const int row = e / BN, c = e % BN;
-    const int m = m0 + row, n = n0 + c;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+    const int row = e / BN, m = m0 + row;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 // Narrow-layer weight-grad (out channels <= 64): block tile BM (out channels, 32 or 64) x BN
@@ -1583,10 +1625,12 @@ __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x,
         ct[(i * 16 + 4 * (lane >> 4) + r) * RS + wid * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
+  static_assert((BN) % BN == 0, "epilogue column must be fixed per thread");
+  const int c = threadIdx.x % BN, n = n0 + c;
+  const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += BN) {
-    const int row = e / BN, c = e % BN;
-    const int m = m0 + row, n = n0 + c;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+    const int row = e / BN, m = m0 + row;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 // Weight-grad v4: 8 waves (BM / 64 x BN / 64, each 64 x 64), BM x BN = 128 x 256 or 256 x 128, a
@@ -1664,10 +1708,12 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
         ct[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int Ntot = g.KH * g.KW * g.C;
+  static_assert((512) % BN == 0, "epilogue column must be fixed per thread");
+  const int c = threadIdx.x % BN, n = n0 + c;
+  const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += 512) {
-    const int row = e / BN, c = e % BN;
-    const int m = m0 + row, n = n0 + c;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + n, ct[row * RS + c]);
+    const int row = e / BN, m = m0 + row;
+    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 }  // namespace v3
@@ -1677,6 +1723,7 @@ Geom make_geom(int N, int H, int W, int C, long xps, int K, int KH, int KW, int 
   Geom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.KH = KH; g.KW = KW; g.S = S; g.P = P;
   g.OH = OH; g.OW = OW; g.xps = xps; g.yps = yps;
+  g.oihw = 0; g.zeroed = 0;
   return g;
 }
 
@@ -1738,7 +1785,7 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
   const dim3 grid((unsigned)gm * gn, splits);
   const bool va = g.K % VW == 0 && g.yps % VW == 0 && aligned16(dy);
   const bool vb = g.C % VW == 0 && g.xps % VW == 0 && aligned16(x);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   if (va && vb) conv_wgrad_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
   else if (va) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
   else if (vb) conv_wgrad_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
@@ -1913,7 +1960,7 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)gm * gn, splits);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   const bool buf = conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
   static const int ns3 = [] {
@@ -1968,7 +2015,7 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, const Geom& g, hip
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)tiles, splits);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   return (int)hipGetLastError();
@@ -2003,7 +2050,7 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hi
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)tiles, splits);
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
+  if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   constexpr int NS = 3 * v3::WgradLdsN<BM, BN>::STAGE <= 80 * 1024 ? 3 : 2;  // keep 2 blocks per CU
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   if (conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob)
@@ -2061,6 +2108,11 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
 }  // namespace
 
 // ================================================================ C ABI (include/dmayolo.h)
+#define DMY_WGRAD_OIHW 1
+#define DMY_WGRAD_ZEROED 2
+DMY_API int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C,
+                              long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, int flags,
+                              void* stream);
 // BN partial rows of the forward epilogue: 2 per 128 (big tile) or 64 rows of M.  The v3 kernel's
 // 64-row wave rows number the same way (wave row wm of 256-row tile tm = row 4 tm + wm).
 DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile(M, K) ? 128 : 64); }
@@ -2086,9 +2138,17 @@ DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
 
 DMY_API int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C,
                            long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream) {
+  return dmy_conv_wgrad_ex(dtype, x, dy, dw_ohwi, N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps, 0, stream);
+}
+
+DMY_API int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C,
+                              long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, int flags,
+                              void* stream) {
   Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  return dtype ? conv_wgrad_t<bf16>(x, dy, dw_ohwi, g, (hipStream_t)stream)
-               : conv_wgrad_t<float>(x, dy, dw_ohwi, g, (hipStream_t)stream);
+  g.oihw = flags & DMY_WGRAD_OIHW ? 1 : 0;
+  g.zeroed = flags & DMY_WGRAD_ZEROED ? 1 : 0;
+  return dtype ? conv_wgrad_t<bf16>(x, dy, dw, g, (hipStream_t)stream)
+               : conv_wgrad_t<float>(x, dy, dw, g, (hipStream_t)stream);
 }
 
 DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH,
@@ -2097,6 +2157,19 @@ DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w
   const int grid = grid_cap(ceil_div(total, 256), 1024);
   if (dtype) wprep_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (bf16*)w_ohwi, (bf16*)w_ihwo, K, C, Cp, KH, KW);
   else wprep_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (float*)w_ohwi, (float*)w_ihwo, K, C, Cp, KH, KW);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_conv_wprep_s2d(int dtype, const float* w_oihw, void* w_s2d, int K, int C, int Cs, void* stream) {
+  const int grid = grid_cap(ceil_div((long)K * 9 * Cs, 256), 1024);
+  if (dtype) wprep_s2d_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (bf16*)w_s2d, K, C, Cs);
+  else wprep_s2d_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (float*)w_s2d, K, C, Cs);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_conv_wgrad_s2d_to_oihw(const float* dw_s2d, float* dw_oihw, int K, int C, int Cs, void* stream) {
+  wgrad_s2d_to_oihw_kernel<<<grid_cap(ceil_div((long)K * C * 36, 256), 1024), 256, 0, (hipStream_t)stream>>>(
+      dw_s2d, dw_oihw, K, C, Cs);
   return (int)hipGetLastError();
 }
 

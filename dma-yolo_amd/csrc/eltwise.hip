@@ -1297,6 +1297,54 @@ DMY_API int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh,
   DISPATCH_T(dtype, ca_apply_bwd_att_kernel<T><<<egrid((long)N * (H + W) * C), 256, 0, st>>>((const T*)x, xps, (const T*)lh, (const T*)lw, (const T*)dout, dps, (T*)dlh, (T*)dlw, N, H, W, C));
   return (int)hipGetLastError();
 }
+// NCHW image (uint8 or fp32, H and W even) -> space-to-depth NHWC [N][H/2][W/2][Cs] T, channel
+// (dy * 2 + dx) * C + c = x[c][2 oy + dy][2 ox + dx] * scale, channels [4C, Cs) zero.  The k6 s2 p2 stem
+// conv (models/common.py:50-77 with yolov5*.yaml layer 0 args [64, 6, 2, 2]) over x equals a k3 s1 p1
+// conv over this tensor (DESIGN.md §3.1 "stem"): half the stem's input bytes of the 8-channel padded
+// layout and a dense 3x3 contraction instead of a stride-2 6x6 gather.
+template <typename S, typename T>
+__global__ void image_s2d_kernel(const S* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W, int Cs,
+                                 float scale) {
+  constexpr int VW = Traits<T>::VW;
+  const int H2 = H >> 1, W2 = W >> 1;
+  const long HW = (long)H * W, total = (long)N * H2 * W2;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % W2);
+    const long t = i / W2;
+    const int oy = (int)(t % H2);
+    const long b = t / H2;
+    const S* src = x + b * C * HW + (long)(2 * oy) * W + 2 * ox;
+    T* dst = y + i * Cs;
+    for (int c0 = 0; c0 < Cs; c0 += VW) {
+      float f[VW];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const int ch = c0 + j;
+        if (ch < 4 * C) {
+          const int q = ch / C, c = ch - q * C;  // q = dy * 2 + dx
+          f[j] = (float)src[(long)c * HW + (q >> 1) * W + (q & 1)] * scale;
+        } else {
+          f[j] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(dst + c0) = pack<T>(f);
+    }
+  }
+}
+
+DMY_API int dmy_image_s2d(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cs,
+                          float scale, void* stream) {
+  const int VW = dtype ? 8 : 4;
+  if ((H | W) & 1 || Cs % VW || Cs < 4 * C || (((uintptr_t)y) & 15)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)N * (H / 2) * (W / 2);
+  if (src_kind == 0) {
+    DISPATCH_T(dtype, image_s2d_kernel<uint8_t, T><<<egrid(n), 256, 0, st>>>((const uint8_t*)x, (T*)y, N, C, H, W, Cs, scale));
+  } else {
+    DISPATCH_T(dtype, image_s2d_kernel<float, T><<<egrid(n), 256, 0, st>>>((const float*)x, (T*)y, N, C, H, W, Cs, scale));
+  }
+  return (int)hipGetLastError();
+}
 // src_kind: 0 = uint8, 1 = fp32; output NHWC with pixel stride Cp >= C (zero-filled tail channels)
 DMY_API int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cp,
                              float scale, void* stream) {

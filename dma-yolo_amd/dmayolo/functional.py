@@ -105,6 +105,43 @@ def sink_result(sink, buf):
 
 # ------------------------------------------------------------------ convolution (+BN +act)
 
+WGRAD_OIHW, WGRAD_ZEROED = 1, 2  # dmy_conv_wgrad_ex flags
+
+
+class WgradArena:
+    """Per-training-forward fp32 buffer holding every conv / linear weight gradient of a Model in
+    torch OIHW order.  Model.forward clears it with ONE fill; each weight-grad launch then
+    accumulates straight into its slice (no per-launch memset, no layout pass), and the slice is
+    handed to autograd as the parameter's gradient.  A new buffer per forward, so the previous
+    step's .grad views are never overwritten (gradient accumulation stays correct); a weight used
+    twice in one forward gets a fresh tensor the second time."""
+    current = None
+    ALIGN = 64  # elements (256 B): slices stay 16-B aligned for the vectorised optimizer kernels
+
+    def __init__(self, buf, offsets):
+        self.buf, self.offsets, self.taken = buf, offsets, set()
+
+    @classmethod
+    def layout(cls, params):
+        """data_ptr -> (offset, numel) for every weight with dim >= 2; total size"""
+        offs, n = {}, 0
+        for q in params:
+            if q.dim() >= 2 and q.dtype == torch.float32 and q.requires_grad:
+                offs[q.data_ptr()] = (n, q.numel())
+                n += -(-q.numel() // cls.ALIGN) * cls.ALIGN
+        return offs, n
+
+    def take(self, key, shape):
+        o = self.offsets.get(key)
+        numel = 1
+        for d in shape:
+            numel *= d
+        if o is None or o[1] != numel or key in self.taken:
+            return None
+        self.taken.add(key)
+        return self.buf[o[0]:o[0] + numel].view(shape)
+
+
 class ConvSpec:
     """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None)."""
     __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache')
@@ -176,37 +213,60 @@ class KernelTimer:
         return {k: dict(launches=v[0], flops=v[1], seconds=v[2], bytes=v[3]) for k, v in out.items()}
 
 
-def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW):
+def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka):
+    """(k, s, p) and x's shape are the launch geometry; Ca / ka the layer's real input channels and kernel
+    (they differ for the space-to-depth stem and the channel-padded stem), used for the flop / byte count"""
     N, C, H, W = x.shape
     es = x.element_size()
-    KernelTimer.run('conv_fwd', 2.0 * N * OH * OW * K * C * k * k, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf),
+    Hi, Wi = (2 * H, 2 * W) if ka != k else (H, W)
+    KernelTimer.run('conv_fwd', 2.0 * N * OH * OW * K * Ca * ka * ka, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf),
                     ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(),
-                    tag=(N, C, H, W, K, k, s), nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
+                    tag=(N, Ca, Hi, Wi, K, ka, s if ka == k else 2),
+                    nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
 
 
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None):
-        cpad = zero_padded_channels(x)
-        x, xps = pixel_stride(x)
-        N, C, H, W = x.shape
+        s2d = getattr(x, '_dmy_s2d', 0)
         K, C2, k, _ = weight.shape
-        assert C2 == C, (C2, C)
-        # stem: read the zero-padded storage as Cp channels (16-byte vectors) with zero weights
-        Cp = cpad if (cpad and C % VW[x.dtype] and xps >= cpad) else C
-        s, p = spec.stride, spec.pad
-        OH, OW = conv_out_hw(H, W, k, s, p)
-        dev, dt = x.device, x.dtype
-        need_grad = any(ctx.needs_input_grad[:6])
-        if not need_grad and not torch.is_grad_enabled() and spec.wcache is not None and \
-                spec.wcache[0] == (weight.data_ptr(), weight._version, dt):
-            wf, wt = spec.wcache[1], None
+        ctx.s2d = 0
+        if s2d:
+            # stem over the space-to-depth image (image_s2d): the k6 s2 p2 conv runs as k3 s1 p1 over Cs channels
+            assert C2 == s2d and k == 6 and spec.stride == 2 and spec.pad == 2, 's2d input feeds only the k6 s2 p2 stem'
+            x, xps = pixel_stride(x)
+            N, Cs, H2, W2 = x.shape
+            C, H, W = s2d, 2 * H2, 2 * W2
+            OH, OW = H2, W2
+            wf = torch.empty((K, 9 * Cs), dtype=x.dtype, device=x.device)
+            call('dmy_conv_wprep_s2d', DT[x.dtype], ptr(weight.detach().contiguous()), ptr(wf), K, C, Cs, stream())
+            wt = None
+            ctx.s2d = Cs
+            # from here on the launch geometry is the k3 s1 p1 view
+            Cg, Hg, Wg, kg, sg, pg = Cs, H2, W2, 3, 1, 1
+            Cp = C
         else:
-            wf, wt = prep_weight(weight, dt, need_grad and Cp == C, Cp)
-            if not need_grad:
-                spec.wcache = ((weight.data_ptr(), weight._version, dt), wf)
-        if Cp != C:
-            x = x.as_strided((N, Cp, H, W), x.stride())
+            cpad = zero_padded_channels(x)
+            x, xps = pixel_stride(x)
+            N, C, H, W = x.shape
+            assert C2 == C, (C2, C)
+            # stem: read the zero-padded storage as Cp channels (16-byte vectors) with zero weights
+            Cp = cpad if (cpad and C % VW[x.dtype] and xps >= cpad) else C
+            OH, OW = conv_out_hw(H, W, k, spec.stride, spec.pad)
+            need_grad = any(ctx.needs_input_grad[:6])
+            dt = x.dtype
+            if not need_grad and not torch.is_grad_enabled() and spec.wcache is not None and \
+                    spec.wcache[0] == (weight.data_ptr(), weight._version, dt):
+                wf, wt = spec.wcache[1], None
+            else:
+                wf, wt = prep_weight(weight, dt, need_grad and Cp == C, Cp)
+                if not need_grad:
+                    spec.wcache = ((weight.data_ptr(), weight._version, dt), wf)
+            if Cp != C:
+                x = x.as_strided((N, Cp, H, W), x.stride())
+            Cg, Hg, Wg, kg, sg, pg = Cp, H, W, k, spec.stride, spec.pad
+        s, p = spec.stride, spec.pad
+        dev, dt = x.device, x.dtype
         M = N * OH * OW
         z = new_act(N, K, OH, OW, x)
         bn = spec.bn
@@ -220,7 +280,7 @@ class ConvBNActFn(torch.autograd.Function):
             if train_bn:
                 P = call('dmy_conv_fwd_partial_rows', M, K)
                 psum, psq = f32(P * K, dev), f32(P * K, dev)
-                _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, k, s, p, OH, OW)
+                _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, kg, sg, pg, OH, OW, C, k)
                 if P > 256:  # two-stage column reduction of the epilogue partials
                     S = call('dmy_colsum2_rows', P)
                     ps2, pq2 = f32(S * K, dev), f32(S * K, dev)
@@ -233,7 +293,7 @@ class ConvBNActFn(torch.autograd.Function):
                      ptr(bn.num_batches_tracked) if upd else None, float(mom), float(bn.eps), upd,
                      ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
             else:
-                _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, k, s, p, OH, OW)
+                _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k)
                 call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
                      float(bn.eps), K, ptr(scale), ptr(shift), stream())
             y = new_act(N, K, OH, OW, x)
@@ -241,7 +301,7 @@ class ConvBNActFn(torch.autograd.Function):
                  M, K, stream())
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
         else:
-            _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, k, s, p, OH, OW)
+            _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k)
             if spec.act != ACT_NONE or res is not None:
                 y = new_act(N, K, OH, OW, x)
                 one, zero = torch.ones(K, device=dev), torch.zeros(K, device=dev)
@@ -252,9 +312,12 @@ class ConvBNActFn(torch.autograd.Function):
             ctx.save_for_backward(x, wt, z)
         ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
+        ctx.ggeom = (Hg, Wg, kg, sg, pg)
         ctx.cp = Cp
         ctx.has_bias = bias is not None
         ctx.xsink, ctx.rsink = xsink, rsink
+        ctx.arena = WgradArena.current
+        ctx.wkey = weight.data_ptr()
         return y
 
     @staticmethod
@@ -307,20 +370,42 @@ class ConvBNActFn(torch.autograd.Function):
         dx = dw = None
         Cp = ctx.cp
         if ctx.needs_input_grad[0]:
-            if Cp != C:
+            if Cp != C or ctx.s2d:
                 raise NotImplementedError('input gradient of a channel-padded stem conv')
             buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
             KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf),
                             acc, N, H, W, C, bps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
                             nbytes=z.element_size() * (M * K + K * C * k * k + (1 + acc) * N * H * W * C))
             dx = sink_result(ctx.xsink, buf)
-        if ctx.needs_input_grad[1]:
-            dwo = f32(K * Cp * k * k, dev)
+        if ctx.needs_input_grad[1] and ctx.s2d:
+            Cs = ctx.s2d
+            H2, W2 = ctx.ggeom[:2]
+            dwo = f32(K * 9 * Cs, dev)
             KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
-                            H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
-                            nbytes=z.element_size() * (N * H * W * Cp + M * K) + 4 * K * Cp * k * k)
-            dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
-            call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
+                            H2, W2, Cs, xps, K, 3, 3, 1, 1, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
+                            nbytes=z.element_size() * (N * H2 * W2 * Cs + M * K) + 4 * K * Cs * 9)
+            dw = ctx.arena.take(ctx.wkey, (K, C, k, k)) if ctx.arena is not None else None
+            if dw is None:
+                dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
+            call('dmy_conv_wgrad_s2d_to_oihw', ptr(dwo), ptr(dw), K, C, Cs, stream())
+        elif ctx.needs_input_grad[1]:
+            wkw = dict(tag=(N, C, H, W, K, k, s), nbytes=z.element_size() * (N * H * W * Cp + M * K) + 4 * K * Cp * k * k)
+            dw = ctx.arena.take(ctx.wkey, (K, C, k, k)) if ctx.arena is not None else None
+            zeroed = dw is not None
+            if dw is None:
+                dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
+            if k == 1 and Cp == C:
+                # 1x1: the GEMM view IS torch OIHW -> accumulate straight into the step's zeroed arena slice
+                flags = WGRAD_OIHW | (WGRAD_ZEROED if zeroed else 0)
+                KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad_ex', dt, ptr(x), ptr(dz),
+                                ptr(dw), N, H, W, C, xps, K, k, k, s, p, OH, OW, dzps, flags, stream(), **wkw)
+            else:
+                # k > 1: OIHW-order atomics would scatter every tile row with stride k*k (measured 1.5x slower
+                # weight-grad on yolov5s); accumulate in GEMM order, then one layout pass (drops stem padding)
+                dwo = f32(K * Cp * k * k, dev)
+                KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz),
+                                ptr(dwo), N, H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), **wkw)
+                call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
         dres = None
         if ctx.has_res:
             dres = dy if ctx.rsink is None else ctx.rsink.passthrough(dy)
@@ -566,6 +651,22 @@ class AddFn(torch.autograd.Function):
     def backward(ctx, dy):
         da = dy if ctx.asink is None else ctx.asink.passthrough(dy)
         return da, dy, None
+
+
+def image_s2d(x, dtype):
+    """NCHW image (uint8 -> /255, or float) -> space-to-depth NHWC storage [N, Cs, H/2, W/2] for the k6 s2 p2
+    stem (csrc dmy_image_s2d); the result carries `_dmy_s2d` = C, read by ConvBNActFn.  No gradient."""
+    N, C, H, W = x.shape
+    Cs = -(-4 * C // VW[dtype]) * VW[dtype]
+    buf = torch.empty((N, Cs, H // 2, W // 2), dtype=dtype, device=x.device, memory_format=CL)
+    xc = x.detach().contiguous()
+    if x.dtype == torch.uint8:
+        call('dmy_image_s2d', DT[dtype], 0, ptr(xc), ptr(buf), N, C, H, W, Cs, 1.0 / 255.0, stream())
+    else:
+        xf = xc if xc.dtype == torch.float32 else xc.float()
+        call('dmy_image_s2d', DT[dtype], 1, ptr(xf), ptr(buf), N, C, H, W, Cs, 1.0, stream())
+    buf._dmy_s2d = C
+    return buf
 
 
 class ToNHWC(torch.autograd.Function):

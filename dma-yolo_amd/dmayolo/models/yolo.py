@@ -162,22 +162,51 @@ class Model(nn.Module):
             raise NotImplementedError('test-time augmentation is outside the DMA-YOLO hot path')
         return self._forward_once(x)
 
+    def _s2d_stem(self, x):
+        """layer 0 is the k6 s2 p2 stem Conv (every yolov5* / DMA-YOLO yaml) and the image allows the
+        space-to-depth form (even H, W; no input gradient)"""
+        m0 = self.model[0]
+        if type(m0) is not Conv or x.dim() != 4 or x.requires_grad or x.shape[2] % 2 or x.shape[3] % 2:
+            return False
+        c = m0.conv
+        return (c.kernel_size == (6, 6) and c.stride == (2, 2) and c.padding == (2, 2) and c.in_channels == x.shape[1]
+                and c.groups == 1 and getattr(self, 's2d_stem', True))
+
     def to_input(self, x):
-        """uint8/float NCHW image batch -> NHWC act_dtype (train.py:402 `/255` for uint8)."""
+        """uint8/float NCHW image batch -> NHWC act_dtype (train.py:402 `/255` for uint8).  With the k6 s2 p2
+        stem the image is stored space-to-depth (Fn.image_s2d) and the stem runs as a k3 s1 p1 conv."""
         if x.dtype == self.act_dtype and x.dim() == 4 and (x.shape[1] == 1 or x.stride(1) == 1):
             return x
+        if x.is_cuda and self._s2d_stem(x):
+            return Fn.image_s2d(x, self.act_dtype)
         y = Fn.ToNHWC.apply(x, self.act_dtype)
         y._dmy_cpad = -(-x.shape[1] // Fn.VW[self.act_dtype]) * Fn.VW[self.act_dtype]  # zero-padded channels
         return y
 
+    def _wgrad_arena(self):
+        """Fresh zeroed weight-gradient arena for this training forward (functional.WgradArena)."""
+        lay = getattr(self, '_arena_layout', None)
+        first = next(self.parameters())
+        if lay is None or lay[0] != (first.data_ptr(), first.device):
+            offs, n = Fn.WgradArena.layout(self.parameters())
+            lay = self._arena_layout = ((first.data_ptr(), first.device), offs, n)
+        return Fn.WgradArena(torch.zeros(lay[2], dtype=torch.float32, device=first.device), lay[1])
+
     def _forward_once(self, x, profile=False, visualize=False):
         x = self.to_input(x)
         y = []
-        for m in self.model:
-            if m.f != -1:
-                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
-            x = m(x)
-            y.append(x if m.i in self.save else None)
+        arena = self.training and torch.is_grad_enabled() and x.is_cuda
+        prev = Fn.WgradArena.current
+        if arena:
+            Fn.WgradArena.current = self._wgrad_arena()
+        try:
+            for m in self.model:
+                if m.f != -1:
+                    x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+                x = m(x)
+                y.append(x if m.i in self.save else None)
+        finally:
+            Fn.WgradArena.current = prev
         return x
 
     def _initialize_biases(self, cf=None):

@@ -31,9 +31,17 @@ int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int 
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
                    int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
+/* flags: 1 = write dw in torch OIHW order (the parameter's .grad layout, no wgrad_to_oihw pass; needs Cp == C),
+ *        2 = dw is already zero (a per-step gradient arena cleared once), skip the memset.  Same sums as above. */
+int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C, long xps, int K,
+                      int KH, int KW, int S, int P, int OH, int OW, long yps, int flags, void* stream);
 /* Cp >= C: input channels zero-padded to a full 16-byte vector (the 3-channel stem, yaml:15) */
 int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH, int KW,
                    void* stream);
+/* Stem as space-to-depth (yolov5*.yaml / DMA-YOLO yaml layer 0: Conv(3, c2, 6, 2, 2), models/common.py:50-77):
+ * the k6 s2 p2 conv over x == a k3 s1 p1 conv over dmy_image_s2d(x) with these weights (Cs >= 4C channels). */
+int dmy_conv_wprep_s2d(int dtype, const float* w_oihw, void* w_s2d, int K, int C, int Cs, void* stream);
+int dmy_conv_wgrad_s2d_to_oihw(const float* dw_s2d, float* dw_oihw, int K, int C, int Cs, void* stream);
 int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int Cp, int KH, int KW, void* stream);
 
 /* ---- BatchNorm2d + activation: replaces nn.BatchNorm2d/nn.SiLU/nn.Hardswish in models/common.py:68-73,
@@ -99,6 +107,10 @@ int dmy_ca_apply_fwd(int dtype, const void* x, long xps, const void* lh, const v
 int dmy_ca_apply_bwd(int dtype, const void* x, long xps, const void* lh, const void* lw, const void* dout, long dps,
                      void* dx, long dxps, void* dlh, void* dlw, int N, int H, int W, int C, void* stream);
 /* input normalisation imgs.float()/255 (train.py:402) + layout changes */
+/* NCHW image (uint8 / fp32, even H, W) -> space-to-depth NHWC [N][H/2][W/2][Cs], channel (dy*2+dx)*C+c,
+ * times scale (train.py:402 `/255`); the stem conv's input in its k3 s1 form */
+int dmy_image_s2d(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cs, float scale,
+                  void* stream);
 int dmy_nchw_to_nhwc(int dtype, int src_kind, const void* x, void* y, int N, int C, int H, int W, int Cp, float scale,
                      void* stream);
 int dmy_nhwc_to_nchw_f32(int dtype, const void* x, long xps, float* y, int N, int C, int H, int W, void* stream);

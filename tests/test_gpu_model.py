@@ -1,11 +1,14 @@
 """GPU parity of whole models (product Model/parse_model) against golden vectors captured from
 the reference: train-mode outputs, parameter gradients, eval-mode decoded predictions."""
+import os
+
 import pytest
 import torch
 
 from golden_util import Fixture, load_sd
 
 pytestmark = pytest.mark.gpu
+CFG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'dma-yolo_amd', 'dmayolo', 'configs')
 
 
 def _model(fx, dtype=torch.float32):
@@ -24,6 +27,12 @@ def _model(fx, dtype=torch.float32):
 def test_model_train_eval_fp32(name):
     fx = Fixture(name)
     m = _model(fx)
+    if name == 'model_c5':
+        # config 5's CBAM channel-max / SPP max-pool argmaxes sit on near-ties at this fixture: the s2d stem's
+        # different fp32 summation order (layer-0 output within 5e-7 relative, tools/gpu/s2d_check4.py) flips a
+        # few of them and reroutes C3TR gradients.  Pin c5 with the direct stem; s2d is pinned on v5s / dma
+        # here and against the direct stem in test_s2d_stem_matches_strided_stem.
+        m.s2d_stem = False
     x = fx.t('in.0').cuda()
     m.train()
     outs = m(x)
@@ -58,3 +67,33 @@ def test_model_bf16_close_to_fp32():
         z16, _ = m16(x)
     err = (z16 - z32).abs().max() / z32.abs().max()
     assert float(err) < 2e-2, float(err)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_s2d_stem_matches_strided_stem(dtype):
+    """The space-to-depth stem (image_s2d + k3 s1 p1 over Cs channels) against the direct k6 s2 p2 stem over
+    the channel-padded image: layer-0 output, stem weight gradient and BN gradients (uint8 input as train.py)."""
+    from dmayolo.models.yolo import Model
+    import dmayolo.functional as Fn
+    torch.manual_seed(0)
+    ms = []
+    for s2d in (True, False):
+        torch.manual_seed(0)
+        m = Model(os.path.join(CFG, 'yolov5n.yaml'), nc=10, act_dtype=dtype).cuda().train()
+        m.s2d_stem = s2d
+        ms.append(m)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 256, (2, 3, 96, 160), generator=g, dtype=torch.uint8).cuda()
+    assert Fn.image_s2d(x, dtype)._dmy_s2d == 3
+    outs, grads = [], []
+    for m in ms:
+        y0 = m.model[0](m.to_input(x))
+        gup = torch.randn(y0.shape, generator=torch.Generator().manual_seed(2)).to(y0.device)
+        (y0.float() * gup).sum().backward()
+        outs.append(y0.float())
+        grads.append([m.model[0].conv.weight.grad.clone(), m.model[0].bn.weight.grad.clone()])
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs[0], outs[1], **tol)
+    for a, b in zip(grads[0], grads[1]):
+        scale = float(b.abs().max())
+        torch.testing.assert_close(a, b, rtol=tol['rtol'] * 5, atol=tol['atol'] * 5 * max(1.0, scale))
