@@ -90,6 +90,8 @@ SIGNATURES = {
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
     'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P],
+    # metrics.hip
+    'dmy_process_batch': [P, P, P, P, I, P, I, P, P, P, P, P],
     # swin.hip
     'dmy_layernorm_fwd': [I, P, L, P, P, P, P, P, L, I, F, P],
     'dmy_layernorm_bwd_blocks': [L],

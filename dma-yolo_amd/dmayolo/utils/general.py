@@ -32,6 +32,29 @@ def xyxy2xywh(x):
     return y
 
 
+def clip_coords(boxes, shape):
+    """utils/general.py:620-630 (tensor branch): clamp xyxy boxes to (height, width) in place."""
+    boxes[:, 0].clamp_(0, shape[1])
+    boxes[:, 1].clamp_(0, shape[0])
+    boxes[:, 2].clamp_(0, shape[1])
+    boxes[:, 3].clamp_(0, shape[0])
+
+
+def scale_coords(img1_shape, coords, img0_shape, ratio_pad=None):
+    """utils/general.py:605-617: xyxy coords from the letterboxed img1_shape back to img0_shape, in place."""
+    if ratio_pad is None:
+        gain = min(img1_shape[0] / img0_shape[0], img1_shape[1] / img0_shape[1])
+        pad = (img1_shape[1] - img0_shape[1] * gain) / 2, (img1_shape[0] - img0_shape[0] * gain) / 2
+    else:
+        gain = ratio_pad[0][0]
+        pad = ratio_pad[1]
+    coords[:, [0, 2]] -= pad[0]
+    coords[:, [1, 3]] -= pad[1]
+    coords[:, :4] /= gain
+    clip_coords(coords, img0_shape)
+    return coords
+
+
 def _pow2(n, lo=2048):
     c = lo
     while c < n:

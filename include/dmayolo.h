@@ -220,6 +220,14 @@ int dmy_mha_bwd(int dtype, const void* q, long qps, const void* k, long kps, con
 int dmy_dropout(int dtype, const void* x, long xps, void* y, long yps, long M, int C, float p, unsigned long long seed,
                 void* stream);
 
+/* ---- validation matching: replaces process_batch (val.py:62-83) with box_iou (utils/metrics.py:254-276) for
+ *      a batch of images in one launch.  det [ND][6] (x1 y1 x2 y2 conf cls), lab [NL][5] (cls x1 y1 x2 y2),
+ *      det_off / lab_off [B + 1] per-image row offsets, iouv [T]; workspaces ws_* of ND entries;
+ *      correct [ND][T] (0/1).  Matching rules: csrc/metrics.hip header. */
+int dmy_process_batch(const float* det, const int* det_off, const float* lab, const int* lab_off, int B,
+                      const float* iouv, int T, int* ws_lab, float* ws_iou, int* ws_win, unsigned char* correct,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif
