@@ -139,6 +139,7 @@ def main():
     from dmayolo.optim import build_optimizer
     from dmayolo.synthetic import images, targets, clustered_predictions
     from dmayolo.utils.loss import ComputeLoss
+    from dmayolo.infer import GraphedDetector
     from dmayolo.utils.general import non_max_suppression
     from dmayolo.utils.torch_utils import ModelEMA
 
@@ -214,17 +215,24 @@ def main():
         # detect p50 (detect.py:175-243): bs1 uint8 on device -> forward -> NMS(0.25, 0.45, max_det 1000)
         model.eval()
         x1 = images(1, img, seed=3, device=device)
-        lat = []
-        with torch.no_grad():
-            for i in range(60):
+        graphed = GraphedDetector(model)
+
+        def p50(fwd, n=60):
+            lat = []
+            for i in range(n):
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
-                z, _ = model(x1)
+                z, _ = fwd(x1)
                 non_max_suppression(z, 0.25, 0.45, max_det=1000)
                 torch.cuda.synchronize()
                 lat.append(time.perf_counter() - t1)
             lat = sorted(lat[10:])
-            extra['detect_p50_ms'] = round(lat[len(lat) // 2] * 1e3, 3)
+            return z, round(lat[len(lat) // 2] * 1e3, 3)
+
+        with torch.no_grad():
+            z, extra['detect_eager_p50_ms'] = p50(model)
+            zg, extra['detect_p50_ms'] = p50(graphed)  # HIP-graph replay of the forward + NMS (infer.py)
+            assert torch.equal(z, zg), 'graph replay differs from the eager forward'
             A = z.shape[1]
             sp = clustered_predictions(1, A, nc, device=device)
             nl = []

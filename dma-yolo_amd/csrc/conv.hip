@@ -173,6 +173,39 @@ struct Geom {
   int zeroed;           // weight-grad: the output is already zero (caller-cleared arena): no memset
 };
 
+// Inference epilogue (eval BatchNorm folded per channel + activation + residual, applied to the T-rounded
+// conv output exactly as dmy_bn_act_fwd would read it back): y = act(z * scale + shift) (+ res).
+// scale / shift may be null (1 / 0).  `on` = 0 leaves the plain (+bias) store.
+struct Epi {
+  const float* scale;
+  const float* shift;
+  const void* res;
+  long rps;
+  int act;
+  int on;
+};
+
+template <typename T, int VW>
+DEV void epi_store(const Epi& ep, const T* src, T* dst, int n, int K, long m, bool full) {
+  float f[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    if (n + j < K) {
+      const float sc = ep.scale ? ep.scale[n + j] : 1.f, sh = ep.shift ? ep.shift[n + j] : 0.f;
+      float v = act_fwd(ep.act, to_f(src[j]) * sc + sh);
+      if (ep.res) v += to_f(reinterpret_cast<const T*>(ep.res)[m * ep.rps + n + j]);
+      f[j] = v;
+    } else {
+      f[j] = 0.f;
+    }
+  }
+  if (full) {
+    *reinterpret_cast<uint4*>(dst) = pack<T>(f);
+  } else {
+    for (int j = 0; j < VW && n + j < K; ++j) dst[j] = from_f<T>(f[j]);
+  }
+}
+
 // weight-grad GEMM column n = (kh * KW + kw) * C + c -> its offset inside one output row of dw
 DEV long wgrad_col(const Geom& g, int n) {
   if (!g.oihw) return n;
@@ -526,7 +559,7 @@ template <typename T, int BM, int BN, bool VEC, bool P1>
 __global__ void __launch_bounds__(NT) conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
                                                       const float* __restrict__ bias, T* __restrict__ y,
                                                       float* __restrict__ psum, float* __restrict__ psq, Geom g,
-                                                      int gm, int gn) {
+                                                      int gm, int gn, Epi ep) {
   using TT = Tile<T, BM, BN, false, false>;
   __shared__ __attribute__((aligned(16))) char smem[TT::LDS_BYTES];
   T* lds = reinterpret_cast<T*>(smem);
@@ -570,6 +603,10 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const T* __restrict__ x, c
     const int n = n0 + cv * VW;
     if (m >= M || n >= g.K) continue;
     const T* src = lds + row * RS + cv * VW;
+    if (ep.on) {
+      epi_store<T, VW>(ep, src, y + m * g.yps + n, n, g.K, m, vec && n + VW <= g.K);
+      continue;
+    }
     if (vec && n + VW <= g.K) {
       *reinterpret_cast<uint4*>(y + m * g.yps + n) = *reinterpret_cast<const uint4*>(src);
     } else {
@@ -1019,7 +1056,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
                                                             float* __restrict__ psum, float* __restrict__ psq,
                                                             int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                            unsigned wbytes, S2Cls cls) {
+                                                            unsigned wbytes, S2Cls cls, Epi ep) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1113,6 +1150,10 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
       pix = ((long)bb * cls.HX + 2 * i2 + cls.a) * cls.WX + 2 * j2 + cls.b;
     }
     uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + n);
+    if (!DG && ep.on) {
+      epi_store<bf16, 8>(ep, ct + row * RS + cv * 8, y + pix * g.yps + n, n, g.K, pix, true);
+      continue;
+    }
     if (accumulate) {
       float a[8], b[8];
       unpack<bf16>(v, a);
@@ -1733,17 +1774,18 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool big_tile(long M, int N) { return M >= 4096 && N > 64; }
 
 template <typename T, int BM, int BN>
-int launch_fwd(const T* x, const T* w, const float* b, T* y, float* ps, float* pq, const Geom& g, hipStream_t st) {
+int launch_fwd(const T* x, const T* w, const float* b, T* y, float* ps, float* pq, const Geom& g, hipStream_t st,
+               const Epi& ep = Epi{}) {
   constexpr int VW = Traits<T>::VW;
   const long M = (long)g.N * g.OH * g.OW;
   const int gm = ceil_div(M, BM), gn = ceil_div(g.K, BN);
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
   const bool vec = g.C % VW == 0 && g.xps % VW == 0 && aligned16(x);
   const unsigned grid = (unsigned)gm * gn;
-  if (vec && p1) conv_fwd_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
-  else if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
-  else if (p1) conv_fwd_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
-  else conv_fwd_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn);
+  if (vec && p1) conv_fwd_kernel<T, BM, BN, true, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn, ep);
+  else if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn, ep);
+  else if (p1) conv_fwd_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn, ep);
+  else conv_fwd_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, w, b, y, ps, pq, g, gm, gn, ep);
   return (int)hipGetLastError();
 }
 
@@ -1821,7 +1863,7 @@ inline int p1_tile_mode() {
 
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-              hipStream_t st) {
+              hipStream_t st, const Epi& ep = Epi{}) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
@@ -1830,7 +1872,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const unsigned xbytes = buf ? (unsigned)xb : 0u, wbytes = buf ? (unsigned)wb : 0u;
 #define V3_GO(BM, BN, NS, P1_, BUF_)                                                                          \
   v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
-                                                                          wbytes, v3::S2Cls{0, 0, 0, 0})
+                                                                          wbytes, v3::S2Cls{0, 0, 0, 0}, ep)
 #define V3_LAUNCH(BM, BN, NS)                                \
   {                                                          \
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN); \
@@ -1857,15 +1899,16 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
 }
 
 template <typename T>
-int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st) {
+int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
+               const Epi& ep = Epi{}) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
-    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M))
-      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st);
+    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
+      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
   }
   if (big_tile(M, g.K))
-    return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
-  return launch_fwd<T, 64, 64>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st);
+    return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
+  return launch_fwd<T, 64, 64>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
 }
 // stride-2 data-grad on the v3 buffer loader: one launch per output-parity class (a, b), each a GEMM
 // over the class's input pixels and only the taps of matching parity (FwdLdsB S2 mode)
@@ -1889,11 +1932,11 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
       if (g.C > 64) {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
         v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls);
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
       } else {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 64);
         v3::conv_fwd_v3<256, 64, 2, false, true, 3><<<(unsigned)gm * gn, 256, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls);
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
       }
     }
   return (int)hipGetLastError();
@@ -2124,6 +2167,17 @@ DMY_API int dmy_conv_fwd(int dtype, const void* x, const void* w, const float* b
   if ((long)N * OH * OW == 0 || K == 0) return 0;
   return dtype ? conv_fwd_t<bf16>(x, w, bias, y, psum, psq, g, (hipStream_t)stream)
                : conv_fwd_t<float>(x, w, bias, y, psum, psq, g, (hipStream_t)stream);
+}
+
+DMY_API int dmy_conv_fwd_act(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H, int W,
+                             int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
+                             const float* scale, const float* shift, int act, const void* res, long rps,
+                             void* stream) {
+  Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  if ((long)N * OH * OW == 0 || K == 0) return 0;
+  const Epi ep{scale, shift, res, rps, act, 1};
+  return dtype ? conv_fwd_t<bf16>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep)
+               : conv_fwd_t<float>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep);
 }
 
 DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,

@@ -24,6 +24,7 @@ SIGNATURES = {
     'dmy_conv_wprep_s2d': [I, P, P, I, I, I, P],
     'dmy_conv_wgrad_s2d_to_oihw': [P, P, I, I, I, P],
     'dmy_image_s2d': [I, I, P, P, I, I, I, I, I, F, P],
+    'dmy_conv_fwd_act': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P, P, I, P, L, P],
     'dmy_conv_wgrad_ex': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P],
     'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
     'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, I, P],

@@ -5,6 +5,8 @@ throughput); master weights, BN statistics and reductions are fp32.
 Every forward/backward here launches hand-written HIP kernels; no ATen compute op sits on the
 hot path (torch is used for allocation and the current stream only).
 """
+import weakref
+
 import torch
 
 from . import _lib
@@ -142,13 +144,32 @@ class WgradArena:
         return self.buf[o[0]:o[0] + numel].view(shape)
 
 
+# Bumped whenever our kernels write parameters or BN buffers through raw pointers (fused optimizers, EMA,
+# train-mode BN running statistics): torch's _version does not see those writes, so the inference caches
+# (prepped weights, eval BN coefficients) key on this as well.
+PARAM_GEN = [0]
+
+
 class ConvSpec:
-    """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None)."""
-    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache')
+    """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None).
+    wcache / ecache: inference-only caches of the prepped weight and the eval BN coefficients."""
+    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', '__weakref__')
 
     def __init__(self, stride, pad, act, bn=None):
         self.stride, self.pad, self.act, self.bn = int(stride), int(pad), int(act), bn
-        self.wcache = None
+        self.wcache = self.ecache = None
+
+
+_SPECS = weakref.WeakKeyDictionary()
+
+
+def spec_for(owner, stride, pad, act, bn):
+    """The persistent ConvSpec of a conv module (keyed weakly on the module, so deepcopies such as the EMA
+    model get their own)."""
+    sp = _SPECS.get(owner)
+    if sp is None or (sp.stride, sp.pad, sp.act) != (int(stride), int(pad), int(act)) or sp.bn is not bn:
+        sp = _SPECS[owner] = ConvSpec(stride, pad, act, bn)
+    return sp
 
 
 def prep_weight(w, dtype, need_t, Cp=None):
@@ -213,16 +234,39 @@ class KernelTimer:
         return {k: dict(launches=v[0], flops=v[1], seconds=v[2], bytes=v[3]) for k, v in out.items()}
 
 
-def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka):
+def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka, epi=None):
     """(k, s, p) and x's shape are the launch geometry; Ca / ka the layer's real input channels and kernel
-    (they differ for the space-to-depth stem and the channel-padded stem), used for the flop / byte count"""
+    (they differ for the space-to-depth stem and the channel-padded stem), used for the flop / byte count.
+    epi = (scale, shift, act, res, rps): fused inference epilogue (dmy_conv_fwd_act)"""
     N, C, H, W = x.shape
     es = x.element_size()
     Hi, Wi = (2 * H, 2 * W) if ka != k else (H, W)
-    KernelTimer.run('conv_fwd', 2.0 * N * OH * OW * K * Ca * ka * ka, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf),
-                    ptr(bias), ptr(y), ptr(psum), ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(),
-                    tag=(N, Ca, Hi, Wi, K, ka, s if ka == k else 2),
-                    nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
+    kw = dict(tag=(N, Ca, Hi, Wi, K, ka, s if ka == k else 2),
+              nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
+    fl = 2.0 * N * OH * OW * K * Ca * ka * ka
+    if epi is None:
+        KernelTimer.run('conv_fwd', fl, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), ptr(psum),
+                        ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(), **kw)
+    else:
+        sc, sh, act, res, rps = epi
+        KernelTimer.run('conv_fwd', fl, 'dmy_conv_fwd_act', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), N, H, W, C,
+                        xps, K, k, k, s, p, OH, OW, yps, ptr(sc), ptr(sh), act, ptr(res), rps, stream(), **kw)
+
+
+def eval_coef(spec, dev):
+    """eval-mode BN scale / shift from the running statistics (dmy_bn_eval_coef), cached on the spec until a
+    parameter / buffer changes (torch _version, or PARAM_GEN for our in-place kernels)"""
+    bn = spec.bn
+    key = (PARAM_GEN[0],) + tuple((t.data_ptr(), t._version) if t is not None else None
+                                  for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)) + (float(bn.eps),)
+    if spec.ecache is not None and spec.ecache[0] == key:
+        return spec.ecache[1], spec.ecache[2]
+    K = bn.running_mean.numel()
+    scale, shift = f32(K, dev), f32(K, dev)
+    call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
+         float(bn.eps), K, ptr(scale), ptr(shift), stream())
+    spec.ecache = (key, scale, shift)
+    return scale, shift
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -231,6 +275,12 @@ class ConvBNActFn(torch.autograd.Function):
         s2d = getattr(x, '_dmy_s2d', 0)
         K, C2, k, _ = weight.shape
         ctx.s2d = 0
+        need_grad = any(ctx.needs_input_grad[:6])
+        bn = spec.bn
+        train_bn = bn is not None and (bn.training or not bn.track_running_stats)
+        infer = not need_grad and not train_bn  # one fused launch: conv + eval-BN + act (+ residual)
+        wkey = (PARAM_GEN[0], weight.data_ptr(), weight._version, x.dtype, s2d)
+        cached = infer and spec.wcache is not None and spec.wcache[0] == wkey
         if s2d:
             # stem over the space-to-depth image (image_s2d): the k6 s2 p2 conv runs as k3 s1 p1 over Cs channels
             assert C2 == s2d and k == 6 and spec.stride == 2 and spec.pad == 2, 's2d input feeds only the k6 s2 p2 stem'
@@ -238,8 +288,13 @@ class ConvBNActFn(torch.autograd.Function):
             N, Cs, H2, W2 = x.shape
             C, H, W = s2d, 2 * H2, 2 * W2
             OH, OW = H2, W2
-            wf = torch.empty((K, 9 * Cs), dtype=x.dtype, device=x.device)
-            call('dmy_conv_wprep_s2d', DT[x.dtype], ptr(weight.detach().contiguous()), ptr(wf), K, C, Cs, stream())
+            if cached:
+                wf = spec.wcache[1]
+            else:
+                wf = torch.empty((K, 9 * Cs), dtype=x.dtype, device=x.device)
+                call('dmy_conv_wprep_s2d', DT[x.dtype], ptr(weight.detach().contiguous()), ptr(wf), K, C, Cs, stream())
+                if infer:
+                    spec.wcache = (wkey, wf)
             wt = None
             ctx.s2d = Cs
             # from here on the launch geometry is the k3 s1 p1 view
@@ -253,28 +308,32 @@ class ConvBNActFn(torch.autograd.Function):
             # stem: read the zero-padded storage as Cp channels (16-byte vectors) with zero weights
             Cp = cpad if (cpad and C % VW[x.dtype] and xps >= cpad) else C
             OH, OW = conv_out_hw(H, W, k, spec.stride, spec.pad)
-            need_grad = any(ctx.needs_input_grad[:6])
-            dt = x.dtype
-            if not need_grad and not torch.is_grad_enabled() and spec.wcache is not None and \
-                    spec.wcache[0] == (weight.data_ptr(), weight._version, dt):
+            if cached:
                 wf, wt = spec.wcache[1], None
             else:
-                wf, wt = prep_weight(weight, dt, need_grad and Cp == C, Cp)
-                if not need_grad:
-                    spec.wcache = ((weight.data_ptr(), weight._version, dt), wf)
+                wf, wt = prep_weight(weight, x.dtype, need_grad and Cp == C, Cp)
+                if infer:
+                    spec.wcache = (wkey, wf)
             if Cp != C:
                 x = x.as_strided((N, Cp, H, W), x.stride())
             Cg, Hg, Wg, kg, sg, pg = Cp, H, W, k, spec.stride, spec.pad
         s, p = spec.stride, spec.pad
         dev, dt = x.device, x.dtype
         M = N * OH * OW
-        z = new_act(N, K, OH, OW, x)
-        bn = spec.bn
-        train_bn = bn is not None and (bn.training or not bn.track_running_stats)
         if res is not None:
             res, rps = pixel_stride(res)
         else:
             rps = 0
+        if infer:
+            y = new_act(N, K, OH, OW, x)
+            scale, shift = eval_coef(spec, dev) if bn is not None else (None, None)
+            if scale is None and spec.act == ACT_NONE and res is None:
+                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k)
+            else:
+                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k,
+                                 epi=(scale, shift, spec.act, res, rps))
+            return y
+        z = new_act(N, K, OH, OW, x)
         if bn is not None:
             scale, shift, mean, invstd = f32(K, dev), f32(K, dev), f32(K, dev), f32(K, dev)
             if train_bn:
@@ -287,6 +346,8 @@ class ConvBNActFn(torch.autograd.Function):
                     call('dmy_colsum2', ptr(psum), ptr(psq), P, K, ptr(ps2), ptr(pq2), stream())
                     psum, psq, P = ps2, pq2, S
                 upd = int(bn.training and bn.track_running_stats)
+                if upd:
+                    PARAM_GEN[0] += 1  # running stats change behind torch's back: drop inference caches
                 mom = bn.momentum if bn.momentum is not None else 0.0
                 call('dmy_bn_finalize', ptr(psum), ptr(psq), P, K, float(M), ptr(bn.weight), ptr(bn.bias),
                      ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,

@@ -53,7 +53,8 @@ def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None):
     xsink / rsink: Fn.GradSink for the gradients of x / res when they have other consumers."""
     assert conv.groups == 1 and conv.dilation in (1, (1, 1)), 'grouped/dilated conv not on the DMA-YOLO path'
     s = conv.stride if isinstance(conv.stride, int) else conv.stride[0]
-    return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, _pad_int(conv.padding), act_code(act), res=res,
+    pad, a = _pad_int(conv.padding), act_code(act)
+    return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, pad, a, res=res, spec=Fn.spec_for(conv, s, pad, a, bn),
                           xsink=xsink, rsink=rsink)
 
 

@@ -57,10 +57,13 @@ class Detect(nn.Module):
         z = torch.empty((bs, total, self.no), dtype=torch.float32, device=out[0].device)
         off = 0
         anchors = self.anchors.float().contiguous()
+        sl = getattr(self, 'stride_list', None)
+        if not sl or len(sl) != len(out):  # host copy of the strides: no device sync per forward (graph-capturable)
+            sl = self.stride_list = [float(v) for v in self.stride.cpu()]
         for i, p in enumerate(out):
             _, na, ny, nx, no = p.shape
             s = p.stride()
-            call('dmy_detect_decode', dcode(p), ptr(p), s[0], s[2], s[3], bs, ny, nx, na, no, float(self.stride[i]),
+            call('dmy_detect_decode', dcode(p), ptr(p), s[0], s[2], s[3], bs, ny, nx, na, no, sl[i],
                  ptr(anchors[i]), ptr(z), off, total, stream())
             off += na * ny * nx
         return z
@@ -231,6 +234,7 @@ class Model(nn.Module):
         self = super()._apply(fn)
         m = self.model[-1]
         if isinstance(m, Detect):
+            m.stride_list = [float(v) for v in m.stride.cpu()] if m.stride.numel() else []
             m.stride = fn(m.stride)
             m.grid = list(map(fn, m.grid))
             if isinstance(m.anchor_grid, list):

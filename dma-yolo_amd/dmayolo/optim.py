@@ -10,6 +10,7 @@ import ctypes
 import torch
 
 from ._lib import lib, stream, call
+from .functional import PARAM_GEN
 
 lib.dmy_chunk_size.restype = ctypes.c_int
 lib.dmy_chunk_size.argtypes = []
@@ -84,6 +85,7 @@ class FusedSGD(torch.optim.Optimizer):
                     st['momentum_buffer'] = torch.empty_like(p)
                 bufs.append(st['momentum_buffer'])
             tb = _Table.get([ps, [p.grad for p in ps], bufs], ps[0].device)
+            PARAM_GEN[0] += 1
             _check(lib.dmy_sgd(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.nchunks, float(g['lr']),
                                float(g['momentum']), float(g['weight_decay']), int(g['nesterov']), int(first),
                                stream()), 'dmy_sgd')
@@ -115,6 +117,7 @@ class FusedAdam(torch.optim.Optimizer):
             bc1 = 1 - b1 ** t
             bc2s = (1 - b2 ** t) ** 0.5
             tb = _Table.get([ps, [p.grad for p in ps], ms, vs], ps[0].device)
+            PARAM_GEN[0] += 1
             _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
                                 float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
                                 float(bc1), float(bc2s), stream()), 'dmy_adam')

@@ -64,6 +64,8 @@ class ModelEMA:
                 self._pairs = ([a for a, _ in pairs], [b for _, b in pairs])
                 self._pairs_of = m
             ema_update(self._pairs[0], self._pairs[1], d)
+            from ..functional import PARAM_GEN
+            PARAM_GEN[0] += 1  # EMA weights written in place by the kernel
 
     def update_attr(self, model, include=(), exclude=('process_group', 'reducer')):
         for k, v in model.__dict__.items():

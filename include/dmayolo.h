@@ -27,6 +27,12 @@ int dmy_conv_fwd_partial_rows(long M, int K);
 int dmy_conv_fwd(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, float* psum, float* psq,
                  int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
                  void* stream);
+/* Inference form (eval BN / fused-model Conv), in one launch:
+ * y = act(T(conv(x) + bias) * scale + shift) (+ res), the value dmy_conv_fwd + dmy_bn_act_fwd produce, in one
+ * launch (models/common.py:69-77 forward / forward_fuse with BN in eval mode).  scale/shift may be NULL. */
+int dmy_conv_fwd_act(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, int N, int H, int W,
+                     int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, const float* scale,
+                     const float* shift, int act, const void* res, long rps, void* stream);
 int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,

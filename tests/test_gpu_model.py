@@ -97,3 +97,63 @@ def test_s2d_stem_matches_strided_stem(dtype):
     for a, b in zip(grads[0], grads[1]):
         scale = float(b.abs().max())
         torch.testing.assert_close(a, b, rtol=tol['rtol'] * 5, atol=tol['atol'] * 5 * max(1.0, scale))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_inference_epilogue_matches_unfused_and_tracks_updates(dtype):
+    """no-grad eval forward (one launch per conv: conv + eval-BN + act + residual epilogue, cached prepped weights
+    and BN coefficients) vs the training-path kernels on the same eval model; again after a FusedSGD step and a
+    train-mode forward changed weights / running stats behind torch's back (cache invalidation); and fused."""
+    from dmayolo.models.yolo import Model
+    from dmayolo.optim import FusedSGD
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5n.yaml'), nc=10, act_dtype=dtype).cuda()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 256, (2, 3, 160, 192), generator=g, dtype=torch.uint8).cuda()
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+
+    def both():
+        m.eval()
+        with torch.no_grad():
+            a, _ = m(x)
+        with torch.enable_grad():  # parameters require grad -> the unfused training-path kernels
+            b, _ = m(x)
+        return a.float(), b.detach().float()
+
+    a, b = both()
+    torch.testing.assert_close(a, b, **tol)
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9)
+    m.train()
+    outs = m(x)
+    sum(o.float().square().mean() for o in outs).backward()
+    opt.step()
+    a2, b2 = both()
+    torch.testing.assert_close(a2, b2, **tol)
+    assert float((a2 - a).abs().max()) > 1e-3  # the step changed the predictions: caches were refreshed
+    m.fuse()
+    with torch.no_grad():
+        c, _ = m.eval()(x)
+    torch.testing.assert_close(c.float(), a2, **(tol if dtype == torch.float32 else dict(rtol=5e-2, atol=6e-2)))
+
+
+def test_graphed_detector_replays_eager_forward():
+    """infer.GraphedDetector (HIP-graph replay of the eval forward) == the eager forward, bit for bit, and it
+    re-captures after the weights change (FusedSGD writes them through raw pointers)."""
+    from dmayolo.models.yolo import Model
+    from dmayolo.infer import GraphedDetector
+    from dmayolo.optim import FusedSGD
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5s.yaml'), nc=10, act_dtype=torch.bfloat16).cuda().eval()
+    gd = GraphedDetector(m)
+    g = torch.Generator().manual_seed(4)
+    xs = [torch.randint(0, 256, (1, 3, 256, 320), generator=g, dtype=torch.uint8).cuda() for _ in range(3)]
+    with torch.no_grad():
+        for x in xs:
+            torch.testing.assert_close(gd(x)[0], m(x)[0], rtol=0, atol=0)
+    m.train()
+    opt = FusedSGD(m.parameters(), lr=0.1)
+    sum(o.float().square().mean() for o in m(xs[0])).backward()
+    opt.step()
+    m.eval()
+    with torch.no_grad():
+        torch.testing.assert_close(gd(xs[1])[0], m(xs[1])[0], rtol=0, atol=0)
