@@ -736,6 +736,33 @@ __global__ void wprep_kernel(const float* __restrict__ w, T* __restrict__ wf, T*
   }
 }
 
+// Every conv weight of a model in one launch (training forward: the fp32 masters change every step):
+// blockIdx.y = layer, blocks grid-stride over that layer's K*KH*KW*C elements (no channel padding).
+struct WprepDesc {
+  const float* w;
+  void* wf;
+  void* wt;
+  int K, C, KH, KW;
+};
+template <typename T>
+__global__ void wprep_multi_kernel(const WprepDesc* __restrict__ d) {
+  const WprepDesc L = d[blockIdx.y];
+  const long total = (long)L.K * L.C * L.KH * L.KW;
+  T* wf = reinterpret_cast<T*>(L.wf);
+  T* wt = reinterpret_cast<T*>(L.wt);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % L.C);
+    long t = i / L.C;
+    const int kw = (int)(t % L.KW);
+    t /= L.KW;
+    const int kh = (int)(t % L.KH);
+    const int k = (int)(t / L.KH);
+    const float v = L.w[(((long)k * L.C + c) * L.KH + kh) * L.KW + kw];
+    wf[i] = from_f<T>(v);
+    if (wt) wt[(((long)c * L.KH + kh) * L.KW + kw) * L.K + k] = from_f<T>(v);
+  }
+}
+
 // Stem k6 s2 p2 weights as the equivalent k3 s1 p1 conv over the space-to-depth image (dmy_image_s2d):
 // ws[k][ky][kx][(dy * 2 + dx) * C + c] = w[k][c][2 ky + dy][2 kx + dx], channels [4C, Cs) zero
 template <typename T>
@@ -2211,6 +2238,16 @@ DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w
   const int grid = grid_cap(ceil_div(total, 256), 1024);
   if (dtype) wprep_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (bf16*)w_ohwi, (bf16*)w_ihwo, K, C, Cp, KH, KW);
   else wprep_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w_oihw, (float*)w_ohwi, (float*)w_ihwo, K, C, Cp, KH, KW);
+  return (int)hipGetLastError();
+}
+
+// descs: device array of n WprepDesc {w, wf, wt (nullable), K, C, KH, KW} (40 bytes each, include/dmayolo.h)
+DMY_API int dmy_conv_wprep_multi(int dtype, const void* descs, int n, void* stream) {
+  if (n <= 0) return 0;
+  static_assert(sizeof(WprepDesc) == 40, "WprepDesc layout is part of the C ABI");
+  const dim3 grid(64, n);
+  if (dtype) wprep_multi_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const WprepDesc*)descs);
+  else wprep_multi_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const WprepDesc*)descs);
   return (int)hipGetLastError();
 }
 

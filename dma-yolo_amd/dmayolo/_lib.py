@@ -21,6 +21,7 @@ SIGNATURES = {
     'dmy_conv_fwd': [I, P, P, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_dgrad': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_wgrad': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
+    'dmy_conv_wprep_multi': [I, P, I, P],
     'dmy_conv_wprep_s2d': [I, P, P, I, I, I, P],
     'dmy_conv_wgrad_s2d_to_oihw': [P, P, I, I, I, P],
     'dmy_image_s2d': [I, I, P, P, I, I, I, I, I, F, P],

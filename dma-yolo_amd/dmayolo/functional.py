@@ -150,6 +150,40 @@ class WgradArena:
 PARAM_GEN = [0]
 
 
+class WeightPrep:
+    """Training forward: the activation-dtype copies of every conv weight of a Model (OHWI forward operand,
+    IHWO data-grad operand) written by ONE dmy_conv_wprep_multi launch per forward instead of one
+    dmy_conv_wprep per layer.  Buffer, operand views and the 40-byte device descriptor table are built once
+    per model (host work per step: one launch).  Reusing the buffer is safe: its content is a pure function
+    of the current weights, which change only at optimizer.step, between a backward and the next forward."""
+    current = None
+    ALIGN = 64  # elements: every operand 16-B aligned (v3 loaders)
+
+    def __init__(self, weights, dtype, dev):
+        import numpy as np
+        sizes = [-(-w.numel() // self.ALIGN) * self.ALIGN for w in weights]
+        self.buf = torch.empty(2 * sum(sizes), dtype=dtype, device=dev)
+        self.map, recs, off = {}, [], 0
+        for w, n in zip(weights, sizes):
+            K, C, KH, KW = w.shape
+            wf = self.buf[off:off + w.numel()].view(K, KH * KW * C)
+            wt = self.buf[off + n:off + n + w.numel()].view(C, KH * KW * K)
+            self.map[w.data_ptr()] = (wf, wt)
+            recs.append((w.data_ptr(), wf.data_ptr(), wt.data_ptr(), K, C, KH, KW))
+            off += 2 * n
+        rec = np.dtype([('w', '<u8'), ('wf', '<u8'), ('wt', '<u8'), ('K', '<i4'), ('C', '<i4'), ('KH', '<i4'),
+                        ('KW', '<i4')])
+        self.table = torch.from_numpy(np.array(recs, dtype=rec).view(np.uint8)).to(dev)
+        self.n, self.dtype = len(recs), dtype
+
+    def launch(self):
+        call('dmy_conv_wprep_multi', DT[self.dtype], ptr(self.table), self.n, stream())
+        return self
+
+    def get(self, weight, dtype):
+        return self.map.get(weight.data_ptr()) if dtype == self.dtype else None
+
+
 class ConvSpec:
     """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None).
     wcache / ecache: inference-only caches of the prepped weight and the eval BN coefficients."""
@@ -308,8 +342,11 @@ class ConvBNActFn(torch.autograd.Function):
             # stem: read the zero-padded storage as Cp channels (16-byte vectors) with zero weights
             Cp = cpad if (cpad and C % VW[x.dtype] and xps >= cpad) else C
             OH, OW = conv_out_hw(H, W, k, spec.stride, spec.pad)
+            pre = WeightPrep.current.get(weight, x.dtype) if WeightPrep.current is not None and Cp == C else None
             if cached:
                 wf, wt = spec.wcache[1], None
+            elif pre is not None:
+                wf, wt = pre
             else:
                 wf, wt = prep_weight(weight, x.dtype, need_grad and Cp == C, Cp)
                 if infer:

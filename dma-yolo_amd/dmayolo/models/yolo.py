@@ -186,6 +186,18 @@ class Model(nn.Module):
         y._dmy_cpad = -(-x.shape[1] // Fn.VW[self.act_dtype]) * Fn.VW[self.act_dtype]  # zero-padded channels
         return y
 
+    def _weight_prep(self, dev):
+        """functional.WeightPrep over every groups-1 Conv2d except a 3-channel stem (space-to-depth /
+        channel-padded, prepped by its own layout kernel); rebuilt when the parameters move or fuse() ran"""
+        first = next(self.parameters())
+        key = (first.data_ptr(), dev, self.act_dtype)
+        c = getattr(self, '_prep', None)
+        if c is None or c[0] != key:
+            ws = [m.weight for m in self.modules() if isinstance(m, nn.Conv2d) and m.groups == 1 and
+                  m.in_channels > 4 and m.dilation in (1, (1, 1)) and m.weight.requires_grad]
+            c = self._prep = (key, Fn.WeightPrep(ws, self.act_dtype, dev))
+        return c[1]
+
     def _wgrad_arena(self):
         """Fresh zeroed weight-gradient arena for this training forward (functional.WgradArena)."""
         lay = getattr(self, '_arena_layout', None)
@@ -199,9 +211,10 @@ class Model(nn.Module):
         x = self.to_input(x)
         y = []
         arena = self.training and torch.is_grad_enabled() and x.is_cuda
-        prev = Fn.WgradArena.current
+        prev = Fn.WgradArena.current, Fn.WeightPrep.current
         if arena:
             Fn.WgradArena.current = self._wgrad_arena()
+            Fn.WeightPrep.current = self._weight_prep(x.device).launch()
         try:
             for m in self.model:
                 if m.f != -1:
@@ -209,7 +222,7 @@ class Model(nn.Module):
                 x = m(x)
                 y.append(x if m.i in self.save else None)
         finally:
-            Fn.WgradArena.current = prev
+            Fn.WgradArena.current, Fn.WeightPrep.current = prev
         return x
 
     def _initialize_biases(self, cf=None):
@@ -228,6 +241,7 @@ class Model(nn.Module):
                 m.conv = fuse_conv_and_bn(m.conv, m.bn)
                 delattr(m, 'bn')
                 m.forward = m.forward_fuse
+        self._prep = None
         return self
 
     def _apply(self, fn):

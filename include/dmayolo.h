@@ -44,6 +44,10 @@ int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N
 /* Cp >= C: input channels zero-padded to a full 16-byte vector (the 3-channel stem, yaml:15) */
 int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH, int KW,
                    void* stream);
+/* All conv weights of a model in one launch: descs is a DEVICE array of n records
+ * { const float* w_oihw; void* w_ohwi; void* w_ihwo (nullable); int K, C, KH, KW; } (40 bytes, 8-byte aligned),
+ * each as dmy_conv_wprep with Cp == C. */
+int dmy_conv_wprep_multi(int dtype, const void* descs, int n, void* stream);
 /* Stem as space-to-depth (yolov5*.yaml / DMA-YOLO yaml layer 0: Conv(3, c2, 6, 2, 2), models/common.py:50-77):
  * the k6 s2 p2 conv over x == a k3 s1 p1 conv over dmy_image_s2d(x) with these weights (Cs >= 4C channels). */
 int dmy_conv_wprep_s2d(int dtype, const float* w_oihw, void* w_s2d, int K, int C, int Cs, void* stream);
