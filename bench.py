@@ -43,6 +43,9 @@ def parse():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-detect', action='store_true')
+    ap.add_argument('--graph', action='store_true',
+                    help='replay fwd+loss+bwd as one HIP graph (train_graph.py; measured 3405 vs 3398 img/s eager '
+                         'on yolov5s: the gaps between dependent kernels are not launch overhead)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--layer-report', action='store_true', help='per-conv-shape timing table on stderr')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
@@ -140,6 +143,7 @@ def main():
     from dmayolo.synthetic import images, targets, clustered_predictions
     from dmayolo.utils.loss import ComputeLoss
     from dmayolo.infer import GraphedDetector
+    from dmayolo.train_graph import GraphedTrainStep
     from dmayolo.utils.general import non_max_suppression
     from dmayolo.utils.torch_utils import ModelEMA
 
@@ -154,7 +158,14 @@ def main():
     imgs = images(bs, img, seed=1 + rank, device=device)
     tg = targets(bs, nc, seed=1 + rank, device=device)
 
+    graphed = GraphedTrainStep(model, compute_loss, opt, ema) if world == 1 and a.graph else None
+
     def step():
+        if graphed is not None:  # forward + loss + backward replayed as one HIP graph (train_graph.py)
+            return graphed(imgs, tg)[0]
+        return train_step(net, model, compute_loss, opt, ema, imgs, tg, world)
+
+    def eager_step():
         return train_step(net, model, compute_loss, opt, ema, imgs, tg, world)
 
     model.train()
@@ -177,7 +188,7 @@ def main():
     KernelTimer.records = []
     t1 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        eager_step()  # events need the eager launches (a graph replays without the Python timer)
     torch.cuda.synchronize()
     el_events = time.perf_counter() - t1
     KernelTimer.enabled = False
