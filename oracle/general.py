@@ -12,9 +12,10 @@ def xywh2xyxy(x):
     return y
 
 
-def greedy_nms(boxes, scores, iou_thres):
+def greedy_nms(boxes, scores, iou_thres, max_keep=None):
     """torchvision.ops.nms CPU algorithm (third-party, torchvision>=0.8.1 unpinned, requirements.txt:12):
-    stable descending score order; suppress j iff IoU(i, j) > thr; areas without +1."""
+    stable descending score order; suppress j iff IoU(i, j) > thr; areas without +1.
+    `keep` grows in score order, so stopping at max_keep returns exactly nms(...)[:max_keep]."""
     order = torch.sort(scores, stable=True, descending=True)[1]
     x1, y1, x2, y2 = boxes.unbind(1)
     area = (x2 - x1) * (y2 - y1)
@@ -25,6 +26,8 @@ def greedy_nms(boxes, scores, iou_thres):
         if dead[i]:
             continue
         keep.append(int(i))
+        if max_keep is not None and len(keep) >= max_keep:
+            break
         rest = order[k + 1:]
         w = (torch.minimum(x2[i], x2[rest]) - torch.maximum(x1[i], x1[rest])).clamp(min=0)
         h = (torch.minimum(y2[i], y2[rest]) - torch.maximum(y1[i], y1[rest])).clamp(min=0)
@@ -60,6 +63,6 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
         if n > max_nms:
             x = x[torch.sort(x[:, 4], stable=True, descending=True)[1][:max_nms]]
         c = x[:, 5:6] * (0 if agnostic else max_wh)
-        keep = greedy_nms(x[:, :4] + c, x[:, 4], iou_thres)[:max_det]
+        keep = greedy_nms(x[:, :4] + c, x[:, 4], iou_thres, max_det)[:max_det]
         out[b] = x[keep]
     return out

@@ -173,6 +173,7 @@ def test_graphed_train_step_matches_eager():
     m1 = Model(os.path.join(CFG, 'yolov5n.yaml'), nc=10, act_dtype=torch.float32).cuda().train()
     m1.hyp = scaled_hyp(HYP_VISDRONE, 10, 160, 3)
     m2 = copy.deepcopy(m1)
+    p0 = [q.detach().clone() for q in m1.parameters()]
     o1 = FusedSGD(m1.parameters(), lr=0.01, momentum=0.9, nesterov=True)
     o2 = FusedSGD(m2.parameters(), lr=0.01, momentum=0.9, nesterov=True)
     l1, l2 = ComputeLoss(m1), ComputeLoss(m2)
@@ -191,5 +192,12 @@ def test_graphed_train_step_matches_eager():
         torch.testing.assert_close(b, a.detach(), rtol=1e-3, atol=1e-6)
         torch.testing.assert_close(bi, ai, rtol=1e-3, atol=1e-6)
     assert gstep.captures == 2  # first call + the 12-targets/img batch outgrowing tcap 16
-    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
-        torch.testing.assert_close(p2, p1, rtol=1e-3, atol=1e-4, msg=k)
+    # drift between the copies relative to how far each parameter moved from init: fp32 split-K atomics sum
+    # in a run-dependent order (measured 2e-5 absolute on near-zero BN biases after 5 steps), while a stale
+    # or wrong gradient in the graphed step makes the ratio O(1)
+    ratio = {}
+    for (k, p1), p2, q in zip(m1.named_parameters(), m2.parameters(), p0):
+        moved = (p1.detach() - q).double().norm().item()
+        ratio[k] = (p2.detach() - p1.detach()).double().norm().item() / max(moved, 1e-7 * q.numel() ** 0.5)
+    worst = max(ratio, key=ratio.get)
+    assert ratio[worst] < 2e-2, (worst, ratio[worst])
