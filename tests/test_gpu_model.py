@@ -173,10 +173,12 @@ def test_graphed_train_step_matches_eager():
     m1 = Model(os.path.join(CFG, 'yolov5n.yaml'), nc=10, act_dtype=torch.float32).cuda().train()
     m1.hyp = scaled_hyp(HYP_VISDRONE, 10, 160, 3)
     m2 = copy.deepcopy(m1)
+    m3 = copy.deepcopy(m1)  # second eager copy: the run-to-run noise floor of the atomics
     p0 = [q.detach().clone() for q in m1.parameters()]
     o1 = FusedSGD(m1.parameters(), lr=0.01, momentum=0.9, nesterov=True)
     o2 = FusedSGD(m2.parameters(), lr=0.01, momentum=0.9, nesterov=True)
-    l1, l2 = ComputeLoss(m1), ComputeLoss(m2)
+    o3 = FusedSGD(m3.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+    l1, l2, l3 = ComputeLoss(m1), ComputeLoss(m2), ComputeLoss(m3)
     gstep = GraphedTrainStep(m2, l2, o2, tcap=16)
     g = torch.Generator().manual_seed(5)
     for i, nt_per in enumerate([3, 5, 4, 12, 6]):
@@ -186,18 +188,26 @@ def test_graphed_train_step_matches_eager():
         a, ai = l1(m1(x), t)
         a.backward()
         o1.step()
+        o3.zero_grad(set_to_none=True)
+        l3(m3(x), t)[0].backward()
+        o3.step()
         b, bi = gstep(x, t)
         # fp32 split-K weight-grad atomics sum in a run-dependent order: after a few SGD steps the two copies
         # drift by ~2e-4 relative (measured); a wrong graph input / stale gradient shows up at >= 1e-2
         torch.testing.assert_close(b, a.detach(), rtol=1e-3, atol=1e-6)
         torch.testing.assert_close(bi, ai, rtol=1e-3, atol=1e-6)
     assert gstep.captures == 2  # first call + the 12-targets/img batch outgrowing tcap 16
-    # drift between the copies relative to how far each parameter moved from init: fp32 split-K atomics sum
-    # in a run-dependent order (measured 2e-5 absolute on near-zero BN biases after 5 steps), while a stale
-    # or wrong gradient in the graphed step makes the ratio O(1)
-    ratio = {}
-    for (k, p1), p2, q in zip(m1.named_parameters(), m2.parameters(), p0):
-        moved = (p1.detach() - q).double().norm().item()
-        ratio[k] = (p2.detach() - p1.detach()).double().norm().item() / max(moved, 1e-7 * q.numel() ** 0.5)
-    worst = max(ratio, key=ratio.get)
-    assert ratio[worst] < 2e-2, (worst, ratio[worst])
+    # drift from the eager copy relative to how far each parameter moved from init, against the same ratio
+    # for a second eager copy: fp32 split-K weight-grad atomics sum in a run-dependent order and momentum
+    # amplifies it (measured 0.2-3 % on near-zero BN parameters after 5 steps), while a stale or wrong
+    # gradient in the graphed step gives a ratio near 1
+    def drift(mb):
+        r = {}
+        for (k, p1), pb, q in zip(m1.named_parameters(), mb.parameters(), p0):
+            moved = (p1.detach() - q).double().norm().item()
+            r[k] = (pb.detach() - p1.detach()).double().norm().item() / max(moved, 1e-7 * q.numel() ** 0.5)
+        return r
+    rg, re = drift(m2), drift(m3)
+    worst, floor = max(rg, key=rg.get), max(re.values())
+    print(f'graphed vs eager: worst drift/movement {worst} {rg[worst]:.2e} (eager vs eager {floor:.2e})')
+    assert rg[worst] < max(5 * floor, 5e-2), (worst, rg[worst], floor)
