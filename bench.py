@@ -1,17 +1,27 @@
-"""DMA-YOLO hot-path benchmark (BASELINE.json metric: training images/s fwd+bwd, detect p50 ms incl. NMS).
+"""DMA-YOLO hot-path benchmark (BASELINE.json metric: training images/s fwd+bwd @640 & @1536, detect p50 ms incl.
+NMS, 1/2/4/8 GPUs).
 
-python bench.py --gpus N --steps K --warmup W [--config v5s-640|dma-1536|dma-640] [--batch B]
+python bench.py --gpus N --steps K --warmup W [--config dma-1536|v5s-640|...] [--also v5s-640|none]
 
-One timed step = one full training iteration of the reference loop (train.py:400-454) on a
-pre-staged synthetic VisDrone-shaped batch: uint8 -> /255 -> forward -> ComputeLoss (SIoU) ->
-loss*WORLD_SIZE -> backward (DDP all-reduce over RCCL when N > 1) -> SGD-nesterov step -> EMA
-(rank 0).  value = images/s over all ranks (max-over-ranks time), scaling weak (per-GPU batch fixed).
-Also reported: live HIP-event roofline of the dominant implicit-GEMM conv kernel, detect p50
-(bs1, uint8 -> forward -> NMS), and the CPU oracle (`cpu_baseline`, kind "port") on a bounded sample.
+The headline line is DMA-YOLO-l @1536 (BASELINE configs[2]; configs[3] at N = 8), the north-star model; the same
+measurement on yolov5s @640 bs64 (configs[1]) rides in the same JSON line under "at_640" so one default run covers
+both halves of the metric.  `--gpus N` without a torchrun environment re-launches itself as N ranks
+(torch.distributed.run as a child process; this parent never touches the GPU).
+
+One timed step = one iteration of the reference's batch loop (train.py:400-454) through dmayolo.trainer.Trainer on a
+pre-staged synthetic VisDrone-shaped batch: uint8 -> /255 -> forward -> ComputeLoss (SIoU) -> backward seeded with
+loss-scale * WORLD_SIZE (DDP all-reduce over RCCL when N > 1) -> GradScaler step (SGD-nesterov, warmup lr/momentum,
+accumulate) -> EMA (rank 0).  value = images/s over all ranks (max-over-ranks time), scaling weak (per-GPU batch
+fixed).  Also reported: the roofline of the dominant conv kernel family from live HIP events, detect p50 (bs1,
+uint8 -> forward -> NMS) and NMS under a 2,000-candidate load, and the CPU oracle (`cpu_baseline`, kind "port") on a
+bounded sample.
 """
 import argparse
+import gc
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,7 +40,9 @@ CONFIGS = {
     'dmaca-1536': ('yolov5l-ca-sppfcspc-bifpn.yaml', 10, 1536, 32, 'visdrone'),  # C3CA sibling
     'c5-1920': ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 3, 1920, 8, 'visdrone'),  # config 5 (UAVDT nc=3)
 }
-PEAK = {torch.bfloat16: 2500.0, torch.float32: 157.3}  # dense TFLOP/s (MI355X_MICROARCH.md)
+PEAK_FLOPS = {torch.bfloat16: 2500.0e12, torch.float32: 157.3e12}  # dense MFMA (MI355X_MICROARCH.md)
+PEAK_BW = 8.0e12  # HBM3E bytes/s (MI355X_MICROARCH.md)
+VISDRONE_TRAIN_IMAGES = 6471  # VisDrone2019-DET-train (data/VisDrone.yaml): batches per epoch for the schedule
 
 
 def parse():
@@ -38,19 +50,33 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', default='v5s-640', choices=list(CONFIGS))
-    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config)')
+    ap.add_argument('--config', default='dma-1536', choices=list(CONFIGS))
+    ap.add_argument('--also', default='v5s-640', choices=list(CONFIGS) + ['none'],
+                    help='second configuration measured in the same run (nested in the JSON line)')
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch of --config (default: the config)')
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-detect', action='store_true')
-    ap.add_argument('--graph', action='store_true',
-                    help='replay fwd+loss+bwd as one HIP graph (train_graph.py; measured 3405 vs 3398 img/s eager '
-                         'on yolov5s: the gaps between dependent kernels are not launch overhead)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--layer-report', action='store_true', help='per-conv-shape timing table on stderr')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='process-group backend (nccl = RCCL; gloo only to rehearse several ranks on one GPU)')
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """--gpus N outside torchrun: run this script as N ranks under torch.distributed.run (a child process; the
+    parent has not initialised the GPU and only waits) and exit with its status."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    return subprocess.call(cmd, env=env)
 
 
 def build(cfg, dtype, device):
@@ -63,32 +89,17 @@ def build(cfg, dtype, device):
     return m
 
 
-def train_step(net, model, compute_loss, opt, ema, imgs, tg, world):
-    """One iteration of train.py:400-454 on a staged batch: forward (DDP-wrapped `net` when world > 1),
-    loss * WORLD_SIZE (train.py:440; DDP averages, so the applied gradient is the sum over ranks),
-    backward (RCCL bucketed all-reduce overlapped by DDP), optimizer step, rank-0 EMA."""
-    pred = net(imgs)
-    loss, _ = compute_loss(pred, tg)
-    if world > 1:
-        loss = loss * world
-    loss.backward()
-    opt.step()
-    opt.zero_grad(set_to_none=True)
-    if ema is not None:
-        ema.update(model)
-    return loss
-
-
 def cpu_baseline(cfg, seconds):
-    """The oracle (CPU fp32 restatement of the reference) timed on this host: bs1 train step at the
-    bench resolution (fwd + loss + bwd + SGD), repeated for a bounded ~`seconds` sample."""
+    """The oracle (CPU fp32 restatement of the reference) timed on this host: bs1 train step at the bench
+    resolution (fwd + loss + bwd + SGD), repeated for a bounded ~`seconds` sample."""
     from oracle import nn as onn
     from oracle.loss import compute_loss
     from dmayolo.synthetic import CONFIGS as CDIR, HYP_VISDRONE, scaled_hyp, images, targets
     import yaml
     yml, nc, img, _, _ = cfg
     torch.manual_seed(0)
-    d = yaml.safe_load(open(os.path.join(CDIR, yml)))
+    with open(os.path.join(CDIR, yml)) as f:
+        d = yaml.safe_load(f)
     m = onn.bn_defaults(onn.Model(d, nc=nc)).train()
     for mod in m.modules():
         if isinstance(mod, onn.SwinTransformerLayer):
@@ -99,10 +110,9 @@ def cpu_baseline(cfg, seconds):
     opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.937, nesterov=True)
     x = images(1, img).float() / 255
     t = targets(1, nc)
-    for _ in range(2):  # untimed warmup (allocator, oneDNN primitive cache)
-        loss, _ = compute_loss(m(x), t, anchors, hyp, nc)
-        loss.backward()
-        opt.zero_grad(set_to_none=True)
+    loss, _ = compute_loss(m(x), t, anchors, hyp, nc)  # untimed warmup (allocator, oneDNN primitive cache)
+    loss.backward()
+    opt.zero_grad(set_to_none=True)
     n, t0 = 0, time.perf_counter()
     while True:
         p = m(x)
@@ -118,85 +128,95 @@ def cpu_baseline(cfg, seconds):
                 sample=f'{n} bs1 train steps of {yml} @{img} (fp32 CPU oracle, {el:.1f} s)')
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    ndev = torch.cuda.device_count()
-    dev_idx = local % max(ndev, 1)
-    if world > 1:
-        torch.cuda.set_device(dev_idx)
-        if a.backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_idx))
-        else:
-            dist.init_process_group('gloo')
-    device = torch.device('cuda', dev_idx)
-    cfg = list(CONFIGS[a.config])
-    if a.batch:
-        cfg[3] = a.batch
-    yml, nc, img, bs, _ = cfg
-    dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
+def roofline(ks, steps, el_events, dtype, cfg_name):
+    """Dominant conv family by time.  Per launch T_roof = max(F / P_mfma, B / BW_hbm) with F / B its algorithmic
+    flops / bytes; frac = sum T_roof / sum measured launch time; `bound` is the resource that
+    binds the larger share of sum T_roof, and `achieved` / `peak` are in that resource's unit."""
+    dom = max(ks, key=lambda k: ks[k]['seconds'])
+    d = ks[dom]
+    troof = d['troof_mfma'] + d['troof_hbm']
+    hbm = d['troof_hbm'] >= d['troof_mfma']
+    if hbm:
+        achieved, peak, unit = d['bytes'] / d['seconds'] / 1e9, PEAK_BW / 1e9, 'GB/s'
+    else:
+        achieved, peak, unit = d['flops'] / d['seconds'] / 1e12, PEAK_FLOPS[dtype] / 1e12, 'TFLOP/s'
+    traffic, tsrc = None, None
+    tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tr = json.load(f).get(cfg_name, {}).get(dom)
+        if tr:
+            traffic, tsrc = round(tr['bytes_per_launch']), 'profiles/pmc_traffic.json: ' + tr['source']
+    return dict(bound='hbm' if hbm else 'mfma', kernel=f'dmy_{dom} (implicit-GEMM family, all launches of the roofline pass)',
+                achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(troof / d['seconds'], 4),
+                achieved_over_peak=round(achieved / peak, 4),
+                traffic=traffic, traffic_unit='bytes/launch (HBM, PMC)', traffic_source=tsrc,
+                algorithmic_bytes_per_launch=round(d['bytes'] / d['launches']),
+                algorithmic_flops_per_launch=round(d['flops'] / d['launches']),
+                launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
+                troof_share={'mfma': round(d['troof_mfma'] / troof, 3), 'hbm': round(d['troof_hbm'] / troof, 3)},
+                kernels={k: dict(launches=v['launches'], ms=round(v['seconds'] * 1e3 / steps, 3),
+                                 tflops=round(v['flops'] / v['seconds'] / 1e12, 2),
+                                 gbps=round(v['bytes'] / v['seconds'] / 1e9, 1),
+                                 frac=round((v['troof_mfma'] + v['troof_hbm']) / v['seconds'], 4)) for k, v in ks.items()},
+                conv_share_of_step=round(sum(v['seconds'] for v in ks.values()) / el_events, 3),
+                measured_in='separate pass of the same %d steps with per-launch HIP events (%.1f ms/step there)'
+                            % (steps, el_events * 1e3 / steps))
 
+
+def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_seconds=15.0):
     from dmayolo.functional import KernelTimer
-    from dmayolo.optim import build_optimizer
     from dmayolo.synthetic import images, targets, clustered_predictions
-    from dmayolo.utils.loss import ComputeLoss
     from dmayolo.infer import GraphedDetector
-    from dmayolo.train_graph import GraphedTrainStep
+    from dmayolo.trainer import Trainer
     from dmayolo.utils.general import non_max_suppression
-    from dmayolo.utils.torch_utils import ModelEMA
 
+    cfg = list(CONFIGS[name])
+    if batch:
+        cfg[3] = batch
+    yml, nc, img, bs, _ = cfg
+    torch.cuda.reset_peak_memory_stats(device)
     model = build(cfg, dtype, device)
-    hyp = model.hyp
-    compute_loss = ComputeLoss(model)
-    opt = build_optimizer(model, 'sgd', hyp['lr0'], hyp['momentum'], hyp['weight_decay'] * bs * max(round(64 / bs), 1) / 64)
-    ema = ModelEMA(model) if rank == 0 else None
     net = model
-    if world > 1:
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev_idx], output_device=dev_idx)
+    if world > 1:  # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
+        fu = any(isinstance(m, torch.nn.MultiheadAttention) for m in model.modules())
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev_idx], output_device=dev_idx,
+                                                        find_unused_parameters=fu)
+    total_bs = bs * world
+    tr = Trainer(model, model.hyp, total_bs, epochs=300, nb=-(-VISDRONE_TRAIN_IMAGES // total_bs), world_size=world,
+                 rank=rank if world > 1 else -1, net=net)
     imgs = images(bs, img, seed=1 + rank, device=device)
     tg = targets(bs, nc, seed=1 + rank, device=device)
 
-    graphed = GraphedTrainStep(model, compute_loss, opt, ema) if world == 1 and a.graph else None
-
-    def step():
-        if graphed is not None:  # forward + loss + backward replayed as one HIP graph (train_graph.py)
-            return graphed(imgs, tg)[0]
-        return train_step(net, model, compute_loss, opt, ema, imgs, tg, world)
-
-    def eager_step():
-        return train_step(net, model, compute_loss, opt, ema, imgs, tg, world)
-
     model.train()
     for _ in range(a.warmup):
-        step()
+        tr.step(imgs, tg)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss, items = tr.step(imgs, tg)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # roofline pass: the same K steps again with a HIP event pair around every implicit-GEMM launch on its
-    # stream (functional.KernelTimer).  Kept out of the timed region: ~380 event records per yolov5s step
-    # cost ~6 % of the step (3400 vs 3184 img/s measured), which would understate `value`.
+    # roofline pass: the same K steps again with a HIP event pair around every implicit-GEMM launch on its stream
+    # (functional.KernelTimer).  Kept out of the timed region: ~380 event records per yolov5s step cost ~6 % of the
+    # step (3400 vs 3184 img/s measured), which would understate `value`.
     KernelTimer.enabled = True
     KernelTimer.records = []
     t1 = time.perf_counter()
     for _ in range(a.steps):
-        eager_step()  # events need the eager launches (a graph replays without the Python timer)
+        tr.step(imgs, tg)
     torch.cuda.synchronize()
     el_events = time.perf_counter() - t1
     KernelTimer.enabled = False
     detail = {} if a.layer_report else None
-    ks = KernelTimer.summary(detail)
+    ks = KernelTimer.summary(detail, PEAK_FLOPS[dtype], PEAK_BW)
     if detail and rank == 0:
         tot = sum(v[2] for v in detail.values())
-        print('kind        N    C    H    W    K  k s  launches  ms/step  TFLOP/s  share', file=sys.stderr)
+        print(f'[{name}] kind        N    C    H    W    K  k s  launches  ms/step  TFLOP/s  share', file=sys.stderr)
         for (kind, tag), v in sorted(detail.items(), key=lambda kv: -kv[1][2]):
             print('%-10s %s %6d %8.3f %8.1f %6.3f' % (kind, ' '.join('%4d' % t for t in tag), v[0],
                   v[2] * 1e3 / a.steps, v[1] / v[2] / 1e12, v[2] / tot), file=sys.stderr)
@@ -205,38 +225,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     assert torch.isfinite(loss).all(), 'non-finite loss'
-    peak_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30
-    ips = world * bs * a.steps / el
+    res = dict(value=round(world * bs * a.steps / el, 2), unit='images/s', ms_per_step=round(el / a.steps * 1e3, 3),
+               config={'workload': f'{yml} train @{img} nc={nc}', 'model': yml, 'global_batch': total_bs, 'img': img,
+                       'parallelism': f'dp{world}'},
+               roofline=roofline(ks, a.steps, el_events, dtype, name),
+               loss_items=[round(float(v), 5) for v in items], lr=[round(float(g['lr']), 8) for g in tr.optimizer.param_groups],
+               loss_scale=tr.scaler.get_scale())
 
-    # dominant kernel family by time -> roofline
-    dom = max(ks, key=lambda k: ks[k]['seconds'])
-    d = ks[dom]
-    achieved = d['flops'] / d['launches'] / (d['seconds'] / d['launches']) / 1e12
-    # traffic: HBM bytes per launch of the same kernel family from the committed rocprofv3 --pmc passes
-    # (FETCH_SIZE / WRITE_SIZE in separate runs of this bench command, tools/gpu/pmc.sh + tools/pmc_traffic.py)
-    traffic, tsrc = None, None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_traffic.json')
-    if os.path.exists(tpath):
-        tr = json.load(open(tpath)).get(a.config, {}).get(dom)
-        if tr:
-            traffic, tsrc = round(tr['bytes_per_launch']), 'profiles/pmc_traffic.json: ' + tr['source']
-    roof = dict(bound='mfma', kernel=f'dmy_{dom} (implicit-GEMM, all launches of the roofline pass)',
-                achieved=round(achieved, 2), peak=PEAK[dtype], unit='TFLOP/s', frac=round(achieved / PEAK[dtype], 4),
-                traffic=traffic, traffic_unit='bytes/launch (HBM, PMC)', traffic_source=tsrc,
-                algorithmic_bytes_per_launch=round(d['bytes'] / d['launches']),
-                launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
-                kernels={k: dict(launches=v['launches'], ms=round(v['seconds'] * 1e3 / a.steps, 3),
-                                 tflops=round(v['flops'] / v['seconds'] / 1e12, 2)) for k, v in ks.items()},
-                conv_share_of_step=round(sum(v['seconds'] for v in ks.values()) / el_events, 3),
-                measured_in='separate pass of the same %d steps with per-launch HIP events (%.1f ms/step there)'
-                            % (a.steps, el_events * 1e3 / a.steps))
-
-    extra = {}
     if rank == 0 and not a.no_detect:
         # detect p50 (detect.py:175-243): bs1 uint8 on device -> forward -> NMS(0.25, 0.45, max_det 1000)
-        model.eval()
+        ev = tr.ema.ema if tr.ema is not None else model
+        ev.eval()
         x1 = images(1, img, seed=3, device=device)
-        graphed = GraphedDetector(model)
+        graphed = GraphedDetector(ev)
 
         def p50(fwd, n=60):
             lat = []
@@ -251,11 +252,10 @@ def main():
             return z, round(lat[len(lat) // 2] * 1e3, 3)
 
         with torch.no_grad():
-            z, extra['detect_eager_p50_ms'] = p50(model)
-            zg, extra['detect_p50_ms'] = p50(graphed)  # HIP-graph replay of the forward + NMS (infer.py)
+            z, res['detect_eager_p50_ms'] = p50(ev)
+            zg, res['detect_p50_ms'] = p50(graphed)  # HIP-graph replay of the forward + NMS (infer.py)
             assert torch.equal(z, zg), 'graph replay differs from the eager forward'
-            A = z.shape[1]
-            sp = clustered_predictions(1, A, nc, device=device)
+            sp = clustered_predictions(1, z.shape[1], nc, device=device)
             nl = []
             for i in range(30):
                 torch.cuda.synchronize()
@@ -264,24 +264,53 @@ def main():
                 torch.cuda.synchronize()
                 nl.append(time.perf_counter() - t1)
             nl = sorted(nl[5:])
-            extra['nms_2000cand_p50_ms'] = round(nl[len(nl) // 2] * 1e3, 3)
-        model.train()
-
-    cpu = None
+            res['nms_2000cand_p50_ms'] = round(nl[len(nl) // 2] * 1e3, 3)
+    res['peak_hbm_gib'] = round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1)
+    del tr, net, model, imgs, tg
+    gc.collect()
+    torch.cuda.empty_cache()
+    res['cpu_baseline'] = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, a.cpu_seconds)
+        res['cpu_baseline'] = cpu_baseline(cfg, cpu_seconds)
+    return res
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = torch.cuda.device_count()
+    dev_idx = local % max(ndev, 1)
+    if world > 1:
+        torch.cuda.set_device(dev_idx)
+        if a.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_idx))
+        else:
+            dist.init_process_group('gloo')
+    device = torch.device('cuda', dev_idx)
+    dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
+
+    head = run_config(a.config, a, world, rank, dev_idx, device, dtype, a.batch, a.cpu_seconds)
+    also = None
+    if a.also != 'none' and a.also != a.config:
+        also = run_config(a.also, a, world, rank, dev_idx, device, dtype, 0, a.cpu_seconds)
 
     if rank == 0:
+        img = CONFIGS[a.config][2]
         line = {
-            'metric': 'train images/sec (fwd+loss+bwd+SGD+EMA) @%d; detect p50 ms incl. NMS' % img,
-            'value': round(ips, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
-            'ms_per_step': round(el / a.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'metric': 'train images/sec (fwd+loss+bwd+optimizer, train.py batch loop) @%d; detect p50 ms incl. NMS' % img,
+            'value': head.pop('value'), 'unit': head.pop('unit'), 'n_gpus': world, 'steps': a.steps,
+            'warmup': a.warmup, 'ms_per_step': head.pop('ms_per_step'), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
-            'data': 'synthetic (uint8 images seed 1, 50 VisDrone-like targets/img; random-init weights)',
-            'config': {'workload': f'{yml} train @{img} nc={nc}', 'model': yml, 'global_batch': bs * world,
-                       'img': img, 'parallelism': f'dp{world}'},
-            'roofline': roof, 'cpu_baseline': cpu, 'peak_hbm_gib': round(peak_gb, 1), **extra,
+            'data': 'synthetic (uint8 images seed 1+rank, 50 VisDrone-like targets/img; random-init weights)',
+            'config': head.pop('config'), 'roofline': head.pop('roofline'), 'cpu_baseline': head.pop('cpu_baseline'),
+            **head,
         }
+        if also is not None:
+            line['at_%d' % CONFIGS[a.also][2]] = dict(config_name=a.also, **also)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -171,7 +171,18 @@ struct Geom {
   long xps, yps;        // pixel strides of x and y (elements)
   int oihw;             // weight-grad: write [K][C][KH][KW] (torch OIHW) instead of the GEMM view [K][KH][KW][C]
   int zeroed;           // weight-grad: the output is already zero (caller-cleared arena): no memset
+  // weight-grad deterministic mode: split s stores its partial tile to dws[s * dws_slab + idx] (no atomics) and
+  // wgrad_split_reduce sums the splits in index order; null = fp32 atomics into dw
+  float* dws;
+  long dws_slab;
+  int* plan;            // non-null: only report the split count the dispatch would use (*plan), launch nothing
 };
+
+// weight-grad epilogue store: deterministic workspace slot of this split, or an fp32 atomic into dw
+DEV void wgrad_out(const Geom& g, float* dw, int split, long idx, float v) {
+  if (g.dws != nullptr) g.dws[(long)split * g.dws_slab + idx] = v;
+  else atomicAdd(dw + idx, v);
+}
 
 // Inference epilogue (eval BatchNorm folded per channel + activation + residual, applied to the T-rounded
 // conv output exactly as dmy_bn_act_fwd would read it back): y = act(z * scale + shift) (+ res).
@@ -713,7 +724,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const T* __restrict__ x,
   const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += NT) {
     const int row = e / BN, m = m0 + row;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
+    if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 
@@ -1439,7 +1450,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
   const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += 256) {
     const int row = e / BN, m = m0 + row;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
+    if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 // Narrow-layer weight-grad (out channels <= 64): block tile BM (out channels, 32 or 64) x BN
@@ -1698,7 +1709,7 @@ __global__ void __launch_bounds__(BN) conv_wgrad_v3n(const bf16* __restrict__ x,
   const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += BN) {
     const int row = e / BN, m = m0 + row;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
+    if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 // Weight-grad v4: 8 waves (BM / 64 x BN / 64, each 64 x 64), BM x BN = 128 x 256 or 256 x 128, a
@@ -1781,7 +1792,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
   const long coff = wgrad_col(g, n);
   for (int e = threadIdx.x; e < BM * BN; e += 512) {
     const int row = e / BN, m = m0 + row;
-    if (m < g.K && n < Ntot) atomicAdd(dw + (long)m * Ntot + coff, ct[row * RS + c]);
+    if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
 }  // namespace v3
@@ -1792,7 +1803,33 @@ Geom make_geom(int N, int H, int W, int C, long xps, int K, int KH, int KW, int 
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.KH = KH; g.KW = KW; g.S = S; g.P = P;
   g.OH = OH; g.OW = OW; g.xps = xps; g.yps = yps;
   g.oihw = 0; g.zeroed = 0;
+  g.dws = nullptr; g.dws_slab = 0; g.plan = nullptr;
   return g;
+}
+
+// dw[i] += sum over splits s = 0, 1, ... of ws[s][i], in that order (the deterministic split-K reduction)
+__global__ void wgrad_split_reduce(const float* __restrict__ ws, float* __restrict__ dw, long slab, int splits) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < slab; i += (long)gridDim.x * blockDim.x) {
+    float acc = ws[i];
+    for (int k = 1; k < splits; ++k) acc += ws[(long)k * slab + i];
+    dw[i] += acc;
+  }
+}
+
+// Called by every weight-grad launcher once its split count is known.  Returns true when the caller must return
+// right away (plan query).  Deterministic mode with one split keeps the single atomic per element (exact: it adds
+// to a zero or to an earlier stream-ordered launch's value), so g.dws is dropped.
+inline bool wgrad_begin(Geom& g, int splits) {
+  if (g.plan != nullptr) {
+    *g.plan = splits;
+    return true;
+  }
+  if (g.dws != nullptr && splits <= 1) g.dws = nullptr;
+  return false;
+}
+inline void wgrad_end(const Geom& g, float* dw, int splits, hipStream_t st) {
+  if (g.dws != nullptr)
+    wgrad_split_reduce<<<grid_cap(ceil_div(g.dws_slab, 256), 2048), 256, 0, st>>>(g.dws, dw, g.dws_slab, splits);
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -1836,7 +1873,7 @@ int launch_dgrad(const T* dy, const T* wt, T* dx, int acc, const Geom& g, hipStr
 }
 
 template <typename T, int BM, int BN>
-int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t st) {
+int launch_wgrad(const T* x, const T* dy, float* dw, Geom g, hipStream_t st) {
   constexpr int VW = Traits<T>::VW;
   constexpr int BK = Cfg<T>::BK;
   const long NP = (long)g.N * g.OH * g.OW;
@@ -1852,6 +1889,7 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)gm * gn, splits);
+  if (wgrad_begin(g, splits)) return 0;
   const bool va = g.K % VW == 0 && g.yps % VW == 0 && aligned16(dy);
   const bool vb = g.C % VW == 0 && g.xps % VW == 0 && aligned16(x);
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
@@ -1859,6 +1897,7 @@ int launch_wgrad(const T* x, const T* dy, float* dw, const Geom& g, hipStream_t 
   else if (va) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
   else if (vb) conv_wgrad_kernel<T, BM, BN, false, true><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
   else conv_wgrad_kernel<T, BM, BN, false, false><<<grid, NT, 0, st>>>(x, dy, dw, per, g, gm, gn);
+  wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
 
@@ -2002,7 +2041,7 @@ inline int num_cus() {
   return n;
 }
 
-inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const long NP = (long)g.N * g.OH * g.OW;
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, 128), gn = ceil_div(Ntot, 128);
@@ -2030,6 +2069,7 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)gm * gn, splits);
+  if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   const bool buf = conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
@@ -2045,6 +2085,7 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, const Geom&
     v3::conv_wgrad_v3<2, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   else
     v3::conv_wgrad_v3<2, 0><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
+  wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
 
@@ -2059,7 +2100,7 @@ inline int wgrad_v4_mode() {
   return t;
 }
 template <int BM, int BN>
-int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const long NP = (long)g.N * g.OH * g.OW;
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, BM), gn = ceil_div(Ntot, BN);
@@ -2085,15 +2126,17 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, const Geom& g, hip
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)tiles, splits);
+  if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
   v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
 
 // narrow layers (K <= 64): BM = 32 / 64 out-channel tiles, BN = 128 / 256 column tiles
 template <int BM, int BN>
-int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hipStream_t st) {
+int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const long NP = (long)g.N * g.OH * g.OW;
   const int Ntot = g.KH * g.KW * g.C;
   const int gm = ceil_div(g.K, BM), gn = ceil_div(Ntot, BN);
@@ -2120,6 +2163,7 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hi
   const int per = ceil_div(nk, splits);
   splits = ceil_div(nk, per);
   const dim3 grid((unsigned)tiles, splits);
+  if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   constexpr int NS = 3 * v3::WgradLdsN<BM, BN>::STAGE <= 80 * 1024 ? 3 : 2;  // keep 2 blocks per CU
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
@@ -2127,6 +2171,7 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, const Geom& g, hi
     v3::conv_wgrad_v3n<BM, BN, NS, true><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   else
     v3::conv_wgrad_v3n<BM, BN, NS, false><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
+  wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
 
@@ -2228,6 +2273,34 @@ DMY_API int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* d
   Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
   g.oihw = flags & DMY_WGRAD_OIHW ? 1 : 0;
   g.zeroed = flags & DMY_WGRAD_ZEROED ? 1 : 0;
+  return dtype ? conv_wgrad_t<bf16>(x, dy, dw, g, (hipStream_t)stream)
+               : conv_wgrad_t<float>(x, dy, dw, g, (hipStream_t)stream);
+}
+
+// deterministic weight-grad: fp32 workspace elements it needs (0 = the dispatch uses one split: no workspace)
+DMY_API long dmy_conv_wgrad_ws_elems(int dtype, const void* x, const void* dy, int N, int H, int W, int C, long xps,
+                                     int K, int KH, int KW, int S, int P, int OH, int OW, long yps, int flags) {
+  Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  g.oihw = flags & DMY_WGRAD_OIHW ? 1 : 0;
+  g.zeroed = flags & DMY_WGRAD_ZEROED ? 1 : 0;
+  int splits = 1;
+  g.plan = &splits;
+  (void)(dtype ? conv_wgrad_t<bf16>(x, dy, nullptr, g, nullptr) : conv_wgrad_t<float>(x, dy, nullptr, g, nullptr));
+  return splits > 1 ? (long)splits * K * KH * KW * C : 0;
+}
+
+DMY_API int dmy_conv_wgrad_det(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C,
+                               long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, int flags,
+                               float* ws, long ws_elems, void* stream) {
+  const long need = dmy_conv_wgrad_ws_elems(dtype, x, dy, N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps, flags);
+  if (need > 0 && (ws == nullptr || ws_elems < need)) return (int)hipErrorInvalidValue;
+  Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  g.oihw = flags & DMY_WGRAD_OIHW ? 1 : 0;
+  g.zeroed = flags & DMY_WGRAD_ZEROED ? 1 : 0;
+  if (need > 0) {
+    g.dws = ws;
+    g.dws_slab = (long)K * KH * KW * C;
+  }
   return dtype ? conv_wgrad_t<bf16>(x, dy, dw, g, (hipStream_t)stream)
                : conv_wgrad_t<float>(x, dy, dw, g, (hipStream_t)stream);
 }

@@ -8,7 +8,9 @@
 //    forward-mode dual numbers (4 partials: px, py, pw, ph), so they follow the same expression as
 //    the reference autograd graph; torch.minimum/maximum ties split the gradient in half, abs'(0)=0.
 //    tobj keeps the max clamped IoU per cell (sort_obj_iou forced on, loss.py:191-194) via an
-//    integer atomicMax on non-negative float bits -> deterministic.
+//    integer atomicMax on non-negative float bits -> deterministic.  Per-target gradients are summed per cell in
+//    ascending target order (the reference's index_put_ accumulate order) and the loss sums go through per-block
+//    partials reduced in a fixed order: no float atomics, the loss and dL/dp are run-to-run bit-identical.
 // Everything stays on device: target counts are read by the kernels, never by the host.
 #include "common.h"
 #include "dual.h"
@@ -166,14 +168,23 @@ struct LossCfg {
   long sb, sa, sh, sw;  // element strides of p (batch, anchor, row, col); channel stride = 1
 };
 
-// per selected target: SIoU box loss + cls BCE + tobj scatter-max; grads into G (fp32, p-shaped)
+// Loss partial sums: every block writes its own slot of part[3][LOSS_PMAX] (row 0 lbox, 1 lobj, 2 lcls; per level),
+// reduced in a fixed order by loss_finalize_kernel -- no float atomics, so the loss is run-to-run bit-identical.
+constexpr int LOSS_PMAX = 2048;
+
+// per selected target j: SIoU box loss + cls BCE + tobj scatter-max.  The target's gradient contribution to its
+// cell's box / cls channels goes to tgrad[j][4 + nc] (no atomics), and j is pushed on its cell's list (head / nxt);
+// loss_combine_kernel then sums each cell's contributions in ascending j -- the order of the reference's
+// index_put_(accumulate=True) backward of pi[b, a, gj, gi] (utils/loss.py:179).
 template <typename T>
 __global__ void loss_targets_kernel(const T* __restrict__ p, LossCfg cfg, const int* __restrict__ tb,
                                     const int* __restrict__ ta, const int* __restrict__ tgj, const int* __restrict__ tgi,
                                     const int* __restrict__ tcls, const float* __restrict__ tbox,
                                     const float* __restrict__ anch, const int* __restrict__ count,
-                                    float* __restrict__ G, float* __restrict__ tobj, float* __restrict__ acc) {
+                                    float* __restrict__ tgrad, int* __restrict__ head, int* __restrict__ nxt,
+                                    float* __restrict__ tobj, float* __restrict__ part) {
   const int M = *count;
+  const int ng = 4 + (cfg.nc > 1 ? cfg.nc : 0);
   float lbox = 0.f, lcls = 0.f;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < M; j += gridDim.x * blockDim.x) {
     const int b = tb[j], a = ta[j], gj = tgj[j], gi = tgi[j];
@@ -190,23 +201,25 @@ __global__ void loss_targets_kernel(const T* __restrict__ p, LossCfg cfg, const 
     lbox += 1.f - iou.v;
     // d(mean(1-iou))/d p_k  scaled by box gain * bs
     const float gs = -cfg.box_gain * cfg.bs / (float)M;
-    float* g = G + off;
-    atomicAdd(g + 0, gs * iou.d[0] * 2.f * sg[0] * (1.f - sg[0]));
-    atomicAdd(g + 1, gs * iou.d[1] * 2.f * sg[1] * (1.f - sg[1]));
-    atomicAdd(g + 2, gs * iou.d[2] * 2.f * q2 * 2.f * sg[2] * (1.f - sg[2]) * anch[j * 2]);
-    atomicAdd(g + 3, gs * iou.d[3] * 2.f * q3 * 2.f * sg[3] * (1.f - sg[3]) * anch[j * 2 + 1]);
+    float* g = tgrad + (long)j * ng;
+    g[0] = gs * iou.d[0] * 2.f * sg[0] * (1.f - sg[0]);
+    g[1] = gs * iou.d[1] * 2.f * sg[1] * (1.f - sg[1]);
+    g[2] = gs * iou.d[2] * 2.f * q2 * 2.f * sg[2] * (1.f - sg[2]) * anch[j * 2];
+    g[3] = gs * iou.d[3] * 2.f * q3 * 2.f * sg[3] * (1.f - sg[3]) * anch[j * 2 + 1];
     // tobj[b,a,gj,gi] = max(clamp(iou,0))
+    const long cell = (((long)b * cfg.na + a) * cfg.H + gj) * cfg.W + gi;
     const float sc = fmaxf(iou.v, 0.f);
-    atomicMax(reinterpret_cast<int*>(tobj) + (((long)b * cfg.na + a) * cfg.H + gj) * cfg.W + gi, __float_as_int(sc));
+    atomicMax(reinterpret_cast<int*>(tobj) + cell, __float_as_int(sc));
     if (cfg.nc > 1) {
       const float cg = cfg.cls_gain * cfg.bs / ((float)M * cfg.nc);
       const int tc = tcls[j];
       for (int c = 0; c < cfg.nc; ++c) {
         float d;
         lcls += bce(to_f(ps[5 + c]), c == tc ? cfg.cp : cfg.cn, cfg.cls_pw, &d);
-        atomicAdd(g + 5 + c, cg * d);
+        g[4 + c] = cg * d;
       }
     }
+    nxt[j] = atomicExch(head + cell, j);  // list order is arbitrary; the combine sorts it
   }
   __shared__ float r1[16], r2[16];
   lbox = wave_sum(lbox);
@@ -218,8 +231,39 @@ __global__ void loss_targets_kernel(const T* __restrict__ p, LossCfg cfg, const 
     float s1 = 0.f, s2 = 0.f;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { s1 += r1[w]; s2 += r2[w]; }
     if (M > 0) {
-      atomicAdd(acc + 0, s1 / (float)M);
-      if (cfg.nc > 1) atomicAdd(acc + 2, s2 / ((float)M * cfg.nc));
+      part[blockIdx.x] = s1 / (float)M;
+      if (cfg.nc > 1) part[2 * LOSS_PMAX + blockIdx.x] = s2 / ((float)M * cfg.nc);
+    }
+  }
+}
+
+// one thread per target: the smallest j on a cell's list owns the cell and writes G's box / cls channels there as
+// 0 + c_j0 + c_j1 + ... in ascending j (lists hold the few targets sharing a (b, a, gj, gi) cell)
+__global__ void loss_combine_kernel(LossCfg cfg, const int* __restrict__ tb, const int* __restrict__ ta,
+                                    const int* __restrict__ tgj, const int* __restrict__ tgi,
+                                    const int* __restrict__ count, const float* __restrict__ tgrad,
+                                    const int* __restrict__ head, const int* __restrict__ nxt, float* __restrict__ G) {
+  const int M = *count;
+  const int ng = 4 + (cfg.nc > 1 ? cfg.nc : 0);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < M; j += gridDim.x * blockDim.x) {
+    const int b = tb[j], a = ta[j], gj = tgj[j], gi = tgi[j];
+    const long cell = (((long)b * cfg.na + a) * cfg.H + gj) * cfg.W + gi;
+    int mn = j;
+    for (int k = head[cell]; k >= 0; k = nxt[k]) mn = min(mn, k);
+    if (mn != j) continue;
+    float* g = G + b * cfg.sb + gj * cfg.sh + gi * cfg.sw + (long)a * cfg.sa;
+    for (int c = 0; c < ng; ++c) {
+      float acc = 0.f;
+      int last = -1;
+      while (true) {  // next target of the cell in ascending index order
+        int nj = 0x7fffffff;
+        for (int k = head[cell]; k >= 0; k = nxt[k])
+          if (k > last && k < nj) nj = k;
+        if (nj == 0x7fffffff) break;
+        acc += tgrad[(long)nj * ng + c];
+        last = nj;
+      }
+      g[c < 4 ? c : c + 1] = acc;  // channels 0-3 box, 5.. cls (4 is objectness, written by loss_obj_kernel)
     }
   }
 }
@@ -227,7 +271,7 @@ __global__ void loss_targets_kernel(const T* __restrict__ p, LossCfg cfg, const 
 // dense objectness BCE over every (b, a, h, w); writes the obj-channel gradient
 template <typename T>
 __global__ void loss_obj_kernel(const T* __restrict__ p, LossCfg cfg, const float* __restrict__ tobj,
-                                float* __restrict__ G, float* __restrict__ acc) {
+                                float* __restrict__ G, float* __restrict__ part) {
   const long total = (long)cfg.N * cfg.na * cfg.H * cfg.W;
   const float gs = cfg.balance * cfg.obj_gain * cfg.bs / (float)total;
   float s = 0.f;
@@ -250,26 +294,41 @@ __global__ void loss_obj_kernel(const T* __restrict__ p, LossCfg cfg, const floa
   if (threadIdx.x == 0) {
     float q = 0.f;
     for (int k = 0; k < (int)(blockDim.x >> 6); ++k) q += r[k];
-    atomicAdd(acc + 1, q * cfg.balance / (float)total);
+    part[LOSS_PMAX + blockIdx.x] = q * cfg.balance / (float)total;
   }
 }
 
-// acc per level: [lbox_mean, lobj_balanced, lcls_mean]; -> loss[1], items[3]
-__global__ void loss_finalize_kernel(const float* __restrict__ acc, int nl, float box, float obj, float cls, float bs,
-                                     float* __restrict__ loss, float* __restrict__ items) {
-  float lb = 0.f, lo = 0.f, lc = 0.f;
-  for (int i = 0; i < nl; ++i) {
-    lb += acc[i * 3 + 0];
-    lo += acc[i * 3 + 1];
-    lc += acc[i * 3 + 2];
+// part per level: [3][LOSS_PMAX] block partials (lbox mean, lobj balanced, lcls mean); one 256-thread block reduces
+// every row in a fixed order (strided serial sums, then a fixed tree) -> loss[1], items[3]
+__global__ void __launch_bounds__(256) loss_finalize_kernel(const float* __restrict__ part, int nl, float box, float obj,
+                                                            float cls, float bs, float* __restrict__ loss,
+                                                            float* __restrict__ items) {
+  __shared__ float red[256];
+  __shared__ float row[3];
+  float tot[3] = {0.f, 0.f, 0.f};
+  for (int lvl = 0; lvl < nl; ++lvl)
+    for (int r = 0; r < 3; ++r) {
+      const float* pr = part + ((long)lvl * 3 + r) * LOSS_PMAX;
+      float v = 0.f;
+      for (int k = threadIdx.x; k < LOSS_PMAX; k += 256) v += pr[k];
+      red[threadIdx.x] = v;
+      __syncthreads();
+      for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) row[r] = red[0];
+      __syncthreads();
+      tot[r] += row[r];
+      __syncthreads();
+    }
+  if (threadIdx.x == 0) {
+    const float lb = tot[0] * box, lo = tot[1] * obj, lc = tot[2] * cls;
+    items[0] = lb;
+    items[1] = lo;
+    items[2] = lc;
+    loss[0] = (lb + lo + lc) * bs;
   }
-  lb *= box;
-  lo *= obj;
-  lc *= cls;
-  items[0] = lb;
-  items[1] = lo;
-  items[2] = lc;
-  loss[0] = (lb + lo + lc) * bs;
 }
 
 // dp = G * upstream  (G fp32 p-shaped with strides; output T with the same strides)
@@ -300,31 +359,40 @@ DMY_API int dmy_build_targets(const float* targets, int nt, const float* anchors
   return (int)hipGetLastError();
 }
 
-// One level of the loss.  acc3 = this level's 3 accumulators (zeroed by the caller), G zeroed.
+DMY_API int dmy_yolo_loss_part_rows() { return 3 * LOSS_PMAX; }
+
+// One level of the loss.  part = this level's dmy_yolo_loss_part_rows() fp32 block partials (zeroed by the caller),
+// G zeroed (p-shaped fp32), tobj zeroed (N*na*H*W).  Workspaces (contents on entry do not matter): tgrad
+// cap * (4 + nc) fp32, links N*na*H*W + cap int32.
 DMY_API int dmy_yolo_loss_level(int dtype, const void* p, long sb, long sa, long sh, long sw, int N, int na, int H, int W,
                                 int no, int nc, float box_gain, float obj_gain, float cls_gain, float cls_pw,
                                 float obj_pw, float cp, float cn, float balance, float bs, const int* tb,
                                 const int* ta, const int* tgj, const int* tgi, const int* tcls, const float* tbox,
-                                const float* anch, const int* count, int cap, float* G, float* tobj, float* acc3,
-                                void* stream) {
+                                const float* anch, const int* count, int cap, float* G, float* tobj, float* part,
+                                float* tgrad, int* links, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   LossCfg cfg{box_gain, obj_gain, cls_gain, cls_pw, obj_pw, cp, cn, balance, bs, nc, na, no, N, H, W, sb, sa, sh, sw};
   const int gt = grid_cap(ceil_div(cap, 256), 1024);
   const long cells = (long)N * na * H * W;
-  const int go = grid_cap(ceil_div(cells, 256), 2048);
-  if (dtype) {
-    loss_targets_kernel<bf16><<<gt, 256, 0, st>>>((const bf16*)p, cfg, tb, ta, tgj, tgi, tcls, tbox, anch, count, G, tobj, acc3);
-    loss_obj_kernel<bf16><<<go, 256, 0, st>>>((const bf16*)p, cfg, tobj, G, acc3);
-  } else {
-    loss_targets_kernel<float><<<gt, 256, 0, st>>>((const float*)p, cfg, tb, ta, tgj, tgi, tcls, tbox, anch, count, G, tobj, acc3);
-    loss_obj_kernel<float><<<go, 256, 0, st>>>((const float*)p, cfg, tobj, G, acc3);
-  }
+  const int go = grid_cap(ceil_div(cells, 256), LOSS_PMAX);
+  int* head = links;
+  int* nxt = links + cells;
+  (void)hipMemsetAsync(head, 0xff, sizeof(int) * (size_t)cells, st);  // empty lists (-1)
+  if (dtype)
+    loss_targets_kernel<bf16><<<gt, 256, 0, st>>>((const bf16*)p, cfg, tb, ta, tgj, tgi, tcls, tbox, anch, count,
+                                                  tgrad, head, nxt, tobj, part);
+  else
+    loss_targets_kernel<float><<<gt, 256, 0, st>>>((const float*)p, cfg, tb, ta, tgj, tgi, tcls, tbox, anch, count,
+                                                   tgrad, head, nxt, tobj, part);
+  loss_combine_kernel<<<gt, 256, 0, st>>>(cfg, tb, ta, tgj, tgi, count, tgrad, head, nxt, G);
+  if (dtype) loss_obj_kernel<bf16><<<go, 256, 0, st>>>((const bf16*)p, cfg, tobj, G, part);
+  else loss_obj_kernel<float><<<go, 256, 0, st>>>((const float*)p, cfg, tobj, G, part);
   return (int)hipGetLastError();
 }
 
-DMY_API int dmy_yolo_loss_finalize(const float* acc, int nl, float box, float obj, float cls, float bs, float* loss,
+DMY_API int dmy_yolo_loss_finalize(const float* part, int nl, float box, float obj, float cls, float bs, float* loss,
                                    float* items, void* stream) {
-  loss_finalize_kernel<<<1, 1, 0, (hipStream_t)stream>>>(acc, nl, box, obj, cls, bs, loss, items);
+  loss_finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(part, nl, box, obj, cls, bs, loss, items);
   return (int)hipGetLastError();
 }
 
@@ -332,5 +400,23 @@ DMY_API int dmy_loss_grad(int dtype, const float* G, const float* up, void* dp, 
   const int g = grid_cap(ceil_div(n, 256), 4096);
   if (dtype) loss_grad_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>(G, up, (bf16*)dp, n);
   else loss_grad_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>(G, up, (float*)dp, n);
+  return (int)hipGetLastError();
+}
+
+// SIoU of n xywh box pairs through the loss kernel's own siou(): value and d(iou)/d(b1) (test entry)
+__global__ void siou_eval_kernel(const float* __restrict__ b1, const float* __restrict__ b2, float* __restrict__ iou,
+                                 float* __restrict__ grad, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  D4 x = dc(b1[i * 4]), y = dc(b1[i * 4 + 1]), w = dc(b1[i * 4 + 2]), h = dc(b1[i * 4 + 3]);
+  x.d[0] = 1.f; y.d[1] = 1.f; w.d[2] = 1.f; h.d[3] = 1.f;
+  const D4 r = siou(x, y, w, h, b2[i * 4], b2[i * 4 + 1], b2[i * 4 + 2], b2[i * 4 + 3]);
+  iou[i] = r.v;
+  for (int k = 0; k < 4; ++k) grad[i * 4 + k] = r.d[k];
+}
+
+DMY_API int dmy_siou_eval(const float* b1, const float* b2, float* iou, float* grad, int n, void* stream) {
+  if (n <= 0) return 0;
+  siou_eval_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(b1, b2, iou, grad, n);
   return (int)hipGetLastError();
 }

@@ -603,7 +603,8 @@ DEV float u01(unsigned long long seed, unsigned long long idx) {
 }
 template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, long yps, long M, int C, float p,
-                               unsigned long long seed) {
+                               const unsigned long long* __restrict__ seed_ptr) {
+  const unsigned long long seed = *seed_ptr;  // device-resident: a graph replay reads the seed drawn for that replay
   const long total = M * C;
   const float sc = 1.f / (1.f - p);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -694,8 +695,25 @@ DMY_API int dmy_mha_fwd_ref(int dtype, const void* q, long qps, const void* k, l
   return (int)hipGetLastError();
 }
 
+// seed = state = splitmix64 step of the per-device generator state (one lane, vector store): launched on the
+// stream before each dropout forward, so HIP-graph replays draw a fresh mask every step
+__global__ void dropout_seed_kernel(unsigned long long* state, unsigned long long* seed) {
+  if (threadIdx.x == 0) {
+    const unsigned long long s = *state + 0x9E3779B97F4A7C15ull;
+    *state = s;
+    unsigned long long z = (s ^ (s >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    *seed = z ^ (z >> 31);
+  }
+}
+
+DMY_API int dmy_dropout_seed(unsigned long long* state, unsigned long long* seed, void* stream) {
+  dropout_seed_kernel<<<1, 64, 0, (hipStream_t)stream>>>(state, seed);
+  return (int)hipGetLastError();
+}
+
 DMY_API int dmy_dropout(int dtype, const void* x, long xps, void* y, long yps, long M, int C, float p,
-                        unsigned long long seed, void* stream) {
+                        const unsigned long long* seed, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M * C == 0) return 0;
   if (!(p >= 0.f && p < 1.f)) return (int)hipErrorInvalidValue;

@@ -17,7 +17,17 @@ struct TList {
   const long* off;        // chunk table: element offset
 };
 
-__global__ void sgd_kernel(TList L, float lr, float mom, float wd, int nesterov, int first) {
+// GradScaler (train.py:354, 445-450; torch.amp.GradScaler defaults) kept on the device: `scale` is the loss
+// scale, `found` the non-finite flag of this step's gradients.  Both null = scaler disabled.  The optimizer
+// kernels unscale on the fly (g * (1 / scale), exact: the scale is a power of two) and skip the update when
+// `found` is set, as scaler.step() skips optimizer.step(); no host synchronisation anywhere.
+DEV bool amp_skip(const float* found) { return found != nullptr && *found != 0.f; }
+DEV float amp_inv(const float* scale) { return scale != nullptr ? (float)(1.0 / (double)*scale) : 1.f; }
+
+__global__ void sgd_kernel(TList L, float lr, float mom, float wd, int nesterov, const float* scale,
+                           const float* found) {
+  if (amp_skip(found)) return;
+  const float inv = amp_inv(scale);
   const int t = L.tid[blockIdx.x];
   const long o = L.off[blockIdx.x];
   const long end = min(L.n[t], o + CHUNK);
@@ -25,11 +35,10 @@ __global__ void sgd_kernel(TList L, float lr, float mom, float wd, int nesterov,
   const float* g = L.g[t];
   float* b = L.m[t];
   for (long i = o + threadIdx.x; i < end; i += blockDim.x) {
-    float d = g[i];
+    float d = g[i] * inv;
     if (wd != 0.f) d += wd * p[i];
-    float bv;
-    if (first) bv = d;
-    else bv = mom * b[i] + d;
+    // momentum buffers start zeroed: mom * 0 + d == d is torch.optim.SGD's clone-on-first-step exactly
+    const float bv = mom * b[i] + d;
     b[i] = bv;
     if (nesterov) d = d + mom * bv;
     else d = bv;
@@ -37,7 +46,10 @@ __global__ void sgd_kernel(TList L, float lr, float mom, float wd, int nesterov,
   }
 }
 
-__global__ void adam_kernel(TList L, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2s) {
+__global__ void adam_kernel(TList L, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2s,
+                            const float* scale, const float* found) {
+  if (amp_skip(found)) return;
+  const float inv = amp_inv(scale);
   const int t = L.tid[blockIdx.x];
   const long o = L.off[blockIdx.x];
   const long end = min(L.n[t], o + CHUNK);
@@ -47,7 +59,7 @@ __global__ void adam_kernel(TList L, float lr, float b1, float b2, float eps, fl
   float* v = L.v[t];
   const float step = lr / bc1;
   for (long i = o + threadIdx.x; i < end; i += blockDim.x) {
-    float d = g[i];
+    float d = g[i] * inv;
     if (wd != 0.f) d += wd * p[i];
     const float mv = m[i] + (1.f - b1) * (d - m[i]);  // torch: exp_avg.lerp_(grad, 1 - beta1)
     const float vv = v[i] * b2 + (1.f - b2) * d * d;
@@ -67,25 +79,74 @@ __global__ void ema_kernel(TList L, float d) {
   for (long i = o + threadIdx.x; i < end; i += blockDim.x) e[i] = e[i] * d + (1.f - d) * s[i];
 }
 
+// scaler.unscale_'s non-finite check over every gradient of the step (the g list of the table)
+__global__ void amp_check_kernel(TList L, const float* __restrict__ scale, float* __restrict__ found) {
+  const int t = L.tid[blockIdx.x];
+  const long o = L.off[blockIdx.x];
+  const long end = min(L.n[t], o + CHUNK);
+  const float inv = amp_inv(scale);
+  const float* g = L.g[t];
+  bool bad = false;
+  for (long i = o + threadIdx.x; i < end; i += blockDim.x) bad |= !isfinite(g[i] * inv);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *found = 1.f;  // every writer stores the same value
+}
+
+// scaler.update(): backoff on a non-finite step, growth after `interval` clean steps; gup = scale * world is the
+// loss's upstream gradient (scaler.scale(loss * WORLD_SIZE).backward(), train.py:440-445); found is re-armed
+__global__ void amp_update_kernel(float* scale, float* gup, int* tracker, float* found, float world, float growth,
+                                  float backoff, int interval) {
+  if (threadIdx.x != 0) return;
+  float s = *scale;
+  if (*found != 0.f) {
+    s *= backoff;
+    *tracker = 0;
+  } else {
+    const int n = *tracker + 1;
+    if (n == interval) {
+      s *= growth;
+      *tracker = 0;
+    } else {
+      *tracker = n;
+    }
+  }
+  *scale = s;
+  *gup = s * world;
+  *found = 0.f;
+}
+
 }  // namespace
 
 DMY_API int dmy_chunk_size() { return CHUNK; }
 
+DMY_API int dmy_amp_check(const float* const* g, const long* n, const int* tid, const long* off, int nchunks,
+                          const float* scale, float* found, void* stream) {
+  if (nchunks == 0) return 0;
+  TList L{nullptr, g, nullptr, nullptr, n, tid, off};
+  amp_check_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, scale, found);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_amp_update(float* scale, float* gup, int* tracker, float* found, float world, float growth,
+                           float backoff, int interval, void* stream) {
+  amp_update_kernel<<<1, 64, 0, (hipStream_t)stream>>>(scale, gup, tracker, found, world, growth, backoff, interval);
+  return (int)hipGetLastError();
+}
+
 DMY_API int dmy_sgd(float* const* p, const float* const* g, float* const* m, const long* n, const int* tid,
-                    const long* off, int nchunks, float lr, float mom, float wd, int nesterov, int first,
-                    void* stream) {
+                    const long* off, int nchunks, float lr, float mom, float wd, int nesterov, const float* scale,
+                    const float* found, void* stream) {
   if (nchunks == 0) return 0;
   TList L{p, g, m, nullptr, n, tid, off};
-  sgd_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, mom, wd, nesterov, first);
+  sgd_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, mom, wd, nesterov, scale, found);
   return (int)hipGetLastError();
 }
 
 DMY_API int dmy_adam(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n,
                      const int* tid, const long* off, int nchunks, float lr, float b1, float b2, float eps, float wd,
-                     float bc1, float bc2s, void* stream) {
+                     float bc1, float bc2s, const float* scale, const float* found, void* stream) {
   if (nchunks == 0) return 0;
   TList L{p, g, m, v, n, tid, off};
-  adam_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, b1, b2, eps, wd, bc1, bc2s);
+  adam_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, b1, b2, eps, wd, bc1, bc2s, scale, found);
   return (int)hipGetLastError();
 }
 

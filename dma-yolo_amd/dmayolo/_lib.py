@@ -27,6 +27,8 @@ SIGNATURES = {
     'dmy_image_s2d': [I, I, P, P, I, I, I, I, I, F, P],
     'dmy_conv_fwd_act': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P, P, I, P, L, P],
     'dmy_conv_wgrad_ex': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P],
+    'dmy_conv_wgrad_ws_elems': [I, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I],
+    'dmy_conv_wgrad_det': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P, L, P],
     'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
     'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, I, P],
     # bn.hip
@@ -66,10 +68,12 @@ SIGNATURES = {
     # detect_loss.hip
     'dmy_detect_decode': [I, P, L, L, L, I, I, I, I, I, F, P, P, L, L, P],
     'dmy_build_targets': [P, I, P, I, I, I, F, P, P, P, P, P, P, P, P, P],
+    'dmy_yolo_loss_part_rows': [],
     'dmy_yolo_loss_level': [I, P, L, L, L, L, I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P,
-                            I, P, P, P, P],
+                            I, P, P, P, P, P, P],
     'dmy_yolo_loss_finalize': [P, I, F, F, F, F, P, P, P],
     'dmy_loss_grad': [I, P, P, P, L, P],
+    'dmy_siou_eval': [P, P, P, P, I, P],
     # tal.hip
     'dmy_tal_workspace_bytes': [I, I, I],
     'dmy_tal_loss': [I, P, L, L, L, P, L, L, L, I, I, I, P, P, P, P, I, F, F, F, P, P, P, P, P],
@@ -87,7 +91,8 @@ SIGNATURES = {
     'dmy_mha_fwd': [I, P, L, P, L, P, L, P, L, P, I, I, I, I, F, P],
     'dmy_mha_fwd_ref': [I, P, L, P, L, P, L, P, L, P, I, I, I, I, F, P],
     'dmy_mha_bwd': [I, P, L, P, L, P, L, P, P, L, P, P, P, P, P, I, I, I, I, F, P],
-    'dmy_dropout': [I, P, L, P, L, L, I, F, ctypes.c_ulonglong, P],
+    'dmy_dropout_seed': [P, P, P],
+    'dmy_dropout': [I, P, L, P, L, L, I, F, P, P],
     # nms.hip
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
@@ -117,7 +122,7 @@ def _load():
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError = stale build: fail loudly
         fn.argtypes = argt
-        fn.restype = ctypes.c_long if name.endswith('_bytes') else ctypes.c_int
+        fn.restype = ctypes.c_long if name.endswith(('_bytes', '_elems')) else ctypes.c_int
     return lib
 
 
@@ -126,7 +131,7 @@ lib = _load()
 
 def call(name, *args):
     rc = getattr(lib, name)(*args)
-    if name.endswith(('_rows', '_blocks', '_groups', '_bytes')):
+    if name.endswith(('_rows', '_blocks', '_groups', '_bytes', '_elems')):
         return rc
     if rc != 0:
         raise RuntimeError(f'{name} failed with hipError {rc}')

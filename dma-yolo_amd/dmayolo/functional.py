@@ -108,6 +108,26 @@ def sink_result(sink, buf):
 # ------------------------------------------------------------------ convolution (+BN +act)
 
 WGRAD_OIHW, WGRAD_ZEROED = 1, 2  # dmy_conv_wgrad_ex flags
+DETERMINISTIC = [False]  # set_deterministic(): split-K weight-grads through a workspace, reduced in split order
+
+
+def set_deterministic(on=True):
+    """Run-to-run bit-identical training steps on the conv / loss path: weight-gradient split-K partials go to a
+    workspace reduced in split order (dmy_conv_wgrad_det) instead of fp32 atomics.  The loss kernels are always
+    deterministic.  Costs one workspace write + read per split-K weight-grad launch."""
+    DETERMINISTIC[0] = bool(on)
+
+
+def _wgrad(dt, x, dz, dw, N, H, W, C, xps, K, k, s, p, OH, OW, dzps, flags, fl, **kw):
+    """one weight-gradient launch (atomic split-K, or the deterministic workspace form)"""
+    if DETERMINISTIC[0]:
+        ne = call('dmy_conv_wgrad_ws_elems', dt, ptr(x), ptr(dz), N, H, W, C, xps, K, k, k, s, p, OH, OW, dzps, flags)
+        ws = f32(ne, dz.device) if ne else None
+        KernelTimer.run('conv_wgrad', fl, 'dmy_conv_wgrad_det', dt, ptr(x), ptr(dz), ptr(dw), N, H, W, C, xps, K, k, k,
+                        s, p, OH, OW, dzps, flags, ptr(ws), ne, stream(), **kw)
+    else:
+        KernelTimer.run('conv_wgrad', fl, 'dmy_conv_wgrad_ex', dt, ptr(x), ptr(dz), ptr(dw), N, H, W, C, xps, K, k, k,
+                        s, p, OH, OW, dzps, flags, stream(), **kw)
 
 
 class WgradArena:
@@ -247,17 +267,21 @@ class KernelTimer:
         cls.records.append((kind, flops, nbytes, e0, e1, tag))
 
     @classmethod
-    def summary(cls, detail=None):
-        """per-kind totals; when `detail` is a dict it also receives per-(kind, shape) totals"""
+    def summary(cls, detail=None, peak_flops=2.5e15, peak_bw=8.0e12):
+        """Per-kind totals: launches, flops, seconds, bytes, and the roofline time sum_launches max(F / peak_flops,
+        B / peak_bw) split by the binding resource (troof_mfma / troof_hbm).  When `detail` is a dict it also
+        receives per-(kind, shape) [launches, flops, seconds, bytes]."""
         torch.cuda.synchronize()
         out = {}
         for kind, fl, nb, e0, e1, tag in cls.records:
             t = e0.elapsed_time(e1) * 1e-3
-            d = out.setdefault(kind, [0, 0.0, 0.0, 0.0])
+            tm, th = fl / peak_flops, nb / peak_bw
+            d = out.setdefault(kind, [0, 0.0, 0.0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += fl
             d[2] += t
             d[3] += nb
+            d[4 if tm >= th else 5] += max(tm, th)
             if detail is not None:
                 d = detail.setdefault((kind, tag), [0, 0.0, 0.0, 0.0])
                 d[0] += 1
@@ -265,7 +289,8 @@ class KernelTimer:
                 d[2] += t
                 d[3] += nb
         cls.records = []
-        return {k: dict(launches=v[0], flops=v[1], seconds=v[2], bytes=v[3]) for k, v in out.items()}
+        return {k: dict(launches=v[0], flops=v[1], seconds=v[2], bytes=v[3], troof_mfma=v[4], troof_hbm=v[5])
+                for k, v in out.items()}
 
 
 def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka, epi=None):
@@ -479,9 +504,8 @@ class ConvBNActFn(torch.autograd.Function):
             Cs = ctx.s2d
             H2, W2 = ctx.ggeom[:2]
             dwo = f32(K * 9 * Cs, dev)
-            KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz), ptr(dwo), N,
-                            H2, W2, Cs, xps, K, 3, 3, 1, 1, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
-                            nbytes=z.element_size() * (N * H2 * W2 * Cs + M * K) + 4 * K * Cs * 9)
+            _wgrad(dt, x, dz, dwo, N, H2, W2, Cs, xps, K, 3, 1, 1, OH, OW, dzps, 0, 2.0 * M * K * C * k * k,
+                   tag=(N, C, H, W, K, k, s), nbytes=z.element_size() * (N * H2 * W2 * Cs + M * K) + 4 * K * Cs * 9)
             dw = ctx.arena.take(ctx.wkey, (K, C, k, k)) if ctx.arena is not None else None
             if dw is None:
                 dw = torch.empty((K, C, k, k), dtype=torch.float32, device=dev)
@@ -495,14 +519,12 @@ class ConvBNActFn(torch.autograd.Function):
             if k == 1 and Cp == C:
                 # 1x1: the GEMM view IS torch OIHW -> accumulate straight into the step's zeroed arena slice
                 flags = WGRAD_OIHW | (WGRAD_ZEROED if zeroed else 0)
-                KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad_ex', dt, ptr(x), ptr(dz),
-                                ptr(dw), N, H, W, C, xps, K, k, k, s, p, OH, OW, dzps, flags, stream(), **wkw)
+                _wgrad(dt, x, dz, dw, N, H, W, C, xps, K, k, s, p, OH, OW, dzps, flags, 2.0 * M * K * C * k * k, **wkw)
             else:
                 # k > 1: OIHW-order atomics would scatter every tile row with stride k*k (measured 1.5x slower
                 # weight-grad on yolov5s); accumulate in GEMM order, then one layout pass (drops stem padding)
                 dwo = f32(K * Cp * k * k, dev)
-                KernelTimer.run('conv_wgrad', 2.0 * M * K * C * k * k, 'dmy_conv_wgrad', dt, ptr(x), ptr(dz),
-                                ptr(dwo), N, H, W, Cp, xps, K, k, k, s, p, OH, OW, dzps, stream(), **wkw)
+                _wgrad(dt, x, dz, dwo, N, H, W, Cp, xps, K, k, s, p, OH, OW, dzps, 0, 2.0 * M * K * C * k * k, **wkw)
                 call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, Cp, k, k, stream())
         dres = None
         if ctx.has_res:
@@ -902,22 +924,32 @@ class MHAFn(torch.autograd.Function):
         return dq, dk, dv, None
 
 
-def _seed():
-    """a fresh 63-bit dropout seed from torch's CPU generator (no device sync)"""
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64))
+_DROP_STATE = {}
+
+
+def _seed(dev):
+    """A fresh dropout seed in device memory: dmy_dropout_seed advances a per-device generator state (seeded
+    once from torch's CPU generator) on the stream, so a HIP-graph replay of the step draws a new mask each
+    time instead of replaying the captured one.  Returns the [1] int64 seed tensor the kernels read."""
+    st = _DROP_STATE.get(dev)
+    if st is None:
+        st = _DROP_STATE[dev] = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
+    seed = torch.empty(1, dtype=torch.int64, device=dev)
+    call('dmy_dropout_seed', ptr(st), ptr(seed), stream())
+    return seed
 
 
 class DropoutFn(torch.autograd.Function):
     """nn.Dropout(p) in train mode (common.py:328): y = x * keep / (1 - p); the keep mask is a counter
-    hash of (seed, element index), regenerated in the backward."""
+    hash of (seed, element index), regenerated in the backward from the same device-resident seed."""
 
     @staticmethod
     def forward(ctx, x, p):
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
         y = new_act(N, C, H, W, x)
-        seed = _seed()
-        call('dmy_dropout', dcode(x), ptr(x), xps, ptr(y), C, N * H * W, C, float(p), seed, stream())
+        seed = _seed(x.device)
+        call('dmy_dropout', dcode(x), ptr(x), xps, ptr(y), C, N * H * W, C, float(p), ptr(seed), stream())
         ctx.p, ctx.seed = p, seed
         return y
 
@@ -926,7 +958,7 @@ class DropoutFn(torch.autograd.Function):
         dy, dps = pixel_stride(dy)
         N, C, H, W = dy.shape
         dx = new_act(N, C, H, W, dy)
-        call('dmy_dropout', dcode(dy), ptr(dy), dps, ptr(dx), C, N * H * W, C, float(ctx.p), ctx.seed, stream())
+        call('dmy_dropout', dcode(dy), ptr(dy), dps, ptr(dx), C, N * H * W, C, float(ctx.p), ptr(ctx.seed), stream())
         return dx, None
 
 

@@ -16,10 +16,12 @@ lib.dmy_chunk_size.restype = ctypes.c_int
 lib.dmy_chunk_size.argtypes = []
 CHUNK = lib.dmy_chunk_size()
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
-lib.dmy_sgd.argtypes = [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]
-lib.dmy_adam.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _P]
+lib.dmy_sgd.argtypes = [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _P, _P, _P]
+lib.dmy_adam.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P]
 lib.dmy_ema.argtypes = [_P, _P, _P, _P, _P, _I, _F, _P]
-for _f in (lib.dmy_sgd, lib.dmy_adam, lib.dmy_ema):
+lib.dmy_amp_check.argtypes = [_P, _P, _P, _P, _I, _P, _P, _P]
+lib.dmy_amp_update.argtypes = [_P, _P, _P, _P, _F, _F, _F, _I, _P]
+for _f in (lib.dmy_sgd, lib.dmy_adam, lib.dmy_ema, lib.dmy_amp_check, lib.dmy_amp_update):
     _f.restype = ctypes.c_int
 
 
@@ -65,6 +67,12 @@ def _check(rc, name):
         raise RuntimeError(f'{name} failed with hipError {rc}')
 
 
+def _amp_ptrs(opt):
+    """(scale, found) device pointers while a GradScaler.step() runs this optimizer, else (None, None)"""
+    amp = getattr(opt, '_amp', None)
+    return (None, None) if amp is None else (ctypes.c_void_p(amp[0].data_ptr()), ctypes.c_void_p(amp[1].data_ptr()))
+
+
 class FusedSGD(torch.optim.Optimizer):
     def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, nesterov=False):
         super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov))
@@ -77,17 +85,16 @@ class FusedSGD(torch.optim.Optimizer):
                 continue
             for p in ps:
                 assert p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
-            first = 'momentum_buffer' not in self.state[ps[0]]
             bufs = []
             for p in ps:
                 st = self.state[p]
-                if 'momentum_buffer' not in st:
-                    st['momentum_buffer'] = torch.empty_like(p)
+                if 'momentum_buffer' not in st:  # per parameter: a grad that first appears later starts at zero
+                    st['momentum_buffer'] = torch.zeros_like(p)
                 bufs.append(st['momentum_buffer'])
             tb = _Table.get([ps, [p.grad for p in ps], bufs], ps[0].device)
             PARAM_GEN[0] += 1
             _check(lib.dmy_sgd(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.nchunks, float(g['lr']),
-                               float(g['momentum']), float(g['weight_decay']), int(g['nesterov']), int(first),
+                               float(g['momentum']), float(g['weight_decay']), int(g['nesterov']), *_amp_ptrs(self),
                                stream()), 'dmy_sgd')
         return None
 
@@ -120,8 +127,51 @@ class FusedAdam(torch.optim.Optimizer):
             PARAM_GEN[0] += 1
             _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
                                 float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
-                                float(bc1), float(bc2s), stream()), 'dmy_adam')
+                                float(bc1), float(bc2s), *_amp_ptrs(self), stream()), 'dmy_adam')
         return None
+
+
+class GradScaler:
+    """torch.amp.GradScaler as train.py uses it (train.py:354 GradScaler(enabled=cuda); 445 scale(loss).backward();
+    449-450 step / update) with its state on the device: loss scale (init 2**16, growth 2 every 2000 clean steps,
+    backoff 0.5), growth tracker and the non-finite flag.  step() runs one check kernel over every gradient, then
+    the optimizer kernels unscale on the fly and skip themselves when a gradient was non-finite -- no host sync.
+    `upstream` is the loss's backward seed: scale * world (loss *= WORLD_SIZE, train.py:438-440, folded in).
+    Disabled: upstream = world, step() = optimizer.step().  Unlike torch, the .grad tensors keep the scaled
+    values after step() (unscaling is fused into the update)."""
+
+    def __init__(self, device, enabled=True, world=1, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5,
+                 growth_interval=2000):
+        self.enabled, self.world = enabled, float(world)
+        self.growth, self.backoff, self.interval = growth_factor, backoff_factor, growth_interval
+        s = init_scale if enabled else 1.0
+        self.scale = torch.full((1,), s, dtype=torch.float32, device=device)
+        self.upstream = torch.full((1,), s * world, dtype=torch.float32, device=device)
+        self.tracker = torch.zeros(1, dtype=torch.int32, device=device)
+        self.found = torch.zeros(1, dtype=torch.float32, device=device)
+
+    def step(self, optimizer):
+        if not self.enabled:
+            return optimizer.step()
+        gs = [p.grad for g in optimizer.param_groups for p in g['params'] if p.grad is not None]
+        if gs:
+            tb = _Table.get([gs], gs[0].device)
+            _check(lib.dmy_amp_check(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.nchunks, ctypes.c_void_p(self.scale.data_ptr()),
+                                     ctypes.c_void_p(self.found.data_ptr()), stream()), 'dmy_amp_check')
+        optimizer._amp = (self.scale, self.found)
+        try:
+            return optimizer.step()
+        finally:
+            optimizer._amp = None
+
+    def update(self):
+        if self.enabled:
+            P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+            _check(lib.dmy_amp_update(P(self.scale), P(self.upstream), P(self.tracker), P(self.found), self.world,
+                                      self.growth, self.backoff, self.interval, stream()), 'dmy_amp_update')
+
+    def get_scale(self):
+        return float(self.scale)  # host sync: logging only
 
 
 def ema_update(ema_tensors, model_tensors, d):

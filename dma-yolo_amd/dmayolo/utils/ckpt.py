@@ -42,17 +42,17 @@ def save_checkpoint(path, model, ema=None, optimizer=None, epoch=-1, best_fitnes
     return ckpt
 
 
-def load_weights(model, path_or_sd, exclude=(), key=None):
+def load_weights(model, path_or_sd, exclude=(), key='model'):
     """Transfer weights into `model` as train.py:148-156 does (intersect_dicts on matching keys / shapes);
     returns the number of tensors loaded.  `path_or_sd`: a state_dict, or a file holding one or a ckpt dict
-    written by save_checkpoint (read with weights_only=True)."""
+    written by save_checkpoint (read with weights_only=True).  From a ckpt dict the `key` entry is taken:
+    'model' as the reference's pretrained / resume path (train.py:148-156: ckpt['model']); attempt_load
+    passes 'ema' (models/experimental.py:128)."""
     sd = path_or_sd
     if not isinstance(sd, dict):
         sd = torch.load(sd, map_location='cpu', weights_only=True)
-    if key is None and 'model' in sd and isinstance(sd['model'], dict):
-        key = 'ema' if sd.get('ema') else 'model'
-    if key is not None:
-        sd = sd[key]
+    if isinstance(sd.get('model'), dict):  # a ckpt dict, not a bare state_dict
+        sd = sd[key] if sd.get(key) is not None else sd['model']
     sd = {k: v.float() if v.is_floating_point() else v for k, v in sd.items()}
     csd = intersect_dicts(sd, model.state_dict(), exclude=exclude)
     model.load_state_dict(csd, strict=False)
@@ -64,7 +64,7 @@ def attempt_load(path, device='cuda', fuse=True, act_dtype=torch.float32):
     load 'ema' if present else 'model' (fp32), fuse BN into the YAML Conv layers, eval mode."""
     ckpt = torch.load(path, map_location='cpu', weights_only=True)
     model = Model(ckpt['yaml'], act_dtype=act_dtype)
-    load_weights(model, ckpt)
+    load_weights(model, ckpt, key='ema')  # ckpt['ema'] or ckpt['model'] (experimental.py:128)
     model = model.to(device)
     if fuse:
         model.fuse()

@@ -41,7 +41,8 @@ class _YoloLossFn(torch.autograd.Function):
         nt = t.shape[0]
         h = cl.hyp
         nl = len(p)
-        acc = torch.zeros(nl * 3, dtype=torch.float32, device=dev)
+        PR = call('dmy_yolo_loss_part_rows')
+        part = torch.zeros(nl * PR, dtype=torch.float32, device=dev)  # per-block partials, fixed-order reduction
         Gs = []
         bs = p[0].shape[0]
         for i, pi in enumerate(p):
@@ -50,16 +51,18 @@ class _YoloLossFn(torch.autograd.Function):
             ii, tbox, anch, cnt, cap = _build_level(t, nt, cl.anchors[i], na, H, W, h['anchor_t'], dev)
             G = torch.zeros_like(pi, dtype=torch.float32)
             tobj = torch.zeros(N * na * H * W, dtype=torch.float32, device=dev)
+            tgrad = torch.empty((cap, 4 + (cl.nc if cl.nc > 1 else 0)), dtype=torch.float32, device=dev)
+            links = torch.empty(N * na * H * W + cap, dtype=torch.int32, device=dev)
             s = pi.stride()
             call('dmy_yolo_loss_level', dcode(pi), ptr(pi), s[0], s[1], s[2], s[3], N, na, H, W, no, cl.nc,
                  float(h['box']), float(h['obj']), float(h['cls']), float(h['cls_pw']), float(h['obj_pw']),
                  float(cl.cp), float(cl.cn), float(cl.balance[i]), float(bs), ptr(ii[0]), ptr(ii[1]), ptr(ii[2]),
-                 ptr(ii[3]), ptr(ii[4]), ptr(tbox), ptr(anch), ptr(cnt), cap, ptr(G), ptr(tobj), ptr(acc[3 * i:]),
-                 stream())
+                 ptr(ii[3]), ptr(ii[4]), ptr(tbox), ptr(anch), ptr(cnt), cap, ptr(G), ptr(tobj), ptr(part[PR * i:]),
+                 ptr(tgrad), ptr(links), stream())
             Gs.append(G)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
         items = torch.empty(3, dtype=torch.float32, device=dev)
-        call('dmy_yolo_loss_finalize', ptr(acc), nl, float(h['box']), float(h['obj']), float(h['cls']), float(bs),
+        call('dmy_yolo_loss_finalize', ptr(part), nl, float(h['box']), float(h['obj']), float(h['cls']), float(bs),
              ptr(loss), ptr(items), stream())
         ctx.Gs = Gs
         ctx.dtypes = [pi.dtype for pi in p]

@@ -41,6 +41,14 @@ int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int
  *        2 = dw is already zero (a per-step gradient arena cleared once), skip the memset.  Same sums as above. */
 int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C, long xps, int K,
                       int KH, int KW, int S, int P, int OH, int OW, long yps, int flags, void* stream);
+/* Deterministic weight-grad (same sums, run-to-run bit-identical): the split-K partials go to the fp32 workspace
+ * ws (no atomics) and are reduced in split order.  dmy_conv_wgrad_ws_elems: workspace elements the same call needs
+ * (0 = one split, ws may be NULL). */
+long dmy_conv_wgrad_ws_elems(int dtype, const void* x, const void* dy, int N, int H, int W, int C, long xps, int K,
+                             int KH, int KW, int S, int P, int OH, int OW, long yps, int flags);
+int dmy_conv_wgrad_det(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C, long xps,
+                       int K, int KH, int KW, int S, int P, int OH, int OW, long yps, int flags, float* ws,
+                       long ws_elems, void* stream);
 /* Cp >= C: input channels zero-padded to a full 16-byte vector (the 3-channel stem, yaml:15) */
 int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w_ihwo, int K, int C, int Cp, int KH, int KW,
                    void* stream);
@@ -134,14 +142,20 @@ int dmy_detect_decode(int dtype, const void* y, long sb, long sh, long sw, int N
 int dmy_build_targets(const float* targets, int nt, const float* anchors, int na, int H, int W, float anchor_t,
                       int* b, int* a, int* gj, int* gi, int* tcls, float* tbox, float* anch, int* count,
                       void* stream);
+/* per level: part = dmy_yolo_loss_part_rows() fp32 block partials (caller-zeroed), G / tobj caller-zeroed;
+ * workspaces tgrad [cap][4 + nc] fp32 and links [N*na*H*W + cap] int32 (no float atomics: deterministic) */
+int dmy_yolo_loss_part_rows(void);
 int dmy_yolo_loss_level(int dtype, const void* p, long sb, long sa, long sh, long sw, int N, int na, int H, int W,
                         int no, int nc, float box_gain, float obj_gain, float cls_gain, float cls_pw, float obj_pw,
                         float cp, float cn, float balance, float bs, const int* b, const int* a, const int* gj,
                         const int* gi, const int* tcls, const float* tbox, const float* anch, const int* count,
-                        int cap, float* grad, float* tobj, float* acc3, void* stream);
-int dmy_yolo_loss_finalize(const float* acc, int nl, float box, float obj, float cls, float bs, float* loss,
+                        int cap, float* grad, float* tobj, float* part, float* tgrad, int* links, void* stream);
+int dmy_yolo_loss_finalize(const float* part, int nl, float box, float obj, float cls, float bs, float* loss,
                            float* items, void* stream);
 int dmy_loss_grad(int dtype, const float* grad, const float* upstream, void* dp, long n, void* stream);
+/* SIoU (utils/metrics.py:192-235, bbox_iou(..., x1y1x2y2=False, SIoU=True)) of n xywh pairs through the
+ * loss kernel's device function: iou [n] and d iou / d b1 [n][4] (forward-mode duals). */
+int dmy_siou_eval(const float* b1, const float* b2, float* iou, float* grad_b1, int n, void* stream);
 
 /* ---- non_max_suppression (utils/general.py:633-725 -> torchvision.ops.nms at :708) */
 int dmy_nms_candidates(const float* pred, int nimg, int A, int no, float conf, int multi_label,
@@ -166,13 +180,22 @@ int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const float* t
                     float* dtab, int B, int H, int W, int C, int nh, int shift, float scale, void* stream);
 int dmy_sample_scale(int dtype, const void* x, const float* scale, void* y, long per, long n, void* stream);
 
-/* ---- optimizer step / EMA (train.py:216-222, 449-454; utils/torch_utils.py:329-339) */
+/* ---- optimizer step / EMA (train.py:216-222, 449-454; utils/torch_utils.py:329-339) and the GradScaler
+ *      (train.py:354, 445-450).  scale / found: device [1] fp32 loss scale and non-finite flag, or both NULL
+ *      (scaler disabled); the update is skipped on the device when *found != 0 (scaler.step). */
 int dmy_chunk_size(void);
 int dmy_sgd(float* const* p, const float* const* g, float* const* m, const long* n, const int* tid, const long* off,
-            int nchunks, float lr, float momentum, float weight_decay, int nesterov, int first, void* stream);
+            int nchunks, float lr, float momentum, float weight_decay, int nesterov, const float* scale,
+            const float* found, void* stream);
 int dmy_adam(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n, const int* tid,
              const long* off, int nchunks, float lr, float beta1, float beta2, float eps, float weight_decay,
-             float bias_corr1, float bias_corr2_sqrt, void* stream);
+             float bias_corr1, float bias_corr2_sqrt, const float* scale, const float* found, void* stream);
+/* scaler.unscale_ check: *found = 1 if any g * (1 / *scale) is non-finite (found is not cleared here) */
+int dmy_amp_check(const float* const* g, const long* n, const int* tid, const long* off, int nchunks,
+                  const float* scale, float* found, void* stream);
+/* scaler.update(): backoff / growth of *scale, *gup = *scale * world (the loss's upstream gradient), re-arms found */
+int dmy_amp_update(float* scale, float* gup, int* tracker, float* found, float world, float growth, float backoff,
+                   int interval, void* stream);
 int dmy_ema(float* const* ema, const float* const* src, const long* n, const int* tid, const long* off, int nchunks,
             float decay, void* stream);
 
@@ -226,9 +249,12 @@ int dmy_mha_fwd_ref(int dtype, const void* q, long qps, const void* k, long kps,
 int dmy_mha_bwd(int dtype, const void* q, long qps, const void* k, long kps, const void* v, long vps, const void* o,
                 const void* dout, long ops, const float* lse2, float* Dq, void* dq, void* dk, void* dv, int B, int L,
                 int nh, int d, float scale, void* stream);
-/* y[m][c] = x[m][c] * (u(seed, m * C + c) >= p) / (1 - p); the same call with the same seed on dy is the backward */
-int dmy_dropout(int dtype, const void* x, long xps, void* y, long yps, long M, int C, float p, unsigned long long seed,
-                void* stream);
+/* y[m][c] = x[m][c] * (u(*seed, m * C + c) >= p) / (1 - p); the same call with the same seed on dy is the backward.
+ * seed is device memory (graph-replay safe); dmy_dropout_seed advances a device generator state and writes a
+ * fresh seed (nn.Dropout's per-call RNG draw, common.py:328). */
+int dmy_dropout_seed(unsigned long long* state, unsigned long long* seed, void* stream);
+int dmy_dropout(int dtype, const void* x, long xps, void* y, long yps, long M, int C, float p,
+                const unsigned long long* seed, void* stream);
 
 /* ---- validation matching: replaces process_batch (val.py:62-83) with box_iou (utils/metrics.py:254-276) for
  *      a batch of images in one launch.  det [ND][6] (x1 y1 x2 y2 conf cls), lab [NL][5] (cls x1 y1 x2 y2),

@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     src = open(os.path.join(ROOT, 'include', 'dmayolo.h')).read()
-    return sorted(set(re.findall(r'^\s*int\s+(dmy_\w+)\s*\(', src, re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|long)\s+(dmy_\w+)\s*\(', src, re.M)))
 
 
 def test_header_nonempty():
@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
 def test_bindings_cover_header():
     from dmayolo import _lib
     import dmayolo.optim  # noqa: F401  (binds the optimizer symbols)
-    extra = {'dmy_chunk_size', 'dmy_sgd', 'dmy_adam', 'dmy_ema'}
+    extra = {'dmy_chunk_size', 'dmy_sgd', 'dmy_adam', 'dmy_ema', 'dmy_amp_check', 'dmy_amp_update'}
     unbound = [s for s in header_symbols() if s not in _lib.SIGNATURES and s not in extra]
     assert not unbound, unbound
 

@@ -47,3 +47,23 @@ def test_save_checkpoint_attempt_load_round_trip(tmp_path):
     assert load_weights(m3, p, exclude=('anchor',)) == len([k for k in m3.state_dict() if 'anchor' not in k])
     fused = attempt_load(p, device='cpu', fuse=True)
     assert not any(hasattr(mm, 'bn') for mm in fused.model if type(mm).__name__ == 'Conv')
+
+
+def test_load_weights_takes_model_entry_attempt_load_takes_ema(tmp_path):
+    """train.py:148-156 transfers ckpt['model']; attempt_load (experimental.py:128) prefers ckpt['ema']."""
+    from dmayolo.utils.ckpt import save_checkpoint, attempt_load, load_weights
+    from dmayolo.utils.torch_utils import ModelEMA
+    fx, m = _model('model_v5s')
+    load_sd(m, fx.group('sd'))
+    ema = ModelEMA(m)
+    with torch.no_grad():
+        for q in ema.ema.parameters():
+            q.add_(1.0)
+    p = str(tmp_path / 'last.pt')
+    save_checkpoint(p, m, ema=ema, half=False)
+    _, m2 = _model('model_v5s')
+    load_weights(m2, p)
+    k = 'model.0.conv.weight'
+    torch.testing.assert_close(m2.state_dict()[k], m.state_dict()[k], rtol=0, atol=0)
+    m3 = attempt_load(p, device='cpu', fuse=False)
+    torch.testing.assert_close(m3.state_dict()[k], ema.ema.state_dict()[k], rtol=0, atol=0)

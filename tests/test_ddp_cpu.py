@@ -1,8 +1,8 @@
-"""CPU, world_size 2 over gloo: the data-parallel training step of bench.py (train.py:400-454 +
-DDP at train.py:326) shards images by rank and applies the SUM of the per-rank gradients
-(loss * WORLD_SIZE, DDP averaging, train.py:440).  The model here is the CPU oracle: the
-product modules need the GPU; what is checked is the sharding / exchange / step logic that
-bench.py runs over RCCL on the GPU box."""
+"""CPU, world_size 2 over gloo: the data-parallel step of dmayolo.trainer.Trainer (train.py:400-454 + DDP at
+train.py:326) shards images by rank and applies the SUM of the per-rank gradients (the backward is seeded with
+WORLD_SIZE, train.py:440, and DDP averages).  The model here is the CPU oracle, stepped the way Trainer.step does
+(loss.backward(upstream = scale * WORLD_SIZE), scale 1 without a GPU); the product Model / ComputeLoss / FusedSGD
+under DDP is the GPU test tests/test_gpu_ddp.py (two gloo ranks on cuda:0)."""
 import os
 import socket
 import sys
@@ -51,12 +51,13 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    import bench
     model = _model()
     net = torch.nn.parallel.DistributedDataParallel(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, nesterov=True)
     x, t = _batch(rank)
-    loss = bench.train_step(net, model, _loss_fn(model), opt, None, x, t, world)
+    loss, _ = _loss_fn(model)(net(x), t)
+    loss.backward(torch.full((1,), float(world)))  # Trainer.step: GradScaler.upstream = scale * WORLD_SIZE
+    opt.step()
     assert torch.isfinite(loss).all()
     if rank == 0:
         torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, out)

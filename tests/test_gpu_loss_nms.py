@@ -67,13 +67,22 @@ def test_loss_no_targets():
     assert float(items[0]) == 0.0 and float(items[2]) == 0.0
 
 
-def test_siou_gradients_vs_golden():
-    """SIoU through the loss kernel's dual numbers equals torch autograd of the reference formula."""
+def test_siou_kernel_vs_golden():
+    """The loss kernel's SIoU device function (forward-mode dual numbers, csrc/detect_loss.hip) through the
+    C ABI (dmy_siou_eval) against the reference's bbox_iou(..., SIoU=True) value and its autograd gradient
+    w.r.t. the predicted box (tools/gen_golden.py gen_siou: incl. near-coincident centres and
+    sin_alpha == 1 rows)."""
+    from dmayolo.functional import call, ptr, stream
     fx = Fixture('siou')
-    from oracle.loss import siou
-    b1 = fx.t('b1')
-    ref = siou(b1, fx.t('b2'))
-    torch.testing.assert_close(ref, fx.t('iou'), equal_nan=True)
+    b1, b2 = fx.t('b1').cuda().contiguous(), fx.t('b2').cuda().contiguous()
+    n = b1.shape[0]
+    iou = torch.empty(n, device='cuda')
+    g = torch.empty(n, 4, device='cuda')
+    call('dmy_siou_eval', ptr(b1), ptr(b2), ptr(iou), ptr(g), n, stream())
+    ref_iou, ref_g = fx.t('iou'), fx.t('g')
+    torch.testing.assert_close(iou.cpu(), ref_iou, rtol=1e-5, atol=1e-6, equal_nan=True)
+    ok = torch.isfinite(ref_g).all(1)
+    torch.testing.assert_close(g.cpu()[ok], ref_g[ok], rtol=1e-3, atol=1e-4)
 
 
 @pytest.mark.parametrize('name', golden_names('nms_'))

@@ -133,3 +133,33 @@ def test_c3tr_bf16_vs_oracle(c, hw):
             continue
         err = float((gp[k].grad.float().cpu() - p.grad).norm()) / max(float(p.grad.norm()), 1e-2 * gmax)
         assert err < 8e-2, (k, err)
+
+
+def test_dropout_mask_redrawn_on_graph_replay():
+    """DropoutFn's seed is drawn on the device (dmy_dropout_seed), so a HIP graph that captured forward +
+    backward draws a fresh mask on every replay, and the backward of each replay uses that replay's mask."""
+    import dmayolo.functional as Fn
+    x = torch.randn(2, 64, 8, 8, device='cuda').contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    gup = torch.ones_like(x)
+    y = Fn.DropoutFn.apply(x, 0.5)  # eager warm-up (creates the generator state outside the capture)
+    y.backward(gup)
+    x.grad = None
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            sy = Fn.DropoutFn.apply(x, 0.5)
+            sy.backward(gup)
+    torch.cuda.current_stream().wait_stream(s)
+    masks = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        keep = sy.detach() != 0
+        assert torch.equal(keep, x.grad != 0)  # backward regenerated this replay's mask
+        torch.testing.assert_close(sy.detach()[keep], (x.detach() * 2)[keep])
+        masks.append(keep.clone())
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    frac = float(torch.stack(masks).float().mean())
+    assert 0.45 < frac < 0.55, frac

@@ -1,0 +1,94 @@
+"""GPU parity of the fused optimizer / EMA kernels (csrc/optim.hip) against the reference's own
+torch.optim.SGD(nesterov) / Adam and ModelEMA results captured in tests/golden/optim.npz
+(tools/gen_golden.py `gen_optim`): train.py:216-222 grouping (g0 BN weights, g1 weights +
+AdConcat.w with weight decay, g2 biases; Adam hard-codes g0 lr=3e-4), per-group lr / momentum
+written into param_groups as the warmup does (train.py:416-420), two steps; ModelEMA.update
+(utils/torch_utils.py:329-339) twice over params AND float buffers."""
+import pytest
+import torch
+
+from golden_util import Fixture, load_sd
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-6, atol=1e-7)  # fp32 kernels vs torch CPU: one rounding of an fma at most
+
+
+def _model(fx):
+    from dmayolo.models.yolo import Model
+    m = Model(fx.meta['yaml'], nc=10)
+    load_sd(m, fx.group('sd'))
+    return m.cuda()
+
+
+def _check_groups(opt, m, fx):
+    names = {id(p): k for k, p in m.named_parameters()}
+    got = [[names[id(p)] for p in g['params']] for g in opt.param_groups]
+    assert got == [fx.meta['groups'][k] for k in ('g0', 'g1', 'g2')]
+
+
+@pytest.mark.parametrize('kind', ['sgd', 'adam'])
+def test_fused_optimizer_matches_reference(kind):
+    from dmayolo.optim import build_optimizer
+    fx = Fixture('optim')
+    m = _model(fx)
+    opt = build_optimizer(m, kind, 0.01, 0.937, 0.0005)
+    _check_groups(opt, m, fx)
+    for j, g in enumerate(opt.param_groups):
+        g['lr'] = [0.001, 0.002, 0.05][j]
+        if 'momentum' in g:
+            g['momentum'] = 0.8
+    grads = fx.group('grad')
+    params = dict(m.named_parameters())
+    for step in range(2):
+        for k, p in params.items():
+            p.grad = (grads[k] * (1 + step)).cuda()
+        opt.step()
+    exp = fx.group(kind)
+    assert set(exp) == set(params)
+    for k, p in params.items():
+        torch.testing.assert_close(p.detach().cpu(), exp[k], **TOL, msg=lambda s: f'{kind} {k}: {s}')
+
+
+def test_fused_sgd_late_parameter_starts_from_zero_momentum():
+    """A parameter whose grad first appears at step 2 gets torch's clone-on-first-step buffer (no stale
+    momentum from uninitialised memory)."""
+    from dmayolo.optim import FusedSGD
+    torch.manual_seed(0)
+    a = torch.nn.Parameter(torch.randn(3000, device='cuda'))
+    b = torch.nn.Parameter(torch.randn(5000, device='cuda'))
+    ra, rb = [torch.nn.Parameter(t.detach().cpu().clone()) for t in (a, b)]
+    opt = FusedSGD([a, b], lr=0.1, momentum=0.9, nesterov=True)
+    ref = torch.optim.SGD([ra, rb], lr=0.1, momentum=0.9, nesterov=True)
+    ga, gb = torch.randn(3000), torch.randn(5000)
+    a.grad, ra.grad = ga.cuda(), ga.clone()
+    opt.step()
+    ref.step()
+    a.grad, b.grad, ra.grad, rb.grad = ga.cuda(), gb.cuda(), ga.clone(), gb.clone()
+    opt.step()
+    ref.step()
+    for p, r in ((a, ra), (b, rb)):
+        torch.testing.assert_close(p.detach().cpu(), r.detach(), **TOL)
+
+
+def test_model_ema_matches_reference():
+    from dmayolo.utils.torch_utils import ModelEMA
+    fx = Fixture('optim')
+    m = _model(fx)
+    ema = ModelEMA(m)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.1)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.add_(0.2)
+    ema.update(m)
+    ema.update(m)
+    got = ema.ema.state_dict()
+    exp = fx.group('ema')
+    assert set(exp) == set(got)
+    for k, v in exp.items():
+        g = got[k].cpu()
+        if v.dtype.is_floating_point:
+            torch.testing.assert_close(g, v, **TOL, msg=lambda s: f'ema {k}: {s}')
+        else:
+            assert torch.equal(g.to(v.dtype), v), k
