@@ -284,8 +284,8 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     ndev = torch.cuda.device_count()
     dev_idx = local % max(ndev, 1)
+    torch.cuda.set_device(dev_idx)
     if world > 1:
-        torch.cuda.set_device(dev_idx)
         if a.backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev_idx))
         else:

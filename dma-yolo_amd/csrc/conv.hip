@@ -1795,6 +1795,185 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
     if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
   }
 }
+
+// ---------------------------------------------------------------- tap-fused 3x3 stride-1 weight-grad
+// C[m = out channel][n = (tap, ci)] = sum over output pixels p of dy[p][m] * x[p + tap shift][ci], for a block tile
+// of 128 out channels x (all 9 taps x 32 input channels) = 288 columns.  The reduction walks 8 x 8 output-pixel
+// patches (64 pixels per K step): the x operand is the patch's 10 x 10 halo (32 channels) loaded ONCE and read by
+// all 9 taps through shifted LDS addresses, so x is fetched ~1.6x per (out-channel tile) and dy once per 32-channel
+// group -- vs 9x / 18x for the (tap, channel)-column tiles of conv_wgrad_v3/v4.
+//   A (dy): [64 pixel rows][BM ch] k-major, the kmaj_off<BM> swizzle, frag_k<BM> (as conv_wgrad_v3 / v3n);
+//   BM = 128, or 64 for layers with <= 64 output channels.
+//   B (x halo): 10 rows of pitch 12 pixels x 32 ch (64-B rows), chunk ^ 2 (halo row y & 1): the 8 rows one
+//   ds_read_b64_tr_b16 group touches ((y, x .. x + 3), (y + 1, x .. x + 3)) then hit 64 distinct banks.
+//   Stages: BM/8 KiB A + 8 KiB B (120 of 128 halo rows used), 3-stage LDS-DMA ring, a counted vmcnt keeps one
+//   stage in flight across each barrier.  4 waves = 2 (m) x 2 (n), wave tile BM/2 x 144 (BM/32 x 9 MFMA frags).
+// Valid for KH = KW = 3, S = 1, P = 1, OH = H, OW = W, C % 32 == 0 (host-checked).  Split-K over patches; the
+// (tile, split) -> linear id mapping keeps a split's tiles on one XCD (they read the same patches).
+template <int BM>
+struct WgradTapLds {
+  static constexpr int BC = 32, PH = 8, PW = 8, HP = 12;  // halo pitch 12 (10 used)
+  static constexpr int A_BYTES = 64 * BM * 2, B_BYTES = 8 * 1024, STAGE = A_BYTES + B_BYTES;
+  static constexpr int APW = A_BYTES / 1024 / 4;           // dy pieces per wave (4 waves)
+  static constexpr int SLOTS = BM / 8, RPP = 64 / SLOTS;   // 16-B slots per pixel row, pixel rows per piece
+  __amdgpu_buffer_rsrc_t rx, rdy;
+  int OH, OW, H, W, npw, nph;
+  int pb, py, px;                    // patch cursor (uniform)
+  int arel[APW], ar[APW], ac[APW];   // dy: per piece pixel (r, c) in the patch and element offset rel. to the patch
+  int acol[APW];                     // dy column (element) this lane loads for the piece
+  bool aok[APW];
+  int brel[2], by[2], bx[2];         // x halo: per piece halo (y, x) and element offset rel. to the halo origin
+  int bcol[2];
+  bool bok[2];
+  int yps, xps;
+  DEV WgradTapLds(const bf16* x, const bf16* dy, const Geom& g, int m0, int c0, int kt0, int wid, int lane,
+                  unsigned xbytes, unsigned dybytes)
+      : OH(g.OH), OW(g.OW), H(g.H), W(g.W) {
+    rx = make_rsrc(x, xbytes);
+    rdy = make_rsrc(dy, dybytes);
+    yps = (int)g.yps;
+    xps = (int)g.xps;
+    npw = (g.OW + PW - 1) / PW;
+    nph = (g.OH + PH - 1) / PH;
+    px = kt0 % npw;
+    const int t = kt0 / npw;
+    py = t % nph;
+    pb = t / nph;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {  // piece wid * APW + j: pixel rows RPP * piece + lane / SLOTS
+      const int row = (wid * APW + j) * RPP + lane / SLOTS;
+      const int slot = lane % SLOTS;
+      // physical slot -> logical chunk under the kmaj_off<BM> key of this pixel row
+      const int key = (2 * BM >= 256) ? 2 * ((row & 3) | (((row >> 3) & 1) << 2))
+                                      : 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+      const int chunk = (slot ^ key) & (SLOTS - 1);
+      acol[j] = m0 + chunk * 8;
+      aok[j] = acol[j] < g.K;
+      ar[j] = row >> 3;
+      ac[j] = row & 7;
+      arel[j] = (ar[j] * g.OW + ac[j]) * yps;
+    }
+    // halo: 8 pieces x 16 rows of 64 B; this wave fills pieces wid * 2 + j; lane: row (lane >> 2), slot lane & 3
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (wid * 2 + j) * 16 + (lane >> 2);
+      by[j] = row / HP;
+      bx[j] = row % HP;
+      const int chunk = (lane & 3) ^ (2 * (by[j] & 1));
+      bok[j] = row < 10 * HP && bx[j] < 10;
+      brel[j] = (by[j] * g.W + bx[j]) * xps;
+      bcol[j] = c0 + chunk * 8;
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+    const int oy0 = py * PH, ox0 = px * PW;
+    const int abase = ((pb * OH + oy0) * OW + ox0) * yps;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      const bool ok = aok[j] && oy0 + ar[j] < OH && ox0 + ac[j] < OW;
+      blds16(rdy, ok ? (unsigned)(abase + arel[j] + acol[j]) * 2u : kBufOob, stage + (wid * APW + j) * 1024);
+    }
+    const int xbase = ((pb * H + oy0 - 1) * W + ox0 - 1) * xps;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = bok[j] && (unsigned)(oy0 - 1 + by[j]) < (unsigned)H && (unsigned)(ox0 - 1 + bx[j]) < (unsigned)W;
+      blds16(rx, ok ? (unsigned)(xbase + brel[j] + bcol[j]) * 2u : kBufOob, stage + A_BYTES + (wid * 2 + j) * 1024);
+    }
+    if (++px == npw) {
+      px = 0;
+      if (++py == nph) { py = 0; ++pb; }
+    }
+  }
+};
+
+// B fragment of tap (kh, kw), 16 channels from ch0, pixels k0 .. k0 + 31 of the patch (frag_k's lane mapping with
+// pixel k -> halo row ((k >> 3) + kh, (k & 7) + kw))
+DEV bf16x8 frag_halo(const bf16* Bs, int kh, int kw, int ch0, int k0, int lane) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const int g = lane >> 4, il = lane & 15, q = il >> 2, p = il & 3;
+  const int ch = ch0 + 4 * p;
+  const int y = (k0 >> 3) + g + kh;
+  const int chunk = (ch >> 3) ^ (2 * (y & 1));
+  const int off = (y * WgradTapLds<128>::HP + q + kw) * 32 + ((chunk & 3) << 3) + (ch & 7);
+  s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(Bs + off));
+  s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(Bs + off + 4 * 32));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int BM>
+__global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                         float* __restrict__ dw, int kt_per_split, Geom g, int gm,
+                                                         int gn, int nk_all, unsigned xbytes, unsigned dybytes) {
+  using LD = WgradTapLds<BM>;
+  constexpr int NS = 3, STAGE = LD::STAGE, TM = BM / 32;  // 4 waves = 2 (m) x 2 (n); wave tile BM/2 x 144
+  constexpr int CTR = BM / 2, CTS = 288 + 4;               // epilogue: half the tile staged at a time
+  constexpr int LDSB = NS * STAGE > CTR * CTS * 4 ? NS * STAGE : CTR * CTS * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
+  const int tm = tile % gm, tc = tile / gm;  // out-channel tiles of one channel group adjacent (share the x halo)
+  const int m0 = tm * BM, c0 = tc * LD::BC;
+  const int kt0 = split * kt_per_split;
+  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
+  f32x4 acc[TM][9];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    LD ld(x, dy, g, m0, c0, kt0, wid, lane, xbytes, dybytes);
+    ld.issue(smem, wid);
+    if (nk > 1) ld.issue(smem + STAGE, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) vm_wait<LD::APW + 2>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = frag_k<BM>(As, wm * (BM / 2) + i * 16, h * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          const int f = wn * 9 + j, tap = f >> 1;
+          const bf16x8 b = frag_halo(Bs, tap / 3, tap % 3, (f & 1) * 16, h * 32, lane);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  vm_wait<0>();
+  const int Ntot = 9 * g.C;
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(i * 16 + 4 * (lane >> 4) + r) * CTS + (wn * 9 + j) * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < CTR * 288; e += 256) {
+      const int row = e / 288, col = e % 288, m = m0 + half * CTR + row;
+      const int n = (col >> 5) * g.C + c0 + (col & 31);  // col = tap * 32 + ci
+      if (m < g.K) wgrad_out(g, dw, split, (long)m * Ntot + wgrad_col(g, n), ct[row * CTS + col]);
+    }
+  }
+}
 }  // namespace v3
 
 // ---------------------------------------------------------------- host dispatch
@@ -2134,6 +2313,59 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_
   return (int)hipGetLastError();
 }
 
+// tap-fused 3x3 s1 weight-grad (v3::conv_wgrad_tap): 0 = off, 1 = on (default) where it applies
+inline int wgrad_tap_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_WGRAD_TAP");
+    return e ? atoi(e) : 1;
+  }();
+  return t;
+}
+inline bool wgrad_tap_ok(const Geom& g, const void* x, const void* dy) {
+  if (!wgrad_tap_mode() || g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.OH != g.H || g.OW != g.W) return false;
+  if (g.C % 32 != 0 || g.xps % 8 != 0 || g.yps % 8 != 0 || g.K % 8 != 0 || !aligned16(x) || !aligned16(dy)) return false;
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
+  if (xb >= (double)v3::kBufOob || db >= (double)v3::kBufOob) return false;
+  // enough (patch, tile) work units that the per-block fp32 atomics of the 288-column tile stay a small share
+  // (tools/gpu/tune_conv.py: 20^2 / 40^2 / 80^2 yolov5s layers are faster on the v3 / v4 column tiles)
+  const long units = (long)g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8) * ceil_div(g.K, 128) * (g.C / 32);
+  return units >= 16384;
+}
+template <int BM>
+int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
+  const int gm = ceil_div(g.K, BM), gn = g.C / 32;
+  const int nk = g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8);  // 8 x 8 patches
+  const int tiles = gm * gn;
+  int maxs = nk / 8;
+  if (maxs < 1) maxs = 1;
+  int splits = 1;
+  if (wgrad_target() > 0) {
+    splits = (wgrad_target() + tiles / 2) / tiles;
+    if (splits < 1) splits = 1;
+  } else {
+    // two resident blocks per CU; ~1.1 us per patch step of the 128-row tile (288 MFMA per wave pair at ~45 %
+    // of peak) and its 147 KiB fp32 tile of atomics per block at 1.3 TB/s (MI355X_MICROARCH.md §Global float
+    // atomics); the 64-row tile halves both
+    const double R = 2.0 * num_cus(), f = BM / 128.0;
+    double best = 1e300;
+    for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
+      const double blocks = (double)tiles * sp;
+      const double t = ceil(blocks / R) * ceil_div(nk, sp) * 1.1 * f + blocks * 0.113 * f;
+      if (t < best) { best = t; splits = sp; }
+    }
+  }
+  if (splits > maxs) splits = maxs;
+  const int per = ceil_div(nk, splits);
+  splits = ceil_div(nk, per);
+  const dim3 grid((unsigned)tiles, splits);
+  if (wgrad_begin(g, splits)) return 0;
+  if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * 9 * g.C, st);
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
+  v3::conv_wgrad_tap<BM><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db);
+  wgrad_end(g, dw, splits, st);
+  return (int)hipGetLastError();
+}
+
 // narrow layers (K <= 64): BM = 32 / 64 out-channel tiles, BN = 128 / 256 column tiles
 template <int BM, int BN>
 int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
@@ -2201,6 +2433,9 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const int nm = wgrad_narrow_for(g, NP);
     const int v4 = wgrad_v4_mode();
     const double xb4 = 2.0 * ((double)g.N * g.H * g.W * g.xps), db4 = 2.0 * ((double)NP * g.yps);
+    if (wgrad_tap_ok(g, x, dy))
+      return g.K <= 64 ? launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                       : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
         db4 < (double)v3::kBufOob) {
       if (v4 == 2 || (v4 == 3 && g.K >= 256)) return launch_wgrad_v4<256, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);

@@ -141,17 +141,16 @@ def test_dropout_mask_redrawn_on_graph_replay():
     import dmayolo.functional as Fn
     x = torch.randn(2, 64, 8, 8, device='cuda').contiguous(memory_format=torch.channels_last).requires_grad_(True)
     gup = torch.ones_like(x)
-    y = Fn.DropoutFn.apply(x, 0.5)  # eager warm-up (creates the generator state outside the capture)
-    y.backward(gup)
-    x.grad = None
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g):
-            sy = Fn.DropoutFn.apply(x, 0.5)
-            sy.backward(gup)
+    with torch.cuda.stream(s):  # warm-up off the default stream (creates the generator state outside the capture)
+        Fn.DropoutFn.apply(x, 0.5).backward(gup)
     torch.cuda.current_stream().wait_stream(s)
+    x.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):  # the same capture pattern as train_graph.GraphedTrainStep
+        sy = Fn.DropoutFn.apply(x, 0.5)
+        sy.backward(gup)
     masks = []
     for _ in range(3):
         g.replay()
