@@ -2097,7 +2097,7 @@ inline int conv_buf_mode() {
 }
 
 // tile of the 1x1 (pure GEMM) layers: 0 = 256 x 128, 3 stages; 1 = 128 x 128, 2 stages (2 blocks / CU);
-// 2 = 128 x 128, 3 stages
+// 2 = 128 x 128, 3 stages; 3 = 256 x 64, 2 stages (2 blocks / CU); 4 = 128 x 64, 3 stages (2 blocks / CU)
 inline int p1_tile_mode() {
   static int t = [] {
     const char* e = getenv("DMY_P1_TILE");
@@ -2136,6 +2136,8 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const int pt = p1 ? p1_tile_mode() : 0;
   if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
   else if (gv.K > 64 && pt == 2) V3_LAUNCH(128, 128, 3)
+  else if (gv.K > 64 && pt == 3) V3_LAUNCH(256, 64, 2)
+  else if (gv.K > 64 && pt == 4) V3_LAUNCH(128, 64, 3)
   else if (gv.K > 64) V3_LAUNCH(256, 128, 3)
   else V3_LAUNCH(256, 64, 2)
 #undef V3_LAUNCH

@@ -62,14 +62,19 @@ def _pow2(n, lo=2048):
     return c
 
 
+_CAP_HINT = {}  # (A, nc, multi) -> sort capacity that held every image's candidates last time
+
+
 def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False,
                         multi_label=False, labels=(), max_det=300):
     """Drop-in for utils/general.py:633-725 (merge=False).  Returns a list of (k, 6) tensors
     [xyxy, conf, cls] on the input device, rows in NMS keep order.
 
-    All per-image work runs in three HIP kernels (candidates, bitonic sort, greedy lazy-IoU scan);
-    the host reads two small count vectors (candidate counts to size the sort, keep counts to
-    slice the output) instead of the reference's per-image syncs.
+    All per-image work runs in three HIP kernels (candidates, bitonic sort, greedy lazy-IoU scan) and the host
+    synchronises ONCE per call, reading the candidate counts and keep counts together (one int32 vector).  The
+    sort capacity is the power of two that held the previous call's candidates for this prediction shape; when a
+    batch overflows it (its true count comes back in the same read) the call reruns once at the exact capacity, so
+    the top-`max_nms` cut always sees every candidate (utils/general.py:702-703).
     """
     assert 0 <= conf_thres <= 1 and 0 <= iou_thres <= 1
     if labels is not None and len(labels) and any(len(l) for l in labels):
@@ -87,26 +92,26 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
     if classes is not None:
         cls_ok = torch.zeros(nc, dtype=torch.uint8, device=dev)
         cls_ok[torch.tensor([c for c in classes if 0 <= c < nc], dtype=torch.long, device=dev)] = 1
-    cap0 = A * (nc if multi else 1)
-    counts = torch.zeros(nimg, dtype=torch.int32, device=dev)
-    # pass 1: count only (cap 0) to size the sort buffer
-    keys = torch.empty(1, dtype=torch.int64, device=dev)
-    call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), 0,
-         ptr(counts), stream())
-    nmax = int(counts.max()) if nimg else 0
-    out_list = [torch.zeros((0, 6), device=dev) for _ in range(nimg)]
-    if nmax == 0:
-        return out_list
-    cap = _pow2(min(nmax, cap0))
-    keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
-    counts.zero_()
-    call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), cap,
-         ptr(counts), stream())
-    call('dmy_nms_sort', ptr(keys), cap, ptr(counts), nimg, stream())
-    boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
-    out = torch.empty((nimg, max_det, 6), dtype=torch.float32, device=dev)
-    nkeep = torch.zeros(nimg, dtype=torch.int32, device=dev)
-    call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
-         ptr(keys), cap, ptr(counts), ptr(boxes), ptr(out), ptr(nkeep), stream())
-    nk = nkeep.tolist()
+    if nimg == 0:
+        return []
+    cap0 = _pow2(A * (nc if multi else 1))
+    key = (A, nc, multi)
+    cap = min(_CAP_HINT.get(key, 2048), cap0)
+    while True:
+        cnt = torch.zeros(2 * nimg, dtype=torch.int32, device=dev)  # [candidate counts | keep counts]
+        keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
+        call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), cap,
+             ptr(cnt), stream())
+        call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), nimg, stream())
+        boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
+        out = torch.empty((nimg, max_det, 6), dtype=torch.float32, device=dev)
+        call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
+             ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
+        h = cnt.tolist()  # the one host synchronisation
+        need = max(h[:nimg])
+        if need <= cap:
+            break
+        cap = _pow2(need)  # overflow: every candidate must enter the sort; rerun once at the exact capacity
+        _CAP_HINT[key] = cap
+    nk = h[nimg:]
     return [out[b, :nk[b]] for b in range(nimg)]

@@ -14,7 +14,7 @@ if [ -z "$NOTESTS" ]; then
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 [ -n "$NOBENCH" ] && exit 0
-timeout -k 10 900 python bench.py --steps $STEPS --warmup 3 ${BENCHARGS} > gpurun_out/bench.log 2>gpurun_out/bench.err
+timeout -k 10 900 python bench.py --steps $STEPS --warmup ${WARMUP:-3} ${BENCHARGS} > gpurun_out/bench.log 2>gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.log; tail -5 gpurun_out/bench.err
 if [ $rc -ne 0 ]; then exit $rc; fi
 [ -n "$NODDP" ] && exit 0
