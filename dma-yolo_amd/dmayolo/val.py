@@ -5,10 +5,10 @@ Per batch: model eval forward (Detect decode) -> non_max_suppression(conf 0.001,
 (utils/metrics.process_batch_multi) -> (correct, conf, pcls, tcls) stats.  At the end ap_per_class
 gives P, R, mAP@0.5 and mAP@0.5:0.95 exactly as val.py:283-291.
 
-Out of scope here (control plane): the dataloader, letterboxing of real images,
-plots, COCO-JSON, confusion matrix, txt saving.  Batches come in as tensors: uint8 images already at
-the network size [N, 3, H, W] and normalised targets [nt, 6] (img, cls, x, y, w, h) as datasets.py:614-629
-collates them; `shapes` (per-image (h0, w0), ((ratio), (pad))) may be given for scale_coords.
+Batches are what dmayolo.data.create_dataloader yields (datasets.py:624-629's collate: uint8 images at the
+network size [N, 3, H, W], normalised targets [nt, 6] (img, cls, x, y, w, h), paths, shapes), or
+(img, targets[, shapes]) tensors; `shapes` (per-image (h0, w0), ((ratio), (pad))) drive scale_coords.
+Out of scope (control plane): plots, COCO-JSON, confusion matrix, txt saving.
 """
 import numpy as np
 import torch
@@ -86,7 +86,7 @@ def run(model, batches, nc, conf_thres=0.001, iou_thres=0.6, max_det=300, single
     stats = []
     for batch in batches:
         img, targets = batch[0], batch[1]
-        shapes = batch[2] if len(batch) > 2 else None
+        shapes = batch[3] if len(batch) > 3 else (batch[2] if len(batch) > 2 else None)  # (img, t, paths, shapes)
         img = img.to(device, non_blocking=True)
         targets = targets.to(device).float()
         nb, _, height, width = img.shape

@@ -76,3 +76,25 @@ def test_val_run_tiny_model_end_to_end():
     tg = synthetic_targets(2, 10, per_image=10, seed=2)
     res, maps, seen, nt = run(m, [(imgs, tg.cpu())], nc=10)
     assert seen == 2 and len(res) == 7 and all(np.isfinite(res))
+
+
+def test_val_run_over_image_directory(tmp_path):
+    """val.run consumes dmayolo.data.create_dataloader batches (images + label files on disk, rect batches,
+    letterbox, collate_fn -> uint8 to the GPU) exactly as it consumes pre-collated tensors."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_data import _tree
+    from dmayolo.data import create_dataloader
+    from dmayolo.models.yolo import Model
+    from dmayolo import val
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    _tree(str(tmp_path), [(480, 640), (300, 500), (640, 360), (200, 200), (700, 400)], nc=4)
+    loader, ds = create_dataloader(str(tmp_path / 'images'), 320, 2, 32, rect=True, workers=0)
+    torch.manual_seed(0)
+    m = Model(os.path.join(root, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5n.yaml'), nc=4).cuda()
+    batches = list(loader)
+    r1, maps1, seen1, nt1 = val.run(m, loader, nc=4)
+    r2, maps2, seen2, nt2 = val.run(m, [(b[0], b[1], b[3]) for b in batches], nc=4)
+    assert seen1 == seen2 == 5 and int(nt1.sum()) == 12  # 4 labelled images x 3 boxes
+    assert r1 == r2 and np.array_equal(maps1, maps2)
