@@ -1087,47 +1087,18 @@ DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
   }
 }
 
-// Forward (DG = false) or stride-1 data-grad (DG = true; `g` is the GEMM view built by the host:
-// rows = input pixels, columns = input channels, gather = dy) with the BN-partial / accumulate epilogue.
-template <int BM, int BN, int NS, bool P1, bool DG, int BUF>
-__global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                            const float* __restrict__ bias, bf16* __restrict__ y,
-                                                            float* __restrict__ psum, float* __restrict__ psq,
-                                                            int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                            unsigned wbytes, S2Cls cls, Epi ep) {
+// Epilogue of the v3 GEMM kernels: (+bias) -> bf16 tile in LDS `ct` [BM][BN+8] + BN partials.  Partial rows
+// follow the v2 numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
+// Then 16-B stores (inference epilogue / accumulate / stride-2 class pixel mapping as configured).
+template <int BM, int BN, int NS, bool DG, int BUF>
+DEV void v3_epilogue(const f32x4 (&acc)[4][4], bf16* ct, const float* __restrict__ bias, bf16* __restrict__ y,
+                     float* __restrict__ psum, float* __restrict__ psq, int accumulate, const Geom& g, int tm,
+                     long m0, int n0, const v3::S2Cls& cls, const Epi& ep) {
   using C3_ = Cfg3<BM, BN, NS>;
-  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int tile = xcd_remap(blockIdx.x, gm * gn);
-  const int tm = tile / gn, tn = tile % gn;
   const long M = (long)g.N * g.OH * g.OW;
-  const long m0 = (long)tm * BM;
-  const int n0 = tn * BN;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // BUF: 0 = FwdLds, 1 = buffer loader (fragments first), 2 = buffer loader (DMA first), 3 = buffer loader,
-  // stride-2 data-grad parity class `cls` (only the class's taps: ceil((KH - kh0) / 2) x ceil((KW - kw0) / 2))
-  const int nk = BUF == 3 ? ((g.KH - ((cls.a + g.P) & 1) + 1) / 2) * ((g.KW - ((cls.b + g.P) & 1) + 1) / 2) * (g.C / BK)
-                          : (g.KH * g.KW * g.C + BK - 1) / BK;
-  if constexpr (BUF == 3) {
-    FwdLdsB<BM, BN, NS, false, true, true> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes, cls);
-    mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
-  } else if constexpr (BUF > 0) {
-    FwdLdsB<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
-    mainloop4<BM, BN, NS, BUF == 2>(ld, nk, smem, acc, wid, lane);
-  } else {
-    FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
-    mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
-  }
-  __syncthreads();
-  // epilogue: (+bias) -> bf16 tile in LDS [BM][BN+8] + BN partials.  Partial rows follow the v2
-  // numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
   const int wm = wid % C3_::WM, wn = wid / C3_::WM;
   constexpr int RS = BN + 8;
-  bf16* ct = reinterpret_cast<bf16*>(smem);
   const bool half = g.K <= 64;
   const long nprow = half ? 2 * ((M + 63) / 64) : 2 * ((M + 127) / 128);
 #pragma unroll
@@ -1202,6 +1173,123 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
     }
     *dst = v;
   }
+}
+
+// Persistent 1x1 (pure GEMM, stride 1) forward / data-grad for C % 64 == 0: gridDim.x blocks walk the tiles
+// t = blockIdx.x, + gridDim.x, ... through ONE continuous LDS-DMA ring of K steps, so the next tile's first
+// stages are in flight while this tile's epilogue runs (the epilogue stages through its own LDS region).  The
+// 1x1 layers have 1..8 K steps per tile, where a one-tile block spent its time in the prologue load latency and
+// the epilogue stores with nothing else in flight on the CU.
+template <int BM, int BN, bool DG>
+__global__ void __launch_bounds__(BM * BN / 64) conv_p1_persist(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                               const float* __restrict__ bias, bf16* __restrict__ y,
+                                                               float* __restrict__ psum, float* __restrict__ psq,
+                                                               int accumulate, Geom g, int gm, int gn, unsigned xbytes,
+                                                               unsigned wbytes, Epi ep) {
+  constexpr int NS = 3;
+  using C3_ = Cfg3<BM, BN, NS>;
+  constexpr int PER = C3_::APW + C3_::BPW;
+  constexpr int CTB = BM * (BN + 8) * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * C3_::STAGE + CTB];
+  bf16* ct = reinterpret_cast<bf16*>(smem + NS * C3_::STAGE);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  const long M = (long)g.N * g.OH * g.OW;
+  const int ntiles = gm * gn, nk = g.C / BK, G = gridDim.x;
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  // issue cursor (tile, k step) and its loader
+  int lt = t, lk = 0;
+  using LD = FwdLdsB<BM, BN, NS, true, DG>;
+  LD ld(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
+  auto issue = [&](int s) {
+    if (lt >= ntiles) return;
+    ld.issue(smem + (s % NS) * C3_::STAGE, wid);
+    if (++lk == nk) {
+      lk = 0;
+      lt += G;
+      if (lt < ntiles) ld = LD(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
+    }
+  };
+  const int my_tiles = (ntiles - 1 - blockIdx.x) / G + 1, total = my_tiles * nk;
+  issue(0);
+  if (total > 1) issue(1);
+  int s = 0;
+  for (; t < ntiles; t += G) {
+    const int tm = t / gn, tn = t % gn;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++s) {
+      if (s + 1 < total) vm_wait<PER>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
+      const bf16* Bs = As + BM * BK;
+      bf16x8 a[2][4], b[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[h][i] = frag_sw(As, wm * 64 + i * 16, h * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[h][j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + NS - 1 < total) issue(s + NS - 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+    }
+    v3_epilogue<BM, BN, NS, DG, 1>(acc, ct, bias, y, psum, psq, accumulate, g, tm, (long)tm * BM, tn * BN,
+                                   v3::S2Cls{0, 0, 0, 0}, ep);
+    vm_wait<0>();  // stores (and any accumulate loads) drained: the loop's counted waits see only stage loads
+  }
+}
+
+// Forward (DG = false) or stride-1 data-grad (DG = true; `g` is the GEMM view built by the host:
+// rows = input pixels, columns = input channels, gather = dy) with the BN-partial / accumulate epilogue.
+template <int BM, int BN, int NS, bool P1, bool DG, int BUF>
+__global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y,
+                                                            float* __restrict__ psum, float* __restrict__ psq,
+                                                            int accumulate, Geom g, int gm, int gn, unsigned xbytes,
+                                                            unsigned wbytes, S2Cls cls, Epi ep) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // BUF: 0 = FwdLds, 1 = buffer loader (fragments first), 2 = buffer loader (DMA first), 3 = buffer loader,
+  // stride-2 data-grad parity class `cls` (only the class's taps: ceil((KH - kh0) / 2) x ceil((KW - kw0) / 2))
+  const int nk = BUF == 3 ? ((g.KH - ((cls.a + g.P) & 1) + 1) / 2) * ((g.KW - ((cls.b + g.P) & 1) + 1) / 2) * (g.C / BK)
+                          : (g.KH * g.KW * g.C + BK - 1) / BK;
+  if constexpr (BUF == 3) {
+    FwdLdsB<BM, BN, NS, false, true, true> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes, cls);
+    mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+  } else if constexpr (BUF > 0) {
+    FwdLdsB<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+    mainloop4<BM, BN, NS, BUF == 2>(ld, nk, smem, acc, wid, lane);
+  } else {
+    FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
+    mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  }
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, DG, BUF>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
+                                    cls, ep);
 }
 
 // Weight-grad: rows m = output channel, columns n = (kh, kw, ci), reduction over pixels (split-K).
@@ -2106,6 +2194,18 @@ inline int p1_tile_mode() {
   return t;
 }
 
+inline int num_cus();
+// persistent 1x1 GEMM kernel (v3::conv_p1_persist): 0 = off (default, one tile per block), 1 = on.  Measured
+// 15-40 % SLOWER on every DMA-YOLO / yolov5s 1x1 shape (profiles/r02/ab_p1_persist.log): one 4-wave block per CU
+// draining its stores before the next tile's steps loses to the hardware's block turnover at 8 waves per CU.
+inline int p1_persist_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_P1_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  return t;
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st, const Epi& ep = Epi{}) {
@@ -2132,6 +2232,19 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       if (p1) V3_GO(BM, BN, NS, true, 0);                    \
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
+  }
+  if (p1 && buf && p1_persist_mode()) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
+    const int NC = num_cus();
+    if (gv.K > 64) {
+      const int gm = ceil_div(M, 128), gn = ceil_div(gv.K, 128);
+      const unsigned grid = (unsigned)min(gm * gn, NC);
+      v3::conv_p1_persist<128, 128, DG><<<grid, 256, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
+    } else {
+      const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 64);
+      const unsigned grid = (unsigned)min(gm * gn, NC);
+      v3::conv_p1_persist<256, 64, DG><<<grid, 256, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
+    }
+    return (int)hipGetLastError();
   }
   const int pt = p1 ? p1_tile_mode() : 0;
   if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
