@@ -145,10 +145,12 @@ class WgradArena:
 
     @classmethod
     def layout(cls, params):
-        """data_ptr -> (offset, numel) for every weight with dim >= 2; total size"""
+        """data_ptr -> (offset, numel) for every fp32 parameter that requires a gradient (conv / linear weights,
+        BN gamma / beta, conv biases: every tensor the conv backward produces comes from here, so the
+        optimizer's pointer tables see the same gradient addresses every step); total size"""
         offs, n = {}, 0
         for q in params:
-            if q.dim() >= 2 and q.dtype == torch.float32 and q.requires_grad:
+            if q.dim() >= 1 and q.dtype == torch.float32 and q.requires_grad:
                 offs[q.data_ptr()] = (n, q.numel())
                 n += -(-q.numel() // cls.ALIGN) * cls.ALIGN
         return offs, n
@@ -441,6 +443,7 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.xsink, ctx.rsink = xsink, rsink
         ctx.arena = WgradArena.current
         ctx.wkey = weight.data_ptr()
+        ctx.pkeys = tuple(t.data_ptr() if t is not None else None for t in (bias, gamma, beta))
         return y
 
     @staticmethod
@@ -452,6 +455,15 @@ class ConvBNActFn(torch.autograd.Function):
         M = N * OH * OW
         dt = dcode(dy)
         dbias = dgamma = dbeta = None
+        arena = ctx.arena
+
+        def pgrad(key, zero=False):
+            """the parameter's gradient tensor: its (zeroed) arena slice, else a fresh one"""
+            g = arena.take(key, (K,)) if (arena is not None and key is not None) else None
+            if g is None:
+                g = torch.zeros(K, dtype=torch.float32, device=dev) if zero else f32(K, dev)
+            return g
+
         if spec.bn is not None:
             x, wt, z, scale, shift, mean, invstd, gamma = ctx.saved_tensors
             dz = new_act(N, K, OH, OW, z)
@@ -461,7 +473,7 @@ class ConvBNActFn(torch.autograd.Function):
                 pdb, pdg = f32(P * K, dev), f32(P * K, dev)
                 call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
                      spec.act, M, K, ptr(pdb), ptr(pdg), stream())
-                dgamma, dbeta = f32(K, dev), f32(K, dev)
+                dgamma, dbeta = pgrad(ctx.pkeys[1]), pgrad(ctx.pkeys[2])
                 call('dmy_bn_bwd_finalize', ptr(pdb), ptr(pdg), P, K, float(M), ptr(gamma), ptr(invstd), ptr(dgamma),
                      ptr(dbeta), ptr(ca), ptr(cb), ptr(cc), stream())
             else:
@@ -486,10 +498,10 @@ class ConvBNActFn(torch.autograd.Function):
                 P = call('dmy_bn_reduce_rows', dt, ptr(dz), dzps, None, 0, M, K)
                 ps_, pq_ = f32(P * K, dev), f32(P * K, dev)
                 call('dmy_bn_stats', dt, ptr(dz), dzps, M, K, ptr(ps_), ptr(pq_), stream())
-                dbias = f32(K, dev)
+                dbias = pgrad(ctx.pkeys[0])
                 call('dmy_reduce_rows', ptr(ps_), P, K, ptr(dbias), 0, stream())
         if spec.bn is not None and ctx.has_bias and ctx.train_bn:
-            dbias = torch.zeros(K, dtype=torch.float32, device=dev)  # sum(dz) == 0 exactly behind train-mode BN
+            dbias = pgrad(ctx.pkeys[0], zero=True)  # sum(dz) == 0 exactly behind train-mode BN
         dx = dw = None
         Cp = ctx.cp
         if ctx.needs_input_grad[0]:
