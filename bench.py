@@ -40,7 +40,7 @@ CONFIGS = {
     'dmaca-1536': ('yolov5l-ca-sppfcspc-bifpn.yaml', 10, 1536, 32, 'visdrone'),  # C3CA sibling
     'c5-1920': ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 3, 1920, 8, 'visdrone'),  # config 5 (UAVDT nc=3)
 }
-PEAK_FLOPS = {torch.bfloat16: 2500.0e12, torch.float32: 157.3e12}  # dense MFMA (MI355X_MICROARCH.md)
+PEAK_FLOPS = {torch.bfloat16: 2500.0e12, torch.float32: 157.3e12, 'fp8': 5000.0e12}  # dense MFMA (MI355X_MICROARCH.md)
 PEAK_BW = 8.0e12  # HBM3E bytes/s (MI355X_MICROARCH.md)
 VISDRONE_TRAIN_IMAGES = 6471  # VisDrone2019-DET-train (data/VisDrone.yaml): batches per epoch for the schedule
 
@@ -59,6 +59,8 @@ def parse():
     ap.add_argument('--no-detect', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--layer-report', action='store_true', help='per-conv-shape timing table on stderr')
+    ap.add_argument('--fp8', action='store_true',
+                    help='config 5 (BASELINE configs[4]): e4m3 MFMA forward for every conv with C %% 128 == 0')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='process-group backend (nccl = RCCL; gloo only to rehearse several ranks on one GPU)')
     return ap.parse_args()
@@ -79,8 +81,9 @@ def spawn_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
-def build(cfg, dtype, device):
+def build(cfg, dtype, device, fp8=False):
     from dmayolo.models.yolo import Model
+    from dmayolo.functional import set_fp8
     from dmayolo.synthetic import CONFIGS as CDIR, HYP_VISDRONE, scaled_hyp
     yml, nc, img, _, _ = cfg
     torch.manual_seed(0)
@@ -98,6 +101,8 @@ def build(cfg, dtype, device):
         np.random.seed(0)
         random.seed(0)
         check_anchors(np.full((200, 2), float(img)), labels, m, thr=m.hyp['anchor_t'], imgsz=img)
+    if fp8:
+        set_fp8(m, True)
     return m.to(device)
 
 
@@ -151,7 +156,8 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
     if hbm:
         achieved, peak, unit = d['bytes'] / d['seconds'] / 1e9, PEAK_BW / 1e9, 'GB/s'
     else:
-        achieved, peak, unit = d['flops'] / d['seconds'] / 1e12, PEAK_FLOPS[dtype] / 1e12, 'TFLOP/s'
+        pk = PEAK_FLOPS['fp8'] if dom.endswith('_f8') else PEAK_FLOPS[dtype]
+        achieved, peak, unit = d['flops'] / d['seconds'] / 1e12, pk / 1e12, 'TFLOP/s'
     traffic, tsrc = None, None
     tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tpath):
@@ -176,7 +182,7 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
                             % (steps, el_events * 1e3 / steps))
 
 
-def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_seconds=15.0):
+def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_seconds=15.0, fp8=False):
     from dmayolo.functional import KernelTimer
     from dmayolo.synthetic import images, targets, clustered_predictions
     from dmayolo.infer import GraphedDetector
@@ -188,7 +194,7 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
         cfg[3] = batch
     yml, nc, img, bs, _ = cfg
     torch.cuda.reset_peak_memory_stats(device)
-    model = build(cfg, dtype, device)
+    model = build(cfg, dtype, device, fp8=fp8)
     net = model
     if world > 1:  # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
         fu = any(isinstance(m, torch.nn.MultiheadAttention) for m in model.modules())
@@ -225,7 +231,7 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     el_events = time.perf_counter() - t1
     KernelTimer.enabled = False
     detail = {} if a.layer_report else None
-    ks = KernelTimer.summary(detail, PEAK_FLOPS[dtype], PEAK_BW)
+    ks = KernelTimer.summary(detail, PEAK_FLOPS[dtype], PEAK_BW, peak_flops_f8=PEAK_FLOPS['fp8'])
     if detail and rank == 0:
         tot = sum(v[2] for v in detail.values())
         print(f'[{name}] kind        N    C    H    W    K  k s  launches  ms/step  TFLOP/s  share', file=sys.stderr)
@@ -314,7 +320,7 @@ def main():
     device = torch.device('cuda', dev_idx)
     dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
 
-    head = run_config(a.config, a, world, rank, dev_idx, device, dtype, a.batch, a.cpu_seconds)
+    head = run_config(a.config, a, world, rank, dev_idx, device, dtype, a.batch, a.cpu_seconds, fp8=a.fp8)
     also = None
     if a.also != 'none' and a.also != a.config:
         also = run_config(a.also, a, world, rank, dev_idx, device, dtype, 0, a.cpu_seconds)
@@ -325,7 +331,8 @@ def main():
             'metric': 'train images/sec (fwd+loss+bwd+optimizer, train.py batch loop) @%d; detect p50 ms incl. NMS' % img,
             'value': head.pop('value'), 'unit': head.pop('unit'), 'n_gpus': world, 'steps': a.steps,
             'warmup': a.warmup, 'ms_per_step': head.pop('ms_per_step'), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
+            'vs_baseline': None,
+            'dtype': ('bf16' if dtype == torch.bfloat16 else 'fp32') + (' (fp8 e4m3 forward convs)' if a.fp8 else ''),
             'data': 'synthetic (uint8 images seed 1+rank, 50 VisDrone-like targets/img; random-init weights)',
             'config': head.pop('config'), 'roofline': head.pop('roofline'), 'cpu_baseline': head.pop('cpu_baseline'),
             **head,

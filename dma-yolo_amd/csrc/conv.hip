@@ -945,9 +945,12 @@ struct S2Cls {
   int a, b, HX, WX;
 };
 
-template <int BM, int BN, int NS, bool P1, bool DG, bool S2 = false>
+// ES = operand element size in bytes: 2 (bf16, 64 elements per K step) or 1 (fp8 e4m3, 128 per K step; the
+// LDS image is byte-identical: 128-B rows of 16-B chunks)
+template <int BM, int BN, int NS, bool P1, bool DG, bool S2 = false, int ES = 2>
 struct FwdLdsB {
   using C3_ = Cfg3<BM, BN, NS>;
+  static constexpr int BKE = 128 / ES;  // elements per K step
   __amdgpu_buffer_rsrc_t rx, rw;
   int H, W, C, KW, xps;
   int kh, kw, ci0, kpos;            // uniform cursor of the next K step
@@ -967,7 +970,7 @@ struct FwdLdsB {
     cb = cls.b;
     kw0 = (cls.b + g.P) & 1;
     if (S2) { kh = (cls.a + g.P) & 1; kw = kw0; }
-    kl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
+    kl = ((lane & 7) ^ ((lane >> 3) & 6)) * (16 / ES);
 #pragma unroll
     for (int j = 0; j < C3_::APW; ++j) {
       const long m = m0 + (wid * C3_::APW + j) * 8 + (lane >> 3);
@@ -984,7 +987,7 @@ struct FwdLdsB {
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j) {
       const int n = n0 + (wid * C3_::BPW + j) * 8 + (lane >> 3);
-      boff[j] = n < g.K ? (unsigned)(n * Ktot + kl) * 2u : kBufOob;
+      boff[j] = n < g.K ? (unsigned)(n * Ktot + kl) * (unsigned)ES : kBufOob;
     }
   }
   DEV void issue(char* stage, int wid) {
@@ -995,15 +998,15 @@ struct FwdLdsB {
     for (int j = 0; j < C3_::APW; ++j) {
       bool ok = aval[j];
       if (!P1) ok = ok && (unsigned)(ih0[j] + dh) < (unsigned)H && (unsigned)(iw0[j] + dw) < (unsigned)W;
-      blds16(rx, ok ? (unsigned)(pix[j] + delta) * 2u : kBufOob, stage + (wid * C3_::APW + j) * 1024);
+      blds16(rx, ok ? (unsigned)(pix[j] + delta) * (unsigned)ES : kBufOob, stage + (wid * C3_::APW + j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j)
-      blds16(rw, boff[j] == kBufOob ? kBufOob : boff[j] + (unsigned)bk * 2u,
+      blds16(rw, boff[j] == kBufOob ? kBufOob : boff[j] + (unsigned)bk * (unsigned)ES,
              stage + C3_::A_BYTES + (wid * C3_::BPW + j) * 1024);
-    kpos += BK;
+    kpos += BKE;
     if (!P1) {
-      ci0 += BK;
+      ci0 += BKE;
       if (ci0 == C) {
         ci0 = 0;
         if (S2) {
@@ -1290,6 +1293,98 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, BUF>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
                                     cls, ep);
+}
+
+// ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 block scales (0x7f = 2^0): 2x the bf16 MFMA rate per clock
+// (MI355X_MICROARCH.md, matrix-core table).  Operands are OCP e4m3fn: activations per tensor (x ~ x8 * amax / 448),
+// weights per output channel (w ~ w8 * wscale[k]); the fp32 accumulator is dequantised by amax / 448 * wscale[n]
+// before the shared v3 epilogue (bias, BN partials, inference BN / act / residual).  A K step is 128 fp8 = the
+// same 128-B LDS rows as a bf16 step, so the loader (FwdLdsB<..., ES = 1>) and the swizzled image are unchanged.
+// A 16x16x128 fragment is 32 bytes per lane; any k order used identically for A and B gives the same dot
+// products, so lane group q takes 16-B chunks q and 4 + q of the row -- exactly the two conflict-free ds_read_b128
+// of the bf16 kernel's h = 0 / 1 fragments (tools/gpu/probe_f8.hip checked the MFMA with exact integer data).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+
+DEV i32x8 frag_f8(const char* X, int r0, int lane) {
+  const int row = r0 + (lane & 15), q = lane >> 4, sw = row & 6;
+  const char* base = X + row * 128;
+  const i32x4v lo = *reinterpret_cast<const i32x4v*>(base + ((q ^ sw) << 4));
+  const i32x4v hi = *reinterpret_cast<const i32x4v*>(base + (((4 + q) ^ sw) << 4));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int BM, int BN, int NS, class LD>
+DEV void mainloop_f8(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int lane) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  constexpr int PER = C3_::APW + C3_::BPW;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  ld.issue(smem, wid);
+  if (NS == 3 && nk > 1) ld.issue(smem + C3_::STAGE, wid);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    const char* As = smem + (kt % NS) * C3_::STAGE;
+    const char* Bs = As + C3_::A_BYTES;
+    i32x8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = frag_f8(As, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = frag_f8(Bs, wn * 64 + j * 16, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                     0x7f7f7f7f);
+  }
+}
+
+template <int BM, int BN, int NS, bool P1>
+__global__ void __launch_bounds__(BM * BN / 64) conv_fwd_f8(const unsigned char* __restrict__ x8,
+                                                            const unsigned char* __restrict__ w8,
+                                                            const float* __restrict__ xamax,
+                                                            const float* __restrict__ wscale,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y,
+                                                            float* __restrict__ psum, float* __restrict__ psq, Geom g,
+                                                            int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = g.KH * g.KW * g.C / 128;
+  FwdLdsB<BM, BN, NS, P1, false, false, 1> ld(reinterpret_cast<const bf16*>(x8), reinterpret_cast<const bf16*>(w8), g,
+                                              M, m0, n0, wid, lane, xbytes, wbytes);
+  mainloop_f8<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  const float am = xamax[0];
+  const float sx = am > 0.f ? am * (1.f / 448.f) : (am == 0.f ? 1.f : am);  // NaN amax propagates
+  const int wn = wid / C3_::WM;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+    const float f = sx * (n < g.K ? wscale[n] : 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] *= f;
+  }
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, false, 1>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, 0, g, tm, m0, n0,
+                                    S2Cls{0, 0, 0, 0}, ep);
 }
 
 // Weight-grad: rows m = output channel, columns n = (kh, kw, ci), reduction over pixels (split-K).
@@ -2580,6 +2675,87 @@ DMY_API int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* d
                               void* stream);
 // BN partial rows of the forward epilogue: 2 per 128 (big tile) or 64 rows of M.  The v3 kernel's
 // 64-row wave rows number the same way (wave row wm of 256-row tile tm = row 4 tm + wm).
+// ---------------------------------------------------------------- fp8 operand preparation
+DEV unsigned pack4_e4m3(float a, float b, float c, float d) {  // OCP e4m3fn, round to nearest even, saturated
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+
+// amax of a bf16 NHWC activation ([rows][C] with pixel stride xps, C % 8 == 0): per-wave max, one atomicMax on
+// the float's bits (non-negative floats order as unsigned ints; a NaN sorts above +inf and propagates)
+__global__ void fp8_amax_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps, float* __restrict__ amax) {
+  float m = 0.f;
+  bool nan = false;
+  for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const unsigned row = v / (unsigned)cv, c8 = v - row * (unsigned)cv;
+    float f[8];
+    unpack<bf16>(*reinterpret_cast<const uint4*>(x + (long)row * xps + c8 * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m = fmaxf(m, fabsf(f[j]));
+      nan |= f[j] != f[j];
+    }
+  }
+  if (nan) m = __builtin_nanf("");
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float t = __shfl_xor(m, o, 64);
+    m = (t != t || t > m) ? t : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(m));
+}
+
+// x8[row][c] = e4m3(x[row][c] * 448 / amax), dense [rows][C] output
+__global__ void fp8_quant_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps,
+                                 unsigned char* __restrict__ q, const float* __restrict__ amax) {
+  const float a = amax[0];
+  const float inv = a > 0.f ? 448.f / a : 1.f;
+  for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const unsigned row = v / (unsigned)cv, c8 = v - row * (unsigned)cv;
+    float f[8];
+    unpack<bf16>(*reinterpret_cast<const uint4*>(x + (long)row * xps + c8 * 8), f);
+    uint2 o;
+    o.x = pack4_e4m3(f[0] * inv, f[1] * inv, f[2] * inv, f[3] * inv);
+    o.y = pack4_e4m3(f[4] * inv, f[5] * inv, f[6] * inv, f[7] * inv);
+    *reinterpret_cast<uint2*>(q + (size_t)v * 8) = o;
+  }
+}
+
+// fp32 OIHW weight -> e4m3 OHWI [K][KH][KW][C] with a per-output-channel scale wscale[k] = amax_k / 448
+__global__ void __launch_bounds__(256) wprep_fp8_kernel(const float* __restrict__ w, unsigned char* __restrict__ w8,
+                                                        float* __restrict__ wscale, int C, int KH, int KW) {
+  __shared__ float red[4];
+  const int k = blockIdx.x, n = C * KH * KW;
+  const float* src = w + (long)k * n;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(src[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float inv = m > 0.f ? 448.f / m : 1.f;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {  // C % 128 == 0: 4 consecutive channels share (kh, kw)
+    const int c = i % C, t = i / C, kw = t % KW, kh = t / KW;
+    const float* s0 = src + ((long)c * KH + kh) * KW + kw;
+    const long cs = (long)KH * KW;
+    *reinterpret_cast<unsigned*>(w8 + (long)k * n + i) =
+        pack4_e4m3(s0[0] * inv, s0[cs] * inv, s0[2 * cs] * inv, s0[3 * cs] * inv);
+  }
+  if (threadIdx.x == 0) wscale[k] = m > 0.f ? m / 448.f : 1.f;
+}
+
+inline bool fp8_fwd_ok(int C, int K, long yps, const void* x8, const void* w8, const void* y, double xbytes,
+                       double wbytes) {
+  return C % 128 == 0 && K % 8 == 0 && K >= 32 && yps % 8 == 0 && aligned16(x8) && aligned16(w8) && aligned16(y) &&
+         xbytes < (double)v3::kBufOob && wbytes < (double)v3::kBufOob;
+}
+
 DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile(M, K) ? 128 : 64); }
 
 DMY_API int dmy_conv_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, float* psum, float* psq,
@@ -2600,6 +2776,59 @@ DMY_API int dmy_conv_fwd_act(int dtype, const void* x, const void* w, const floa
   const Epi ep{scale, shift, res, rps, act, 1};
   return dtype ? conv_fwd_t<bf16>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep)
                : conv_fwd_t<float>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep);
+}
+
+DMY_API int dmy_fp8_quant(const void* x, long rows, int C, long xps, void* x8, float* amax, void* stream) {
+  if (C % 8 != 0 || xps % 8 != 0 || !aligned16(x) || rows * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(amax, 0, sizeof(float), st);
+  const unsigned nvec = (unsigned)(rows * (C / 8));
+  if (nvec == 0) return 0;
+  const int grid = grid_cap(ceil_div(nvec, 256), 4096);
+  fp8_amax_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, amax);
+  fp8_quant_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, (unsigned char*)x8, amax);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_conv_wprep_fp8(const float* w_oihw, void* w8, float* wscale, int K, int C, int KH, int KW,
+                               void* stream) {
+  if (C % 4 != 0) return (int)hipErrorInvalidValue;
+  wprep_fp8_kernel<<<K, 256, 0, (hipStream_t)stream>>>(w_oihw, (unsigned char*)w8, wscale, C, KH, KW);
+  return (int)hipGetLastError();
+}
+
+// BN partial rows the fp8 kernel's epilogue writes (v3 numbering at every M: 2 per 128 rows when K > 64, else per 64)
+DMY_API int dmy_conv_fwd_fp8_partial_rows(long M, int K) { return 2 * ceil_div(M, K > 64 ? 128 : 64); }
+
+DMY_API int dmy_conv_fwd_fp8(const void* x8, const void* w8, const float* xamax, const float* wscale,
+                             const float* bias, void* y, float* psum, float* psq, int N, int H, int W, int C, int K,
+                             int KH, int KW, int S, int P, int OH, int OW, long yps, const float* scale,
+                             const float* shift, int act, const void* res, long rps, void* stream) {
+  const Geom g = make_geom(N, H, W, C, C, K, KH, KW, S, P, OH, OW, yps);
+  const long M = (long)N * OH * OW;
+  if (M == 0 || K == 0) return 0;
+  const double xb = (double)N * H * W * C, wb = (double)K * KH * KW * C;
+  if (!fp8_fwd_ok(C, K, yps, x8, w8, y, xb, wb) || (res && (rps % 8 != 0 || !aligned16(res))))
+    return (int)hipErrorInvalidValue;
+  const Epi ep{scale, shift, res, rps, act, scale != nullptr || res != nullptr || act != 0 ? 1 : 0};
+  const bool p1 = KH == 1 && KW == 1 && S == 1 && P == 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned xbytes = (unsigned)xb, wbytes = (unsigned)wb;
+  const unsigned char *a = (const unsigned char*)x8, *b = (const unsigned char*)w8;
+#define F8_GO(BM, BN, NS)                                                                                          \
+  {                                                                                                                \
+    const int gm = ceil_div(M, BM), gn = ceil_div(K, BN);                                                          \
+    if (p1)                                                                                                        \
+      v3::conv_fwd_f8<BM, BN, NS, true><<<(unsigned)gm * gn, BM * BN / 64, 0, st>>>(                                \
+          a, b, xamax, wscale, bias, (bf16*)y, psum, psq, g, gm, gn, xbytes, wbytes, ep);                          \
+    else                                                                                                           \
+      v3::conv_fwd_f8<BM, BN, NS, false><<<(unsigned)gm * gn, BM * BN / 64, 0, st>>>(                               \
+          a, b, xamax, wscale, bias, (bf16*)y, psum, psq, g, gm, gn, xbytes, wbytes, ep);                          \
+  }
+  if (K > 64) F8_GO(256, 128, 3)
+  else F8_GO(256, 64, 2)
+#undef F8_GO
+  return (int)hipGetLastError();
 }
 
 DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,

@@ -209,11 +209,12 @@ class WeightPrep:
 class ConvSpec:
     """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None).
     wcache / ecache: inference-only caches of the prepped weight and the eval BN coefficients."""
-    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', '__weakref__')
+    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', 'fp8', 'f8cache', '__weakref__')
 
     def __init__(self, stride, pad, act, bn=None):
         self.stride, self.pad, self.act, self.bn = int(stride), int(pad), int(act), bn
-        self.wcache = self.ecache = None
+        self.wcache = self.ecache = self.f8cache = None
+        self.fp8 = False
 
 
 _SPECS = weakref.WeakKeyDictionary()
@@ -225,7 +226,46 @@ def spec_for(owner, stride, pad, act, bn):
     sp = _SPECS.get(owner)
     if sp is None or (sp.stride, sp.pad, sp.act) != (int(stride), int(pad), int(act)) or sp.bn is not bn:
         sp = _SPECS[owner] = ConvSpec(stride, pad, act, bn)
+    sp.fp8 = bool(getattr(owner, 'dmy_fp8', False))
     return sp
+
+
+def fp8_eligible(C, K, dtype, rows):
+    """layers the e4m3 forward kernel takes (dmy_conv_fwd_fp8): bf16 activations, C % 128 == 0 (one 128-wide
+    K step per tap), K % 8 == 0, and byte offsets of the quantised input below the buffer-descriptor range"""
+    return dtype == torch.bfloat16 and C % 128 == 0 and K % 8 == 0 and K >= 32 and rows * C < 0xFFFFFFF0
+
+
+def set_fp8(model, on=True):
+    """Config 5 (BASELINE configs[4]): run the forward of every eligible conv (input channels % 128 == 0) on the
+    fp8 e4m3 MFMA kernel; the backward stays bf16.  Returns the number of convs switched."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, torch.nn.Conv2d) and m.groups == 1 and m.in_channels % 128 == 0 and m.out_channels % 8 == 0:
+            m.dmy_fp8 = bool(on)
+            n += 1
+    PARAM_GEN[0] += 1  # drop cached inference weights / coefficients
+    return n
+
+
+def _fp8_operands(x, xps, weight, spec, wkey):
+    """per-tensor e4m3 copy of the activation (current amax, dmy_fp8_quant) and the per-output-channel e4m3
+    weight (cached on the spec until the weight changes)"""
+    N, C, H, W = x.shape
+    K, _, KH, KW = weight.shape
+    rows = N * H * W
+    x8 = torch.empty(rows * C, dtype=torch.uint8, device=x.device)
+    amax = f32(1, x.device)
+    call('dmy_fp8_quant', ptr(x), rows, C, xps, ptr(x8), ptr(amax), stream())
+    fc = spec.f8cache
+    if fc is not None and fc[0] == wkey:
+        w8, ws = fc[1], fc[2]
+    else:
+        w8 = torch.empty(weight.numel(), dtype=torch.uint8, device=x.device)
+        ws = f32(K, x.device)
+        call('dmy_conv_wprep_fp8', ptr(weight.detach().contiguous()), ptr(w8), ptr(ws), K, C, KH, KW, stream())
+        spec.f8cache = (wkey, w8, ws)
+    return x8, amax, w8, ws
 
 
 def prep_weight(w, dtype, need_t, Cp=None):
@@ -269,7 +309,7 @@ class KernelTimer:
         cls.records.append((kind, flops, nbytes, e0, e1, tag))
 
     @classmethod
-    def summary(cls, detail=None, peak_flops=2.5e15, peak_bw=8.0e12):
+    def summary(cls, detail=None, peak_flops=2.5e15, peak_bw=8.0e12, peak_flops_f8=5.0e15):
         """Per-kind totals: launches, flops, seconds, bytes, and the roofline time sum_launches max(F / peak_flops,
         B / peak_bw) split by the binding resource (troof_mfma / troof_hbm).  When `detail` is a dict it also
         receives per-(kind, shape) [launches, flops, seconds, bytes]."""
@@ -277,7 +317,7 @@ class KernelTimer:
         out = {}
         for kind, fl, nb, e0, e1, tag in cls.records:
             t = e0.elapsed_time(e1) * 1e-3
-            tm, th = fl / peak_flops, nb / peak_bw
+            tm, th = fl / (peak_flops_f8 if kind.endswith('_f8') else peak_flops), nb / peak_bw
             d = out.setdefault(kind, [0, 0.0, 0.0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += fl
@@ -295,17 +335,25 @@ class KernelTimer:
                 for k, v in out.items()}
 
 
-def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka, epi=None):
+def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca, ka, epi=None, f8=None):
     """(k, s, p) and x's shape are the launch geometry; Ca / ka the layer's real input channels and kernel
     (they differ for the space-to-depth stem and the channel-padded stem), used for the flop / byte count.
-    epi = (scale, shift, act, res, rps): fused inference epilogue (dmy_conv_fwd_act)"""
+    epi = (scale, shift, act, res, rps): fused inference epilogue (dmy_conv_fwd_act)
+    f8 = (x8, amax, w8, wscale): run on the e4m3 kernel (dmy_conv_fwd_fp8, timer kind conv_fwd_f8)"""
     N, C, H, W = x.shape
     es = x.element_size()
     Hi, Wi = (2 * H, 2 * W) if ka != k else (H, W)
     kw = dict(tag=(N, Ca, Hi, Wi, K, ka, s if ka == k else 2),
               nbytes=es * (N * H * W * C + K * C * k * k + N * OH * OW * K))
     fl = 2.0 * N * OH * OW * K * Ca * ka * ka
-    if epi is None:
+    if f8 is not None:
+        x8, amax, w8, ws = f8
+        sc, sh, act, res, rps = epi if epi is not None else (None, None, 0, None, 0)
+        kw['nbytes'] = N * H * W * C + K * C * k * k + es * N * OH * OW * K
+        KernelTimer.run('conv_fwd_f8', fl, 'dmy_conv_fwd_fp8', ptr(x8), ptr(w8), ptr(amax), ptr(ws), ptr(bias), ptr(y),
+                        ptr(psum), ptr(psq), N, H, W, C, K, k, k, s, p, OH, OW, yps, ptr(sc), ptr(sh), act, ptr(res),
+                        rps, stream(), **kw)
+    elif epi is None:
         KernelTimer.run('conv_fwd', fl, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), ptr(psum),
                         ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(), **kw)
     else:
@@ -384,6 +432,9 @@ class ConvBNActFn(torch.autograd.Function):
         s, p = spec.stride, spec.pad
         dev, dt = x.device, x.dtype
         M = N * OH * OW
+        f8 = None
+        if spec.fp8 and not s2d and Cp == C and fp8_eligible(C, K, dt, N * H * W):
+            f8 = _fp8_operands(x, xps, weight, spec, wkey)
         if res is not None:
             res, rps = pixel_stride(res)
         else:
@@ -392,18 +443,18 @@ class ConvBNActFn(torch.autograd.Function):
             y = new_act(N, K, OH, OW, x)
             scale, shift = eval_coef(spec, dev) if bn is not None else (None, None)
             if scale is None and spec.act == ACT_NONE and res is None:
-                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k)
+                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             else:
                 _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k,
-                                 epi=(scale, shift, spec.act, res, rps))
+                                 epi=(scale, shift, spec.act, res, rps), f8=f8)
             return y
         z = new_act(N, K, OH, OW, x)
         if bn is not None:
             scale, shift, mean, invstd = f32(K, dev), f32(K, dev), f32(K, dev), f32(K, dev)
             if train_bn:
-                P = call('dmy_conv_fwd_partial_rows', M, K)
+                P = call('dmy_conv_fwd_fp8_partial_rows' if f8 is not None else 'dmy_conv_fwd_partial_rows', M, K)
                 psum, psq = f32(P * K, dev), f32(P * K, dev)
-                _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, kg, sg, pg, OH, OW, C, k)
+                _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, kg, sg, pg, OH, OW, C, k, f8=f8)
                 if P > 256:  # two-stage column reduction of the epilogue partials
                     S = call('dmy_colsum2_rows', P)
                     ps2, pq2 = f32(S * K, dev), f32(S * K, dev)
@@ -418,7 +469,7 @@ class ConvBNActFn(torch.autograd.Function):
                      ptr(bn.num_batches_tracked) if upd else None, float(mom), float(bn.eps), upd,
                      ptr(mean), ptr(invstd), ptr(scale), ptr(shift), stream())
             else:
-                _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k)
+                _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
                 call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
                      float(bn.eps), K, ptr(scale), ptr(shift), stream())
             y = new_act(N, K, OH, OW, x)
@@ -426,7 +477,7 @@ class ConvBNActFn(torch.autograd.Function):
                  M, K, stream())
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
         else:
-            _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k)
+            _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             if spec.act != ACT_NONE or res is not None:
                 y = new_act(N, K, OH, OW, x)
                 one, zero = torch.ones(K, device=dev), torch.zeros(K, device=dev)

@@ -62,6 +62,19 @@ int dmy_conv_wprep_s2d(int dtype, const float* w_oihw, void* w_s2d, int K, int C
 int dmy_conv_wgrad_s2d_to_oihw(const float* dw_s2d, float* dw_oihw, int K, int C, int Cs, void* stream);
 int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, int Cp, int KH, int KW, void* stream);
 
+/* ---- fp8 (OCP e4m3fn) forward conv for config 5 (BASELINE configs[4], "fp8 MFMA conv"): replaces the forward of
+ *      Conv.conv (models/common.py:61-74) when enabled; backward stays bf16.  Activations are quantised per
+ *      tensor with the current amax (x ~ x8 * amax / 448), weights per output channel (w ~ w8 * wscale[k]);
+ *      the MX-scaled 16x16x128 MFMA runs with unit block scales and the accumulator is dequantised in the
+ *      epilogue.  Requirements: C % 128 == 0, K % 8 == 0, x8 dense [N*H*W][C]. */
+int dmy_fp8_quant(const void* x_bf16, long rows, int C, long xps, void* x8, float* amax, void* stream);
+int dmy_conv_wprep_fp8(const float* w_oihw, void* w8_ohwi, float* wscale, int K, int C, int KH, int KW, void* stream);
+int dmy_conv_fwd_fp8_partial_rows(long M, int K); /* BN partial rows of dmy_conv_fwd_fp8's epilogue */
+int dmy_conv_fwd_fp8(const void* x8, const void* w8_ohwi, const float* xamax, const float* wscale, const float* bias,
+                     void* y, float* psum, float* psq, int N, int H, int W, int C, int K, int KH, int KW, int S, int P,
+                     int OH, int OW, long yps, const float* scale, const float* shift, int act, const void* res,
+                     long rps, void* stream);
+
 /* ---- BatchNorm2d + activation: replaces nn.BatchNorm2d/nn.SiLU/nn.Hardswish in models/common.py:68-73,
  *      1176-1180, 1284-1306 with utils/torch_utils.py:161-170 eps/momentum. act: 0 none 1 silu 2 hardswish
  *      3 sigmoid 4 gelu(erf). */

@@ -1,0 +1,176 @@
+"""GPU: the fp8 (OCP e4m3fn) forward conv of config 5 (BASELINE configs[4], "fp8 MFMA conv"; csrc/conv.hip
+conv_fwd_f8 on v_mfma_scale_f32_16x16x128_f8f6f4).
+
+* dmy_fp8_quant / dmy_conv_wprep_fp8 against torch's own float8_e4m3fn cast of the same scaled fp32 values
+  (bit-exact: amax, per-channel weight scales and every byte);
+* dmy_conv_fwd_fp8 against a float64 convolution of the DEQUANTISED operands (x8 * amax / 448, w8 * wscale):
+  the kernel's only error sources are the fp32 accumulation and the bf16 output rounding, so the bound is the
+  bf16 one (relative L2 < 4e-3), including the BN partial sums of the training epilogue and the fused inference
+  epilogue (eval BN + SiLU + residual);
+* the whole config-5 model with fp8 forward convs against its bf16 forward at a stated tolerance: e4m3 keeps 3
+  mantissa bits (relative step 2^-3, i.e. +-6 % per element), averaged over C*k*k products per output and
+  compounded over ~60 layers.  Bound (measured 2026-10, tools/gpu/fp8_model_err): per-level output relative L2 <
+  0.15, cosine > 0.98, loss within 5 %.
+"""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def _e4m3(t):
+    return t.clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def _quant(x_cl, C):
+    from dmayolo.functional import call, ptr, stream, pixel_stride
+    xs, xps = pixel_stride(x_cl)
+    N, _, H, W = xs.shape
+    x8 = torch.empty(N * H * W * C, dtype=torch.uint8, device='cuda')
+    amax = torch.empty(1, device='cuda')
+    call('dmy_fp8_quant', ptr(xs), N * H * W, C, xps, ptr(x8), ptr(amax), stream())
+    return x8, amax
+
+
+@pytest.mark.parametrize('slice_', [False, True])
+def test_fp8_quant_matches_torch_cast(slice_):
+    g = torch.Generator().manual_seed(3)
+    N, C, H, W = 3, 128, 17, 23
+    full = (torch.randn(N, 2 * C if slice_ else C, H, W, generator=g) * 3).bfloat16().cuda()
+    full = full.contiguous(memory_format=torch.channels_last)
+    x = full[:, C:] if slice_ else full  # a concat slice: pixel stride 2C
+    x8, amax = _quant(x, C)
+    torch.cuda.synchronize()
+    xf = x.float().permute(0, 2, 3, 1).reshape(-1, C)
+    a = xf.abs().max()
+    assert float(amax) == float(a)
+    ref = _e4m3(xf * (torch.tensor(448.0, device='cuda') / a)).reshape(-1)
+    assert torch.equal(x8, ref)
+
+
+def test_fp8_wprep_matches_torch_cast():
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(4)
+    K, C, k = 40, 256, 3
+    w = (torch.randn(K, C, k, k, generator=g) * torch.linspace(0.01, 2, K).view(K, 1, 1, 1)).cuda()
+    w[5] = 0  # an all-zero output channel: scale 1, bytes 0
+    w8 = torch.empty(w.numel(), dtype=torch.uint8, device='cuda')
+    ws = torch.empty(K, device='cuda')
+    call('dmy_conv_wprep_fp8', ptr(w), ptr(w8), ptr(ws), K, C, k, k, stream())
+    torch.cuda.synchronize()
+    am = w.abs().amax((1, 2, 3))
+    # tensor / tensor: torch turns a division by a Python scalar into a multiply by its rounded reciprocal
+    exp_s = torch.where(am > 0, am / torch.full_like(am, 448.0), torch.ones_like(am))
+    assert torch.equal(ws, exp_s)
+    inv = torch.where(am > 0, torch.tensor(448.0, device='cuda') / am, torch.ones_like(am))
+    ref = _e4m3(w * inv.view(K, 1, 1, 1)).permute(0, 2, 3, 1).reshape(-1)  # OHWI
+    assert torch.equal(w8, ref)
+
+
+def _dequant(x8, amax, shape_nhwc):
+    v = x8.view(torch.float8_e4m3fn).double().reshape(shape_nhwc)
+    return (v * (float(amax) / 448.0)).permute(0, 3, 1, 2)
+
+
+# (N, C, H, W, K, k, s): 3x3 s1 / s2, 1x1, K <= 64 tile, ragged M, several K steps per tap
+SHAPES = [(2, 128, 40, 36, 128, 3, 1), (4, 256, 33, 29, 64, 3, 2), (3, 128, 50, 41, 256, 1, 1),
+          (2, 384, 21, 27, 136, 3, 1), (5, 128, 64, 64, 40, 3, 1)]
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', SHAPES)
+def test_conv_fwd_fp8_vs_dequantised_reference(N, C, H, W, K, k, s):
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(N * 100 + C + K)
+    p = k // 2
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5).cuda()
+    bias = torch.randn(K, generator=g).cuda() * 0.1
+    x8, amax = _quant(x, C)
+    w8 = torch.empty(w.numel(), dtype=torch.uint8, device='cuda')
+    ws = torch.empty(K, device='cuda')
+    call('dmy_conv_wprep_fp8', ptr(w), ptr(w8), ptr(ws), K, C, k, k, stream())
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    M = N * OH * OW
+    y = torch.empty(N, K, OH, OW, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
+    P = call('dmy_conv_fwd_fp8_partial_rows', M, K)
+    ps = torch.full((P, K), float('nan'), device='cuda')
+    pq = torch.full((P, K), float('nan'), device='cuda')
+    call('dmy_conv_fwd_fp8', ptr(x8), ptr(w8), ptr(amax), ptr(ws), ptr(bias), ptr(y), ptr(ps), ptr(pq), N, H, W, C, K,
+         k, k, s, p, OH, OW, K, None, None, 0, None, 0, stream())
+    torch.cuda.synchronize()
+    xd = _dequant(x8, amax, (N, H, W, C)).cpu()
+    wd = (w8.view(torch.float8_e4m3fn).double().reshape(K, k, k, C).permute(0, 3, 1, 2) * ws.double().view(K, 1, 1, 1))
+    ref = F.conv2d(xd, wd.cpu(), bias.double().cpu(), stride=s, padding=p)
+    got = y.float().cpu()
+    assert _rel(got, ref) < 4e-3, _rel(got, ref)
+    assert float((got.double() - ref).abs().max()) <= float(ref.abs().max()) * 2 ** -7
+    assert torch.isfinite(ps).all() and torch.isfinite(pq).all()
+    s1, s2 = ref.sum((0, 2, 3)), (ref ** 2).sum((0, 2, 3))
+    assert float((ps.sum(0).double().cpu() - s1).abs().max()) < 1e-3 * float(ref.abs().sum((0, 2, 3)).max())
+    assert _rel(pq.sum(0).cpu(), s2) < 1e-3
+    # quantisation itself: the fp8 product stays close to the unquantised bf16 operands' convolution
+    full = F.conv2d(x.double().cpu(), w.double().cpu(), bias.double().cpu(), stride=s, padding=p)
+    assert _rel(got, full) < 0.06
+
+
+def test_conv_fwd_fp8_inference_epilogue():
+    """eval BN scale / shift + SiLU + residual in the fp8 kernel's store loop == the unfused composition"""
+    from dmayolo.functional import call, ptr, stream
+    from dmayolo._lib import ACT_SILU
+    g = torch.Generator().manual_seed(9)
+    N, C, H, W, K = 2, 256, 30, 34, 128
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5).cuda()
+    sc, sh = (torch.rand(K, generator=g) + 0.5).cuda(), torch.randn(K, generator=g).cuda() * 0.2
+    res = torch.randn(N, K, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    x8, amax = _quant(x, C)
+    w8 = torch.empty(w.numel(), dtype=torch.uint8, device='cuda')
+    ws = torch.empty(K, device='cuda')
+    call('dmy_conv_wprep_fp8', ptr(w), ptr(w8), ptr(ws), K, C, 3, 3, stream())
+    z = torch.empty_like(res)
+    y = torch.empty_like(res)
+    args = (N, H, W, C, K, 3, 3, 1, 1, H, W, K)
+    call('dmy_conv_fwd_fp8', ptr(x8), ptr(w8), ptr(amax), ptr(ws), None, ptr(z), None, None, *args, None, None, 0,
+         None, 0, stream())
+    call('dmy_conv_fwd_fp8', ptr(x8), ptr(w8), ptr(amax), ptr(ws), None, ptr(y), None, None, *args, ptr(sc), ptr(sh),
+         ACT_SILU, ptr(res), K, stream())
+    torch.cuda.synchronize()
+    u = z.float() * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1)
+    ref = F.silu(u) + res.float()
+    assert _rel(y.float(), ref) < 6e-3
+
+
+def _c5_outputs(fp8, seed=0):
+    from dmayolo.models.yolo import Model
+    from dmayolo.functional import set_fp8
+    from dmayolo.utils.loss import ComputeLoss
+    from dmayolo.synthetic import images, targets, HYP_SCRATCH, scaled_hyp
+    torch.manual_seed(seed)
+    m = Model(os.path.join(ROOT, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5l-xs-tr-cbam-spp-bifpn.yaml'), nc=3,
+              act_dtype=torch.bfloat16).cuda()
+    m.hyp = scaled_hyp(HYP_SCRATCH, 3, 256)
+    n = set_fp8(m, fp8) if fp8 else 0
+    x, t = images(2, 256, device='cuda'), targets(2, 3, device='cuda')
+    out = m(x)
+    loss, items = ComputeLoss(m)(out, t)
+    return [o.float() for o in out], float(loss), n
+
+
+def test_config5_fp8_forward_close_to_bf16():
+    ref, lref, _ = _c5_outputs(False)
+    got, lgot, n = _c5_outputs(True)
+    assert n >= 20
+    for a, b in zip(got, ref):
+        cos = float(F.cosine_similarity(a.reshape(1, -1).double(), b.reshape(1, -1).double()))
+        print(f'level rel {_rel(a, b):.4f} cos {cos:.5f}')
+        assert _rel(a, b) < 0.15 and cos > 0.98
+    print(f'loss bf16 {lref:.5f} fp8 {lgot:.5f}')
+    assert abs(lgot - lref) < 0.05 * abs(lref)
