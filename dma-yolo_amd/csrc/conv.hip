@@ -2686,36 +2686,49 @@ DEV unsigned pack4_e4m3(float a, float b, float c, float d) {  // OCP e4m3fn, ro
   return (unsigned)v;
 }
 
-// amax of a bf16 NHWC activation ([rows][C] with pixel stride xps, C % 8 == 0): per-wave max, one atomicMax on
-// the float's bits (non-negative floats order as unsigned ints; a NaN sorts above +inf and propagates)
-__global__ void fp8_amax_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps, float* __restrict__ amax) {
+// Per-tensor activation scaling in two passes without atomics: fp8_blockmax_kernel writes one max per block
+// (grid G <= kF8Blocks), fp8_quant_kernel reduces those G maxima in every block (G floats from L2), records the
+// amax it used for the conv's dequantisation and writes x8[row][c] = e4m3(x * 448 / amax) densely.  A NaN
+// anywhere makes amax NaN (and so the conv output), as an unquantised conv would propagate it.
+constexpr int kF8Blocks = 1024;
+
+DEV float nanmax(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b); }
+
+DEV float block_nanmax(float m, float* red) {  // 256 threads
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = nanmax(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
+  __syncthreads();
+  return m;
+}
+
+__global__ void __launch_bounds__(256) fp8_blockmax_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps,
+                                                           float* __restrict__ bmax) {
+  __shared__ float red[4];
   float m = 0.f;
-  bool nan = false;
-  for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
     const unsigned row = v / (unsigned)cv, c8 = v - row * (unsigned)cv;
     float f[8];
     unpack<bf16>(*reinterpret_cast<const uint4*>(x + (long)row * xps + c8 * 8), f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      m = fmaxf(m, fabsf(f[j]));
-      nan |= f[j] != f[j];
-    }
+    for (int j = 0; j < 8; ++j) m = nanmax(m, fabsf(f[j]));
   }
-  if (nan) m = __builtin_nanf("");
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float t = __shfl_xor(m, o, 64);
-    m = (t != t || t > m) ? t : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(m));
+  m = block_nanmax(m, red);
+  if (threadIdx.x == 0) bmax[blockIdx.x] = m;
 }
 
-// x8[row][c] = e4m3(x[row][c] * 448 / amax), dense [rows][C] output
-__global__ void fp8_quant_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps,
-                                 unsigned char* __restrict__ q, const float* __restrict__ amax) {
-  const float a = amax[0];
+__global__ void __launch_bounds__(256) fp8_quant_kernel(const bf16* __restrict__ x, unsigned nvec, int cv, long xps,
+                                                        unsigned char* __restrict__ q, const float* __restrict__ bmax,
+                                                        int nb, float* __restrict__ used) {
+  __shared__ float red[4];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) a = nanmax(a, bmax[i]);
+  a = block_nanmax(a, red);
+  if (blockIdx.x == 0 && threadIdx.x == 0) used[0] = a;
   const float inv = a > 0.f ? 448.f / a : 1.f;
-  for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
     const unsigned row = v / (unsigned)cv, c8 = v - row * (unsigned)cv;
     float f[8];
     unpack<bf16>(*reinterpret_cast<const uint4*>(x + (long)row * xps + c8 * 8), f);
@@ -2778,15 +2791,19 @@ DMY_API int dmy_conv_fwd_act(int dtype, const void* x, const void* w, const floa
                : conv_fwd_t<float>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep);
 }
 
-DMY_API int dmy_fp8_quant(const void* x, long rows, int C, long xps, void* x8, float* amax, void* stream) {
+// ws: at least dmy_fp8_quant_ws_elems() floats; ws[0] receives the amax the quantisation used
+DMY_API int dmy_fp8_quant_ws_elems() { return 1 + kF8Blocks; }
+DMY_API int dmy_fp8_quant(const void* x, long rows, int C, long xps, void* x8, float* ws, void* stream) {
   if (C % 8 != 0 || xps % 8 != 0 || !aligned16(x) || rows * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(amax, 0, sizeof(float), st);
   const unsigned nvec = (unsigned)(rows * (C / 8));
-  if (nvec == 0) return 0;
-  const int grid = grid_cap(ceil_div(nvec, 256), 4096);
-  fp8_amax_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, amax);
-  fp8_quant_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, (unsigned char*)x8, amax);
+  if (nvec == 0) {
+    (void)hipMemsetAsync(ws, 0, sizeof(float), st);
+    return (int)hipGetLastError();
+  }
+  const int grid = grid_cap(ceil_div(nvec, 256), kF8Blocks);
+  fp8_blockmax_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, ws + 1);
+  fp8_quant_kernel<<<grid, 256, 0, st>>>((const bf16*)x, nvec, C / 8, xps, (unsigned char*)x8, ws + 1, grid, ws);
   return (int)hipGetLastError();
 }
 

@@ -236,16 +236,27 @@ def fp8_eligible(C, K, dtype, rows):
     return dtype == torch.bfloat16 and C % 128 == 0 and K % 8 == 0 and K >= 32 and rows * C < 0xFFFFFFF0
 
 
-def set_fp8(model, on=True):
-    """Config 5 (BASELINE configs[4]): run the forward of every eligible conv (input channels % 128 == 0) on the
-    fp8 e4m3 MFMA kernel; the backward stays bf16.  Returns the number of convs switched."""
+def set_fp8(model, on=True, min_k=3):
+    """Config 5 (BASELINE configs[4]): run the forward of every eligible conv (input channels % 128 == 0, kernel
+    >= min_k) on the fp8 e4m3 MFMA kernel; the backward stays bf16.  Default min_k = 3: a 1x1 layer is HBM /
+    latency-bound, so its 2x MFMA rate does not pay for quantising its input (profiles/r02, c5 fp8 A/B).
+    Returns the number of convs switched."""
     n = 0
     for m in model.modules():
-        if isinstance(m, torch.nn.Conv2d) and m.groups == 1 and m.in_channels % 128 == 0 and m.out_channels % 8 == 0:
+        if isinstance(m, torch.nn.Conv2d) and m.groups == 1 and m.in_channels % 128 == 0 and m.out_channels % 8 == 0 \
+                and m.kernel_size[0] >= min_k:
             m.dmy_fp8 = bool(on)
             n += 1
     PARAM_GEN[0] += 1  # drop cached inference weights / coefficients
     return n
+
+
+_F8_WS = [0]
+
+
+def _f8_ws():
+    _F8_WS[0] = call('dmy_fp8_quant_ws_elems')
+    return _F8_WS[0]
 
 
 def _fp8_operands(x, xps, weight, spec, wkey):
@@ -255,7 +266,7 @@ def _fp8_operands(x, xps, weight, spec, wkey):
     K, _, KH, KW = weight.shape
     rows = N * H * W
     x8 = torch.empty(rows * C, dtype=torch.uint8, device=x.device)
-    amax = f32(1, x.device)
+    amax = f32(_F8_WS[0] or _f8_ws(), x.device)  # [0] = the amax the quantisation used
     call('dmy_fp8_quant', ptr(x), rows, C, xps, ptr(x8), ptr(amax), stream())
     fc = spec.f8cache
     if fc is not None and fc[0] == wkey:

@@ -67,7 +67,8 @@ int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, i
  *      tensor with the current amax (x ~ x8 * amax / 448), weights per output channel (w ~ w8 * wscale[k]);
  *      the MX-scaled 16x16x128 MFMA runs with unit block scales and the accumulator is dequantised in the
  *      epilogue.  Requirements: C % 128 == 0, K % 8 == 0, x8 dense [N*H*W][C]. */
-int dmy_fp8_quant(const void* x_bf16, long rows, int C, long xps, void* x8, float* amax, void* stream);
+int dmy_fp8_quant_ws_elems(void);  /* float workspace of dmy_fp8_quant; ws[0] = the amax used */
+int dmy_fp8_quant(const void* x_bf16, long rows, int C, long xps, void* x8, float* ws, void* stream);
 int dmy_conv_wprep_fp8(const float* w_oihw, void* w8_ohwi, float* wscale, int K, int C, int KH, int KW, void* stream);
 int dmy_conv_fwd_fp8_partial_rows(long M, int K); /* BN partial rows of dmy_conv_fwd_fp8's epilogue */
 int dmy_conv_fwd_fp8(const void* x8, const void* w8_ohwi, const float* xamax, const float* wscale, const float* bias,
