@@ -829,9 +829,10 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page[4] = {};
 
 namespace v3 {
 constexpr int BK = 64;
-template <int BM, int BN, int NS = 3> struct Cfg3 {
+// WTR = output rows per wave (64: 64 x 64 wave tiles; 128: 128 x 64, the wide 256 x 256 block)
+template <int BM, int BN, int NS = 3, int WTR = 64> struct Cfg3 {
   static constexpr int NSTAGE = NS;
-  static constexpr int WM = BM / 64, WN = BN / 64, NW = WM * WN, NTH = NW * 64;
+  static constexpr int WM = BM / WTR, WN = BN / 64, NW = WM * WN, NTH = NW * 64;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int APW = A_BYTES / 1024 / NW, BPW = B_BYTES / 1024 / NW;  // 1-KiB pieces per wave
   static constexpr int CT = BM * (BN + 8) * 2;
@@ -947,9 +948,9 @@ struct S2Cls {
 
 // ES = operand element size in bytes: 2 (bf16, 64 elements per K step) or 1 (fp8 e4m3, 128 per K step; the
 // LDS image is byte-identical: 128-B rows of 16-B chunks)
-template <int BM, int BN, int NS, bool P1, bool DG, bool S2 = false, int ES = 2>
+template <int BM, int BN, int NS, bool P1, bool DG, bool S2 = false, int ES = 2, int WTR = 64>
 struct FwdLdsB {
-  using C3_ = Cfg3<BM, BN, NS>;
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
   static constexpr int BKE = 128 / ES;  // elements per K step
   __amdgpu_buffer_rsrc_t rx, rw;
   int H, W, C, KW, xps;
@@ -1093,11 +1094,12 @@ DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
 // Epilogue of the v3 GEMM kernels: (+bias) -> bf16 tile in LDS `ct` [BM][BN+8] + BN partials.  Partial rows
 // follow the v2 numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
 // Then 16-B stores (inference epilogue / accumulate / stride-2 class pixel mapping as configured).
-template <int BM, int BN, int NS, bool DG, int BUF>
-DEV void v3_epilogue(const f32x4 (&acc)[4][4], bf16* ct, const float* __restrict__ bias, bf16* __restrict__ y,
+template <int BM, int BN, int NS, bool DG, int BUF, int WTR = 64>
+DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __restrict__ bias, bf16* __restrict__ y,
                      float* __restrict__ psum, float* __restrict__ psq, int accumulate, const Geom& g, int tm,
                      long m0, int n0, const v3::S2Cls& cls, const Epi& ep) {
-  using C3_ = Cfg3<BM, BN, NS>;
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
+  constexpr int NI = WTR / 16, NQ = NI / 2;  // 16-row fragments and 32-row groups per wave
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long M = (long)g.N * g.OH * g.OW;
   const int wm = wid % C3_::WM, wn = wid / C3_::WM;
@@ -1108,12 +1110,14 @@ DEV void v3_epilogue(const f32x4 (&acc)[4][4], bf16* ct, const float* __restrict
   for (int j = 0; j < 4; ++j) {
     const int c = wn * 64 + j * 16 + (lane & 15);
     const float bv = (bias != nullptr && n0 + c < g.K) ? bias[n0 + c] : 0.f;
-    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+    float s1[NQ], s2[NQ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int q = 0; q < NQ; ++q) s1[q] = s2[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int row = wm * WTR + i * 16 + 4 * (lane >> 4) + r;
         const float v = acc[i][j][r] + bv;
         ct[row * RS + c] = __float2bfloat16(v);
         if (m0 + row < M) {
@@ -1123,25 +1127,31 @@ DEV void v3_epilogue(const f32x4 (&acc)[4][4], bf16* ct, const float* __restrict
       }
     if (psum != nullptr) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        s1[h] += __shfl_xor(s1[h], 16, 64);
-        s1[h] += __shfl_xor(s1[h], 32, 64);
-        s2[h] += __shfl_xor(s2[h], 16, 64);
-        s2[h] += __shfl_xor(s2[h], 32, 64);
+      for (int q = 0; q < NQ; ++q) {
+        s1[q] += __shfl_xor(s1[q], 16, 64);
+        s1[q] += __shfl_xor(s1[q], 32, 64);
+        s2[q] += __shfl_xor(s2[q], 16, 64);
+        s2[q] += __shfl_xor(s2[q], 32, 64);
       }
       const int n = n0 + c;
       if (lane < 16 && n < g.K) {
-        const long wr = (long)tm * C3_::WM + wm;  // 64-row block index
+        const long b32 = (long)tm * (BM / 32) + wm * (WTR / 32);  // first 32-row block of this wave
         if (half) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (2 * wr + h < nprow) {
-              psum[(2 * wr + h) * g.K + n] = s1[h];
-              psq[(2 * wr + h) * g.K + n] = s2[h];
+          for (int q = 0; q < NQ; ++q)
+            if (b32 + q < nprow) {
+              psum[(b32 + q) * g.K + n] = s1[q];
+              psq[(b32 + q) * g.K + n] = s2[q];
             }
-        } else if (wr < nprow) {
-          psum[wr * g.K + n] = s1[0] + s1[1];
-          psq[wr * g.K + n] = s2[0] + s2[1];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NQ; q += 2) {
+            const long wr = (b32 + q) / 2;  // 64-row block index
+            if (wr < nprow) {
+              psum[wr * g.K + n] = s1[q] + s1[q + 1];
+              psq[wr * g.K + n] = s2[q] + s2[q + 1];
+            }
+          }
         }
       }
     }
@@ -1293,6 +1303,66 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, BUF>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
                                     cls, ep);
+}
+
+// ---------------------------------------------------------------- wide tile: 256 x 256 block, 128 x 64 per wave
+// Per K step a wave reads (128 + 64) x 64 bf16 from LDS for 64 MFMAs, against (64 + 64) x 64 for 32 in the
+// 64 x 64 wave tile: the LDS array (256 B/clk/CU) stops pacing the MFMAs on the MFMA-bound layers.  2 LDS stages
+// of 64 KiB (loads of step k + 1 in flight during step k), 8 waves (2 x 4), 128 accumulator registers per lane.
+template <int BM, int BN, int NS, class LD>
+DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int lane) {
+  using C3_ = Cfg3<BM, BN, NS, 128>;
+  constexpr int PER = C3_::APW + C3_::BPW;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  ld.issue(smem, wid);
+  if (NS == 3 && nk > 1) ld.issue(smem + C3_::STAGE, wid);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
+    const bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = frag_sw(As, wm * 128 + i * 16, h * 32, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+template <bool P1, bool DG>
+__global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                  const float* __restrict__ bias, bf16* __restrict__ y,
+                                                  float* __restrict__ psum, float* __restrict__ psq, int accumulate,
+                                                  Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
+  constexpr int BM = 256, BN = 256, NS = 2;
+  using C3_ = Cfg3<BM, BN, NS, 128>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
+  FwdLdsB<BM, BN, NS, P1, DG, false, 2, 128> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+  mainloop_w<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
+                                      n0, S2Cls{0, 0, 0, 0}, ep);
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
@@ -2301,6 +2371,17 @@ inline int p1_persist_mode() {
   return t;
 }
 
+// wide 256 x 256 tiles (v3::conv_fwd_w) for GEMM views with at least this many columns (0 = off).  Default 256:
+// +9..21 % on every DMA-YOLO / yolov5s shape with >= 256 columns and >= one block per CU, 0.66-0.76x at 128
+// columns (half the tile idle) or with fewer blocks than CUs (profiles/r02/ab_wide.log)
+inline int wide_min_cols() {
+  static int t = [] {
+    const char* e = getenv("DMY_CONV_WIDE");
+    return e ? atoi(e) : 256;
+  }();
+  return t;
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st, const Epi& ep = Epi{}) {
@@ -2339,6 +2420,13 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       const unsigned grid = (unsigned)min(gm * gn, NC);
       v3::conv_p1_persist<256, 64, DG><<<grid, 256, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
     }
+    return (int)hipGetLastError();
+  }
+  if (buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
+      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
+    const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 256);
+    if (p1) v3::conv_fwd_w<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
+    else v3::conv_fwd_w<false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
     return (int)hipGetLastError();
   }
   const int pt = p1 ? p1_tile_mode() : 0;

@@ -18,7 +18,9 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           # buffer-descriptor v3 loader (C % 64 == 0): ragged M and K, 3 K steps per tap, stride 2
           (11, 128, 37, 45, 200, 3, 1), (6, 192, 52, 60, 136, 3, 1), (4, 64, 130, 122, 256, 3, 2),
           # stride-2 data-grad on the buffer loader, one launch per parity class: odd sizes, 3 K steps per tap
-          (12, 64, 75, 91, 128, 3, 2), (8, 128, 101, 99, 192, 3, 2)]
+          (12, 64, 75, 91, 128, 3, 2), (8, 128, 101, 99, 192, 3, 2),
+          # wide 256 x 256 tiles (>= 256 GEMM columns, >= one block per CU): fwd + dgrad, and dgrad of a 1x1
+          (16, 256, 64, 64, 256, 3, 1), (16, 512, 64, 64, 128, 1, 1), (17, 256, 61, 63, 264, 3, 1)]
 
 
 def _rel(a, b):

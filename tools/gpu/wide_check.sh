@@ -1,0 +1,7 @@
+# wide tile on by default: conv + model + determinism tests, then both bench configs
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_model.py tests/test_gpu_bench_shape.py tests/test_gpu_determinism.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/t_wide.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/t_wide.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/t_wide.log | head; exit $rc; }
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-detect > gpurun_out/b_wide.log 2>&1; rc=$?; echo "bench rc=$rc"; head -c 300 gpurun_out/b_wide.log; python -c "
+import json; d=json.loads(open('gpurun_out/b_wide.log').read().strip().splitlines()[-1]); print(); print('dma', d['value'], d['ms_per_step'], 'v5s', d['at_640']['value'], d['at_640']['ms_per_step'])"
+exit $rc
