@@ -1338,12 +1338,14 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
   }
 }
 
-template <bool P1, bool DG>
+// BM x BN = 256 x 256 (2 x 4 waves) or 512 x 128 (4 x 2 waves, the 128-column layers; 2 x 80 KiB of LDS)
+template <int BM, int BN, bool P1, bool DG>
 __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
-  constexpr int BM = 256, BN = 256, NS = 2;
+  constexpr int NS = 2;
+  static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
   using C3_ = Cfg3<BM, BN, NS, 128>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2382,6 +2384,17 @@ inline int wide_min_cols() {
   return t;
 }
 
+// tall 512 x 128 tiles (v3::conv_fwd_w) for k > 1 GEMM views with 65..128 columns and >= 4 blocks per CU: 0 = off,
+// 1 = on (default).  +4..8 % on the 128-channel 3x3 layers of DMA-YOLO / config 5, mixed (0.94..1.10) on 1x1 and on
+// smaller grids (profiles/r02/ab_tall.log)
+inline int tall_mode() {
+  static int t = [] {
+    const char* e = getenv("DMY_CONV_TALL");
+    return e ? atoi(e) : 1;
+  }();
+  return t;
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st, const Epi& ep = Epi{}) {
@@ -2422,13 +2435,22 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
     }
     return (int)hipGetLastError();
   }
-  if (buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
-      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
-    const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 256);
-    if (p1) v3::conv_fwd_w<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
-    else v3::conv_fwd_w<false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
-    return (int)hipGetLastError();
+#define W_GO(BM, BN)                                                                                               \
+  {                                                                                                                \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
+    if (p1) v3::conv_fwd_w<BM, BN, true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, \
+                                                                              xbytes, wbytes, ep);                \
+    else v3::conv_fwd_w<BM, BN, false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn,   \
+                                                                               xbytes, wbytes, ep);               \
+    return (int)hipGetLastError();                                                                                 \
   }
+  if (buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
+      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus())
+    W_GO(256, 256)
+  if (buf && tall_mode() && !p1 && gv.K > 64 && gv.K <= 128 &&
+      (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
+    W_GO(512, 128)
+#undef W_GO
   const int pt = p1 ? p1_tile_mode() : 0;
   if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
   else if (gv.K > 64 && pt == 2) V3_LAUNCH(128, 128, 3)

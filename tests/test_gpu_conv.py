@@ -20,7 +20,9 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           # stride-2 data-grad on the buffer loader, one launch per parity class: odd sizes, 3 K steps per tap
           (12, 64, 75, 91, 128, 3, 2), (8, 128, 101, 99, 192, 3, 2),
           # wide 256 x 256 tiles (>= 256 GEMM columns, >= one block per CU): fwd + dgrad, and dgrad of a 1x1
-          (16, 256, 64, 64, 256, 3, 1), (16, 512, 64, 64, 128, 1, 1), (17, 256, 61, 63, 264, 3, 1)]
+          (16, 256, 64, 64, 256, 3, 1), (16, 512, 64, 64, 128, 1, 1), (17, 256, 61, 63, 264, 3, 1),
+          # 512 x 128 tiles (65..128 GEMM columns, >= one block per CU), ragged M and columns
+          (32, 128, 64, 64, 128, 3, 1), (33, 128, 65, 63, 104, 1, 1)]
 
 
 def _rel(a, b):

@@ -25,6 +25,9 @@ SETS = {
               (32, 2048, 48, 48, 1024, 1, 1), (32, 256, 96, 96, 1024, 1, 1), (32, 1280, 96, 96, 256, 1, 1)],
     's2': [(32, 64, 768, 768, 128, 3, 2), (32, 128, 384, 384, 256, 3, 2), (32, 256, 192, 192, 512, 3, 2),
            (64, 32, 320, 320, 64, 3, 2), (64, 64, 160, 160, 128, 3, 2), (64, 128, 80, 80, 256, 3, 2)],
+    'c128': [(32, 128, 192, 192, 128, 3, 1), (32, 128, 384, 384, 128, 3, 1), (32, 512, 192, 192, 128, 1, 1),
+             (32, 128, 192, 192, 128, 1, 1), (32, 128, 384, 384, 128, 1, 1), (8, 128, 240, 240, 128, 3, 1),
+             (64, 128, 80, 80, 128, 3, 1), (64, 256, 80, 80, 128, 1, 1), (32, 256, 192, 192, 128, 1, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
 }
