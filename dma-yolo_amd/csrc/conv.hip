@@ -1091,13 +1091,123 @@ DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
   }
 }
 
+// The data-grad output's producer BatchNorm (+ activation): a stride-1 data-grad whose output is the complete
+// gradient of a train-mode BN layer's output writes that layer's backward-reduce partials itself (sum du and
+// sum du * xhat per 64-row block, du = dy * act'(z * scale + shift), xhat = (z - mean) * invstd -- bn.hip
+// bn_bwd_reduce_vec's arithmetic on the stored bf16 values), so bn_bwd_reduce's second read of dy disappears.
+// z == nullptr: off.
+struct BnB {
+  const bf16* z;
+  long zps;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  int act;
+  float* pdb;
+  float* pdg;
+};
+
+// store loop of the data-grad epilogue with the fused partials: ONE partial row per BM-row tile (the partial array
+// is 2 * 4 B * C per 256 rows of dx, 1/64 of dx's bytes).  Thread t keeps the 8 channels cv = t % CPR and rows
+// t / CPR + G * it; per-thread sums -> xor-shuffles over the lanes sharing cv -> per-wave rows in LDS (the ct region,
+// after a barrier) -> summed over waves in wave order.
+template <int BM, int BN, int NTH>
+DEV void store_dgrad_bn(bf16* ct, bf16* __restrict__ y, int accumulate, const Geom& g, int tm, long m0, int n0,
+                        const BnB& bb) {
+  constexpr int RS = BN + 8, CPR = BN / 8, G = NTH / CPR, IT = BM / G, NW = NTH / 64;
+  static_assert(NTH % CPR == 0 && BM % G == 0 && CPR < 64 && BN >= 128, "store_dgrad_bn tiling");
+  const long M = (long)g.N * g.OH * g.OW;
+  const int cv = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int n = n0 + cv * 8;
+  const bool colok = n < g.K;
+  float sc[8], sh[8], mu[8], is[8], sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = colok ? bb.scale[n + j] : 0.f;
+    sh[j] = colok ? bb.shift[n + j] : 0.f;
+    mu[j] = colok ? bb.mean[n + j] : 0.f;
+    is[j] = colok ? bb.invstd[n + j] : 0.f;
+    sa[j] = sb[j] = 0.f;
+  }
+  // rows in groups of HALF iterations: every z (and accumulate) load of a group is issued before any is consumed,
+  // so a thread keeps HALF 16-B loads in flight instead of one dependent load per row
+  constexpr int HALF = IT >= 8 ? 8 : IT;
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += HALF) {
+    uint4 zv[HALF], ov[HALF];
+#pragma unroll
+    for (int q = 0; q < HALF; ++q) {
+      const long m = m0 + r0 + (i0 + q) * G;
+      const long mc = (m < M && colok) ? m : m0;  // in-range row for the masked lanes
+      zv[q] = *reinterpret_cast<const uint4*>(bb.z + mc * bb.zps + (colok ? n : n0));
+      if (accumulate) ov[q] = *reinterpret_cast<const uint4*>(y + mc * g.yps + (colok ? n : n0));
+    }
+#pragma unroll
+    for (int q = 0; q < HALF; ++q) {
+      const int row = r0 + (i0 + q) * G;
+      const long m = m0 + row;
+      if (m < M && colok) {
+        uint4 v = *reinterpret_cast<const uint4*>(ct + row * RS + cv * 8);
+        if (accumulate) {
+          float a[8], b[8];
+          unpack<bf16>(v, a);
+          unpack<bf16>(ov[q], b);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[j] += b[j];
+          v = pack<bf16>(a);
+        }
+        *reinterpret_cast<uint4*>(y + m * g.yps + n) = v;
+        float f[8], zf[8];
+        unpack<bf16>(v, f);
+        unpack<bf16>(zv[q], zf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float du = f[j] * act_grad(bb.act, zf[j] * sc[j] + sh[j]);
+          sa[j] += du;
+          sb[j] += du * (zf[j] - mu[j]) * is[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[j] += __shfl_xor(sa[j], o, 64);
+      sb[j] += __shfl_xor(sb[j], o, 64);
+    }
+  __syncthreads();  // every read of ct is done: it becomes the [wave][2][BN] reduction buffer
+  float* red = reinterpret_cast<float*>(ct);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < CPR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wid * 2 + 0) * BN + cv * 8 + j] = sa[j];
+      red[(wid * 2 + 1) * BN + cv * 8 + j] = sb[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < BN; c += NTH) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int w = 0; w < NW; ++w) {
+      s1 += red[(w * 2 + 0) * BN + c];
+      s2 += red[(w * 2 + 1) * BN + c];
+    }
+    if (n0 + c < g.K) {
+      bb.pdb[(long)tm * g.K + n0 + c] = s1;
+      bb.pdg[(long)tm * g.K + n0 + c] = s2;
+    }
+  }
+}
+
 // Epilogue of the v3 GEMM kernels: (+bias) -> bf16 tile in LDS `ct` [BM][BN+8] + BN partials.  Partial rows
 // follow the v2 numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
 // Then 16-B stores (inference epilogue / accumulate / stride-2 class pixel mapping as configured).
 template <int BM, int BN, int NS, bool DG, int BUF, int WTR = 64>
 DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __restrict__ bias, bf16* __restrict__ y,
                      float* __restrict__ psum, float* __restrict__ psq, int accumulate, const Geom& g, int tm,
-                     long m0, int n0, const v3::S2Cls& cls, const Epi& ep) {
+                     long m0, int n0, const v3::S2Cls& cls, const Epi& ep, const BnB& bb = BnB{}) {
   using C3_ = Cfg3<BM, BN, NS, WTR>;
   constexpr int NI = WTR / 16, NQ = NI / 2;  // 16-row fragments and 32-row groups per wave
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1157,6 +1267,12 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
     }
   }
   __syncthreads();
+  if constexpr (DG && BUF != 3 && BN >= 128 && BM <= 256) {  // (the 512-row tile would spill its 8 partial rows)
+    if (bb.z != nullptr) {
+      store_dgrad_bn<BM, BN, C3_::NTH>(ct, y, accumulate, g, tm, m0, n0, bb);
+      return;
+    }
+  }
   constexpr int CPR = BN / 8;
   for (int e = threadIdx.x; e < BM * CPR; e += C3_::NTH) {
     const int row = e / CPR, cv = e % CPR;
@@ -1272,7 +1388,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
                                                             float* __restrict__ psum, float* __restrict__ psq,
                                                             int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                            unsigned wbytes, S2Cls cls, Epi ep) {
+                                                            unsigned wbytes, S2Cls cls, Epi ep, BnB bb) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1302,7 +1418,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   }
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, BUF>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
-                                    cls, ep);
+                                    cls, ep, bb);
 }
 
 // ---------------------------------------------------------------- wide tile: 256 x 256 block, 128 x 64 per wave
@@ -1343,7 +1459,8 @@ template <int BM, int BN, bool P1, bool DG>
 __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
-                                                  Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
+                                                  Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep,
+                                                  BnB bb) {
   constexpr int NS = 2;
   static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
   using C3_ = Cfg3<BM, BN, NS, 128>;
@@ -1364,7 +1481,7 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
   mainloop_w<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
-                                      n0, S2Cls{0, 0, 0, 0}, ep);
+                                      n0, S2Cls{0, 0, 0, 0}, ep, bb);
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
@@ -2397,7 +2514,7 @@ inline int tall_mode() {
 
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-              hipStream_t st, const Epi& ep = Epi{}) {
+              hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
@@ -2406,7 +2523,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const unsigned xbytes = buf ? (unsigned)xb : 0u, wbytes = buf ? (unsigned)wb : 0u;
 #define V3_GO(BM, BN, NS, P1_, BUF_)                                                                          \
   v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
-                                                                          wbytes, v3::S2Cls{0, 0, 0, 0}, ep)
+                                                                          wbytes, v3::S2Cls{0, 0, 0, 0}, ep, bb)
 #define V3_LAUNCH(BM, BN, NS)                                \
   {                                                          \
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN); \
@@ -2439,9 +2556,9 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   {                                                                                                                \
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
     if (p1) v3::conv_fwd_w<BM, BN, true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, \
-                                                                              xbytes, wbytes, ep);                \
+                                                                              xbytes, wbytes, ep, bb);            \
     else v3::conv_fwd_w<BM, BN, false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn,   \
-                                                                               xbytes, wbytes, ep);               \
+                                                                               xbytes, wbytes, ep, bb);           \
     return (int)hipGetLastError();                                                                                 \
   }
   if (buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
@@ -2497,18 +2614,36 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
       if (g.C > 64) {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
         v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{}, v3::BnB{});
       } else {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 64);
         v3::conv_fwd_v3<256, 64, 2, false, true, 3><<<(unsigned)gm * gn, 256, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{}, v3::BnB{});
       }
     }
   return (int)hipGetLastError();
 }
 
+// partial rows of the fused producer-BN reduce (v3::BnB) when the bf16 data-grad of this geometry runs on a stride-1
+// v3 256 x 128 / wide 256 x 256 kernel (>= 128-column tiles), else 0 (then the data-grad cannot fuse them)
+inline long dgrad_bn_rows(const Geom& g, const void* dy, const void* wt, const void* dx) {
+  const long M = (long)g.N * g.H * g.W;
+  if (dgrad_s2_v3_ok(g, dy, wt, dx) || g.S != 1 || g.OH != g.H + 2 * g.P - g.KH + 1 ||
+      g.OW != g.W + 2 * g.P - g.KW + 1 || !v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M) || g.C <= 64)
+    return 0;
+  const bool p1 = g.KH == 1 && g.KW == 1 && g.P == 0;
+  const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
+  const bool buf = conv_buf_mode() && g.K % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
+  if (p1 && buf && p1_persist_mode()) return 0;
+  if (p1 && p1_tile_mode() != 0) return 0;  // 128-row / 64-column tiles
+  if (buf && tall_mode() && !p1 && g.C <= 128 && (long)ceil_div(M, 512) * ceil_div(g.C, 128) >= 4L * num_cus())
+    return 0;  // the 512 x 128 tile (launch_v3) does not fuse them
+  return ceil_div(M, 256);  // one partial row per 256-row tile (v3 256 x 128 and wide 256 x 256)
+}
+
 template <typename T>
-int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st) {
+int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st,
+                 const v3::BnB& bb = v3::BnB{}) {
   const long M = (long)g.N * g.H * g.W / (g.S == 2 ? 4 : 1);
   if constexpr (sizeof(T) == 2) {
     if (dgrad_s2_v3_ok(g, dy, wt, dx))
@@ -2517,7 +2652,8 @@ int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& 
         v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M)) {
       // GEMM view: rows = input pixels (N, H, W), columns = C, gather dy (OH x OW x K, stride yps)
       Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 1, g.P, g.H, g.W, g.xps);
-      return launch_v3<true>((const bf16*)dy, (const bf16*)wt, nullptr, (bf16*)dx, nullptr, nullptr, acc, gv, st);
+      return launch_v3<true>((const bf16*)dy, (const bf16*)wt, nullptr, (bf16*)dx, nullptr, nullptr, acc, gv, st,
+                             Epi{}, bb);
     }
   }
   if (big_tile(M, g.C)) return launch_dgrad<T, 128, 128>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
@@ -2902,7 +3038,7 @@ DMY_API int dmy_conv_fwd_act(int dtype, const void* x, const void* w, const floa
 }
 
 // ws: at least dmy_fp8_quant_ws_elems() floats; ws[0] receives the amax the quantisation used
-DMY_API int dmy_fp8_quant_ws_elems() { return 1 + kF8Blocks; }
+DMY_API long dmy_fp8_quant_ws_elems() { return 1 + kF8Blocks; }
 DMY_API int dmy_fp8_quant(const void* x, long rows, int C, long xps, void* x8, float* ws, void* stream) {
   if (C % 8 != 0 || xps % 8 != 0 || !aligned16(x) || rows * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -2956,6 +3092,27 @@ DMY_API int dmy_conv_fwd_fp8(const void* x8, const void* w8, const float* xamax,
   else F8_GO(256, 64, 2)
 #undef F8_GO
   return (int)hipGetLastError();
+}
+
+// Data-grad that also writes the backward-reduce partials of the BatchNorm (+ act) producing the conv's input:
+// dmy_conv_dgrad_bn_rows gives the partial rows (0: this geometry cannot fuse them -- call dmy_conv_dgrad and
+// dmy_bn_bwd_reduce instead); pdb / pdg [rows][C] then feed dmy_bn_bwd_finalize like dmy_bn_bwd_reduce's.
+DMY_API long dmy_conv_dgrad_bn_rows(int dtype, const void* dy, const void* wt, const void* dx, int N, int H, int W,
+                                    int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps) {
+  if (!dtype) return 0;
+  const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  return dgrad_bn_rows(g, dy, wt, dx);
+}
+
+DMY_API int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,
+                              int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
+                              const void* z, long zps, const float* scale, const float* shift, const float* mean,
+                              const float* invstd, int act, float* pdb, float* pdg, void* stream) {
+  const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  if (!dtype || dgrad_bn_rows(g, dy, wt, dx) == 0 || zps % 8 != 0 || !aligned16(z)) return (int)hipErrorInvalidValue;
+  if ((long)N * H * W == 0 || C == 0) return 0;
+  const v3::BnB bb{(const bf16*)z, zps, scale, shift, mean, invstd, act, pdb, pdg};
+  return conv_dgrad_t<bf16>(dy, wt, dx, accumulate, g, (hipStream_t)stream, bb);
 }
 
 DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,

@@ -36,6 +36,8 @@ SIGNATURES = {
     'dmy_conv_fwd_fp8_partial_rows': [L, I],
     'dmy_conv_fwd_fp8': [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, L, P, P, I, P, L, P],
     'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, I, P],
+    'dmy_conv_dgrad_bn_rows': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L],
+    'dmy_conv_dgrad_bn': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P, L, P, P, P, P, I, P, P, P],
     # bn.hip
     'dmy_bn_partial_rows': [L],
     'dmy_bn_stats': [I, P, L, L, I, P, P, P],

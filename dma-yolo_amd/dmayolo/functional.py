@@ -5,6 +5,7 @@ throughput); master weights, BN statistics and reductions are fp32.
 Every forward/backward here launches hand-written HIP kernels; no ATen compute op sits on the
 hot path (torch is used for allocation and the current stream only).
 """
+import os
 import weakref
 
 import torch
@@ -389,9 +390,32 @@ def eval_coef(spec, dev):
     return scale, shift
 
 
+class BnLink:
+    """A train-mode BN (+ act) layer's output, as seen by the conv that consumes it: that conv's data-grad can write the
+    layer's backward-reduce partials itself (dmy_conv_dgrad_bn), saving bn_bwd_reduce's pass over dy.  `ready` holds
+    (the data-grad buffer, its pixel stride, pdb, pdg, rows); the producer's backward uses the partials only when the
+    gradient it receives IS that buffer, unmodified.  Holding the buffer keeps autograd from accumulating another
+    contribution into it in place: any other contribution then arrives as a new tensor and the producer falls back
+    to dmy_bn_bwd_reduce."""
+    __slots__ = ('z', 'zps', 'scale', 'shift', 'mean', 'invstd', 'act', 'K', 'ready')
+
+    def __init__(self, z, scale, shift, mean, invstd, act, K):
+        self.z, self.zps = z, K
+        self.scale, self.shift, self.mean, self.invstd, self.act, self.K = scale, shift, mean, invstd, act, K
+        self.ready = None
+
+
+# data-grad epilogues write the producer BN's reduce partials (dmy_conv_dgrad_bn).  Off by default
+# (DMY_FUSE_BN_REDUCE=1 turns it on): measured SLOWER end to end -- DMA-1536 140.8 -> 138.1 img/s, yolov5s@640
+# 3421 -> 3325 (profiles/r02/ab_bnfuse.log): the epilogue's extra z stream and reduction lengthen the data-grad by
+# more than the separate streaming bn_bwd_reduce pass it saves.
+FUSE_BN_REDUCE = [os.environ.get('DMY_FUSE_BN_REDUCE', '0') == '1']
+
+
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None):
+        link_in = getattr(x, '_dmy_bnlink', None)
         s2d = getattr(x, '_dmy_s2d', 0)
         K, C2, k, _ = weight.shape
         ctx.s2d = 0
@@ -487,6 +511,9 @@ class ConvBNActFn(torch.autograd.Function):
             call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y), K,
                  M, K, stream())
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
+            ctx.bnlink = None
+            if train_bn and need_grad and dt == torch.bfloat16 and FUSE_BN_REDUCE[0]:
+                ctx.bnlink = y._dmy_bnlink = BnLink(z, scale, shift, mean, invstd, spec.act, K)
         else:
             _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             if spec.act != ACT_NONE or res is not None:
@@ -498,6 +525,8 @@ class ConvBNActFn(torch.autograd.Function):
                 y = z
             ctx.save_for_backward(x, wt, z)
         ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
+        ctx.link_in = link_in if (link_in is not None and not s2d and Cp == C and link_in.K == C and
+                                  link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
         ctx.ggeom = (Hg, Wg, kg, sg, pg)
         ctx.cp = Cp
@@ -531,10 +560,23 @@ class ConvBNActFn(torch.autograd.Function):
             dz = new_act(N, K, OH, OW, z)
             ca, cb, cc = f32(K, dev), f32(K, dev), f32(K, dev)
             if ctx.train_bn:
-                P = call('dmy_bn_reduce_rows', dt, ptr(z), K, ptr(dy), dps, M, K)
-                pdb, pdg = f32(P * K, dev), f32(P * K, dev)
-                call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
-                     spec.act, M, K, ptr(pdb), ptr(pdg), stream())
+                link = getattr(ctx, 'bnlink', None)
+                rd = link.ready if link is not None else None
+                if link is not None:
+                    link.ready = None
+                if rd is not None and rd[0].data_ptr() == dy.data_ptr() and rd[1] == dps and \
+                        rd[0]._version == rd[5]:
+                    _, _, pdb, pdg, P, _ = rd  # written by the consumer's data-grad epilogue (a row per tile)
+                    if P > 256:  # two-stage column reduction, as for the forward epilogue partials
+                        S = call('dmy_colsum2_rows', P)
+                        pd2, pg2 = f32(S * K, dev), f32(S * K, dev)
+                        call('dmy_colsum2', ptr(pdb), ptr(pdg), P, K, ptr(pd2), ptr(pg2), stream())
+                        pdb, pdg, P = pd2, pg2, S
+                else:
+                    P = call('dmy_bn_reduce_rows', dt, ptr(z), K, ptr(dy), dps, M, K)
+                    pdb, pdg = f32(P * K, dev), f32(P * K, dev)
+                    call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean),
+                         ptr(invstd), spec.act, M, K, ptr(pdb), ptr(pdg), stream())
                 dgamma, dbeta = pgrad(ctx.pkeys[1]), pgrad(ctx.pkeys[2])
                 call('dmy_bn_bwd_finalize', ptr(pdb), ptr(pdg), P, K, float(M), ptr(gamma), ptr(invstd), ptr(dgamma),
                      ptr(dbeta), ptr(ca), ptr(cb), ptr(cc), stream())
@@ -569,10 +611,24 @@ class ConvBNActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if Cp != C or ctx.s2d:
                 raise NotImplementedError('input gradient of a channel-padded stem conv')
+            link = ctx.link_in
+            last = ctx.xsink is None or ctx.xsink.seen == ctx.xsink.n - 1  # this data-grad completes dx
             buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
-            KernelTimer.run('conv_dgrad', 2.0 * M * K * C * k * k, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf),
-                            acc, N, H, W, C, bps, K, k, k, s, p, OH, OW, dzps, stream(), tag=(N, C, H, W, K, k, s),
-                            nbytes=z.element_size() * (M * K + K * C * k * k + (1 + acc) * N * H * W * C))
+            kw = dict(tag=(N, C, H, W, K, k, s),
+                      nbytes=z.element_size() * (M * K + K * C * k * k + (1 + acc) * N * H * W * C))
+            fl = 2.0 * M * K * C * k * k
+            P = call('dmy_conv_dgrad_bn_rows', dt, ptr(dz), ptr(wt), ptr(buf), N, H, W, C, bps, K, k, k, s, p, OH, OW,
+                     dzps) if (link is not None and last and FUSE_BN_REDUCE[0]) else 0
+            if P > 0:
+                pdb, pdg = f32(P * C, dev), f32(P * C, dev)
+                KernelTimer.run('conv_dgrad', fl, 'dmy_conv_dgrad_bn', dt, ptr(dz), ptr(wt), ptr(buf), acc, N, H, W, C,
+                                bps, K, k, k, s, p, OH, OW, dzps, ptr(link.z), link.zps, ptr(link.scale),
+                                ptr(link.shift), ptr(link.mean), ptr(link.invstd), link.act, ptr(pdb), ptr(pdg),
+                                stream(), **kw)
+                link.ready = (buf, bps, pdb, pdg, P, buf._version)
+            else:
+                KernelTimer.run('conv_dgrad', fl, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf), acc, N, H, W, C, bps,
+                                K, k, k, s, p, OH, OW, dzps, stream(), **kw)
             dx = sink_result(ctx.xsink, buf)
         if ctx.needs_input_grad[1] and ctx.s2d:
             Cs = ctx.s2d

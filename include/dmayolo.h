@@ -35,6 +35,15 @@ int dmy_conv_fwd_act(int dtype, const void* x, const void* w_ohwi, const float* 
                      const float* shift, int act, const void* res, long rps, void* stream);
 int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
+/* data-grad + the backward-reduce partials of the train-mode BN (+ act) that produced the conv input (its z, coefficients
+ * and act; bn.hip bn_bwd_reduce arithmetic): replaces dmy_conv_dgrad + dmy_bn_bwd_reduce when the data-grad output is
+ * that BN layer's complete output gradient.  _rows: partial rows written, 0 = geometry not fusable. */
+long dmy_conv_dgrad_bn_rows(int dtype, const void* dy, const void* w_ihwo, const void* dx, int N, int H, int W, int C,
+                            long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps);
+int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
+                      long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, const void* z, long zps,
+                      const float* scale, const float* shift, const float* mean, const float* invstd, int act,
+                      float* pdb, float* pdg, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
                    int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 /* flags: 1 = write dw in torch OIHW order (the parameter's .grad layout, no wgrad_to_oihw pass; needs Cp == C),
@@ -67,7 +76,7 @@ int dmy_conv_wgrad_to_oihw(const float* dw_ohwi, float* dw_oihw, int K, int C, i
  *      tensor with the current amax (x ~ x8 * amax / 448), weights per output channel (w ~ w8 * wscale[k]);
  *      the MX-scaled 16x16x128 MFMA runs with unit block scales and the accumulator is dequantised in the
  *      epilogue.  Requirements: C % 128 == 0, K % 8 == 0, x8 dense [N*H*W][C]. */
-int dmy_fp8_quant_ws_elems(void);  /* float workspace of dmy_fp8_quant; ws[0] = the amax used */
+long dmy_fp8_quant_ws_elems(void);  /* float workspace of dmy_fp8_quant; ws[0] = the amax used */
 int dmy_fp8_quant(const void* x_bf16, long rows, int C, long xps, void* x8, float* ws, void* stream);
 int dmy_conv_wprep_fp8(const float* w_oihw, void* w8_ohwi, float* wscale, int K, int C, int KH, int KW, void* stream);
 int dmy_conv_fwd_fp8_partial_rows(long M, int K); /* BN partial rows of dmy_conv_fwd_fp8's epilogue */
