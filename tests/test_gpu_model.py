@@ -197,3 +197,20 @@ def test_graphed_train_step_matches_eager():
         assert gstep.captures == 2  # first call + the 12-targets/img batch outgrowing tcap 16
     finally:
         Fn.set_deterministic(False)
+
+
+@pytest.mark.parametrize('name', ['model_v5s', 'model_dma'])
+def test_attempt_load_fused_eval_matches_reference(name, tmp_path):
+    """§8(f) row 3: a checkpoint written by save_checkpoint and read back by attempt_load(fuse=True) -- the
+    models/experimental.py:113-131 path: ema/model entry, BN folded into every YAML-level Conv, eval -- gives the
+    reference's eval output (the fixture's unfused eval: folding is exact up to fp32 rounding)."""
+    from dmayolo.utils.ckpt import save_checkpoint, attempt_load
+    fx = Fixture(name)
+    m = _model(fx).cpu()
+    p = str(tmp_path / 'best.pt')
+    save_checkpoint(p, m, half=False)
+    fm = attempt_load(p, device='cuda', fuse=True)
+    assert not any(hasattr(mm, 'bn') for mm in fm.model if type(mm).__name__ == 'Conv')
+    with torch.no_grad():
+        z, _ = fm(fx.t('in.0').cuda())
+    torch.testing.assert_close(z.cpu(), fx.t('eout.0'), rtol=1e-3, atol=2e-3)
