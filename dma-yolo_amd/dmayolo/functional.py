@@ -1092,13 +1092,18 @@ class DropoutFn(torch.autograd.Function):
         return dx, None
 
 
+def _sample_major(t):
+    """a layout in which each sample (dim 0) is one contiguous block: NHWC for 4-D activations, else row-major"""
+    return t.contiguous(memory_format=CL) if t.dim() == 4 else t.contiguous()
+
+
 class SampleScaleFn(torch.autograd.Function):
-    """y = x * s[b] (DropPath with a pre-drawn per-sample keep mask, common.py:386-403)."""
+    """y = x * s[b] (DropPath with a pre-drawn per-sample keep mask, common.py:386-403), any rank."""
 
     @staticmethod
     def forward(ctx, x, s):
-        x = x.contiguous(memory_format=CL)
-        y = torch.empty_like(x, memory_format=CL)
+        x = _sample_major(x)
+        y = torch.empty_like(x)  # preserve_format: same strides as x
         call('dmy_sample_scale', dcode(x), ptr(x), ptr(s), ptr(y), x.numel() // x.shape[0], x.numel(), stream())
         ctx.save_for_backward(s)
         return y
@@ -1106,8 +1111,8 @@ class SampleScaleFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (s,) = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=CL)
-        dx = torch.empty_like(dy, memory_format=CL)
+        dy = _sample_major(dy)
+        dx = torch.empty_like(dy)
         call('dmy_sample_scale', dcode(dy), ptr(dy), ptr(s), ptr(dx), dy.numel() // dy.shape[0], dy.numel(), stream())
         return dx, None
 
