@@ -214,3 +214,32 @@ def test_attempt_load_fused_eval_matches_reference(name, tmp_path):
     with torch.no_grad():
         z, _ = fm(fx.t('in.0').cuda())
     torch.testing.assert_close(z.cpu(), fx.t('eout.0'), rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_detect_module_vs_reference_golden(dtype):
+    """a11: the product Detect head alone (three 1x1 convs + the dmy_detect_decode kernel) against the reference's
+    own Detect outputs (tests/golden/detect.npz): train-mode raw maps and eval-mode decoded boxes.  bf16 inputs /
+    weights: outputs within bf16 rounding of the fp32 golden (rtol 2e-2 on the raw maps, decoded boxes relative to
+    their scale)."""
+    from dmayolo.models.yolo import Detect
+    fx = Fixture('detect')
+    meta = fx.meta
+    d = Detect(meta['nc'], meta['anchors'], meta['ch'])
+    d.stride = torch.tensor(meta['stride'], dtype=torch.float32)
+    load_sd(d, fx.group('sd'))
+    d = d.cuda()
+    xs = [t.to(dtype).cuda().contiguous(memory_format=torch.channels_last) for t in fx.seq('in')]
+    d.train()
+    outs = d(xs)
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    for a, b in zip(outs, fx.seq('out')):
+        torch.testing.assert_close(a.float().cpu(), b, **tol)
+    d.eval()
+    with torch.no_grad():
+        z, _ = d(xs)
+    ref = fx.t('eout.0')
+    if dtype == torch.float32:
+        torch.testing.assert_close(z.cpu(), ref, rtol=1e-4, atol=1e-3)
+    else:
+        assert float((z.cpu() - ref).abs().max()) < 2e-2 * float(ref.abs().max())
