@@ -7,8 +7,10 @@ Differences from the reference that do not change results:
   * activations are NHWC in `Model.act_dtype` (float32 parity / bfloat16 throughput).
 """
 import math
+import weakref
 from copy import deepcopy
 from pathlib import Path
+from typing import List
 
 import torch
 import torch.nn as nn
@@ -163,6 +165,8 @@ class Model(nn.Module):
     def forward(self, x, augment=False, profile=False, visualize=False):
         if augment:
             raise NotImplementedError('test-time augmentation is outside the DMA-YOLO hot path')
+        if torch.jit.is_tracing():
+            return _traced_forward(self, x)
         return self._forward_once(x)
 
     def _s2d_stem(self, x):
@@ -332,3 +336,29 @@ def parse_model(d, ch):
             ch = []
         ch.append(c2)
     return nn.Sequential(*layers), sorted(save)
+
+
+# ------------------------------------------------------------------ torch.jit.trace support
+# The reference logs the model graph at the first batch (utils/loggers/__init__.py:86:
+# tb.add_graph(torch.jit.trace(de_parallel(model), imgs[0:1], strict=False))).  The per-layer HIP launches go
+# through ctypes, which the tracer cannot see, so under tracing the whole forward is ONE registered dispatcher op,
+# dmayolo::model_forward (torch.library): the trace records that node (and can replay it), the op runs the
+# ordinary HIP forward below the tracer.  Outputs are copies (a custom op may not return views of its
+# intermediates); train mode returns the Detect maps, eval mode (decoded boxes, maps).
+_TRACE_MODELS = weakref.WeakValueDictionary()
+
+
+@torch.library.custom_op('dmayolo::model_forward', mutates_args=())
+def _model_forward_op(x: torch.Tensor, key: int) -> List[torch.Tensor]:
+    m = _TRACE_MODELS[key]
+    with torch.no_grad():
+        y = m._forward_once(x)
+    if isinstance(y, tuple):
+        return [y[0].clone()] + [o.clone() for o in y[1]]
+    return [o.clone() for o in y]
+
+
+def _traced_forward(model, x):
+    _TRACE_MODELS[id(model)] = model
+    res = torch.ops.dmayolo.model_forward(x, id(model))
+    return list(res) if model.training else (res[0], list(res[1:]))

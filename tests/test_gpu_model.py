@@ -243,3 +243,28 @@ def test_detect_module_vs_reference_golden(dtype):
         torch.testing.assert_close(z.cpu(), ref, rtol=1e-4, atol=1e-3)
     else:
         assert float((z.cpu() - ref).abs().max()) < 2e-2 * float(ref.abs().max())
+
+
+def test_jit_trace_like_reference_logger():
+    """Missing-item #7 of round 1: the reference's train.py logs the graph at the first batch with
+    torch.jit.trace(de_parallel(model), imgs[0:1], strict=False) (utils/loggers/__init__.py:86, plots on by default).
+    Under tracing the product forward is one registered op (dmayolo::model_forward); the trace must succeed, record
+    that op, and replay to the eager outputs (train and eval mode)."""
+    import warnings
+    from dmayolo.models.yolo import Model
+    from dmayolo.synthetic import images
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5s.yaml'), nc=10, act_dtype=torch.bfloat16).cuda()
+    x = images(2, 256, device='cuda')
+    for train in (True, False):
+        m.train(train)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            tr = torch.jit.trace(m, x[0:1], strict=False)
+        assert any(n.kind() == 'dmayolo::model_forward' for n in tr.inlined_graph.nodes())
+        with torch.no_grad():
+            got, ref = tr(x[0:1]), m(x[0:1])
+        if not train:
+            got, ref = [got[0]] + list(got[1]), [ref[0]] + list(ref[1])
+        for a, b in zip(got, ref):
+            torch.testing.assert_close(a.float(), b.float(), rtol=0, atol=0)
