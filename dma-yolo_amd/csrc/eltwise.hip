@@ -25,8 +25,30 @@ template <typename T, int NV> DEV void stv(T* p, const float* f) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) p[j] = from_f<T>(f[j]);
 }
-// decompose a vector index over [N][H][W][C/NV] -> (b, h, w, c)
+// i = q * d + r with a 32-bit unsigned division when i fits (see vidx)
+DEV void divmod(long i, int d, long& q, int& r) {
+  if ((unsigned long)i < 0xFFFFFFFFul) {
+    const unsigned u = (unsigned)i, qq = u / (unsigned)d;
+    q = qq;
+    r = (int)(u - qq * (unsigned)d);
+    return;
+  }
+  q = i / d;
+  r = (int)(i % d);
+}
+
+// decompose a vector index over [N][H][W][C/NV] -> (b, h, w, c).  32-bit unsigned divisions whenever the index
+// fits (every activation here): a 64-bit division is a long software sequence, and three of them per 16-B vector
+// made the SCConv gate / pool / resize kernels VALU-bound at a third of the HBM rate.
 DEV void vidx(long i, int H, int W, int CV, int NV, int& b, int& h, int& w, int& c) {
+  if ((unsigned long)i < 0xFFFFFFFFul) {
+    const unsigned u = (unsigned)i, t0 = u / (unsigned)CV, t1 = t0 / (unsigned)W;
+    c = (int)(u - t0 * (unsigned)CV) * NV;
+    w = (int)(t0 - t1 * (unsigned)W);
+    h = (int)(t1 % (unsigned)H);
+    b = (int)(t1 / (unsigned)H);
+    return;
+  }
   c = (int)(i % CV) * NV;
   long t = i / CV;
   w = (int)(t % W);
@@ -724,8 +746,10 @@ __global__ void slice_copy_kernel(const T* __restrict__ src, long sps, T* __rest
   const int cv = VEC ? C / VW : C;
   const long total = M * cv;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / cv;
-    const int c = (int)(i % cv) * (VEC ? VW : 1);
+    long m;
+    int c;
+    divmod(i, cv, m, c);
+    c *= VEC ? VW : 1;
     if (VEC) {
       float f[VW];
       unpack<T>(*reinterpret_cast<const uint4*>(src + m * sps + c), f);
@@ -852,8 +876,9 @@ template <typename T>
 __global__ void ca_pool_fwd_kernel(const T* __restrict__ x, long xps, T* __restrict__ y, int N, int H, int W, int C) {
   const long total = (long)N * (H + W) * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    long t;
+    int c;
+    divmod(i, C, t, c);
     const int r = (int)(t % (H + W));
     const int b = (int)(t / (H + W));
     float s = 0.f;
@@ -874,8 +899,9 @@ __global__ void ca_pool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx,
                                    int H, int W, int C) {
   const long total = (long)N * H * W * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    long t;
+    int c;
+    divmod(i, C, t, c);
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
@@ -895,8 +921,9 @@ __global__ void ca_apply_fwd_kernel(const T* __restrict__ x, long xps, const T* 
                                     int C) {
   const long total = (long)N * H * W * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    long t;
+    int c;
+    divmod(i, C, t, c);
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
@@ -916,8 +943,9 @@ __global__ void ca_apply_bwd_dx_kernel(const T* __restrict__ x, long xps, const 
                                        T* __restrict__ dx, long dxps, int N, int H, int W, int C) {
   const long total = (long)N * H * W * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    long t;
+    int c;
+    divmod(i, C, t, c);
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
@@ -935,8 +963,9 @@ __global__ void ca_apply_bwd_att_kernel(const T* __restrict__ x, long xps, const
                                         T* __restrict__ dlh, T* __restrict__ dlw, int N, int H, int W, int C) {
   const long total = (long)N * (H + W) * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
+    long t;
+    int c;
+    divmod(i, C, t, c);
     const int r = (int)(t % (H + W));
     const int b = (int)(t / (H + W));
     float s = 0.f;
