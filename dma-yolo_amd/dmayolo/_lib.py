@@ -30,6 +30,9 @@ SIGNATURES = {
     'dmy_conv_wgrad_ws_elems': [I, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I],
     'dmy_conv_wgrad_det': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P, L, P],
     'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
+    # augment.hip
+    'dmy_aug_desc_bytes': [],
+    'dmy_augment_batch': [P, I, P, I, I, P],
     'dmy_fp8_quant_ws_elems': [],
     'dmy_fp8_quant': [P, L, I, L, P, P, P],
     'dmy_conv_wprep_fp8': [P, P, P, I, I, I, I, P],

@@ -3,19 +3,22 @@
 Model.to_input (uint8 -> /255 on the GPU, train.py:402 / val.py:199) and val.run.
 
 Follows utils/datasets.py: img2label_paths (370-373), the label checks of verify_image_label (884-935),
-LoadImagesAndLabels (376-656) without augmentation (the val / detect path: load_image 659-675 -> letterbox with
-the rect batch shape -> labels to pixel xyxy -> back to clipped normalised xywh -> HWC BGR to CHW RGB),
-collate_fn (624-629), create_dataloader (95-121, DistributedSampler under DDP), and letterbox
-(utils/augmentations.py:92-123).  cv2 is absent from this image (and from the reference's import path here), so
-the two resamplers it uses are restated on the host in numpy: cv2.INTER_LINEAR for 8-bit images in OpenCV's
-fixed-point form (11-bit coefficients, (v + 2^21) >> 22) and cv2.INTER_AREA as the exact box-filter average
-(round to nearest); pixel values are therefore unpinned against cv2 (letterbox geometry is pinned by the
-reference's own detect log, tutorial.ipynb:474-475).  Training augmentation (mosaic, random_perspective, HSV,
-flips, mixup) is not built: augment=True raises.
+LoadImagesAndLabels (376-656: the val / detect path load_image 659-675 -> letterbox with the rect batch shape ->
+labels to pixel xyxy -> back to clipped normalised xywh -> HWC BGR to CHW RGB; with augment=True the training
+path of 552-622: 4-mosaic + random_perspective with probability hyp['mosaic'], mixup, else letterbox +
+random_perspective, then HSV, up-down / left-right flips -- dmayolo.augment), collate_fn (624-629),
+create_dataloader (95-121, DistributedSampler under DDP), and letterbox (utils/augmentations.py:92-123).  cv2 is
+absent from this image (and from the reference's import path here), so the resamplers it uses are restated on the
+host in numpy: cv2.INTER_LINEAR for 8-bit images in OpenCV's fixed-point form (11-bit coefficients,
+(v + 2^21) >> 22), cv2.INTER_AREA as the exact box-filter average (round to nearest), and warpAffine / cvtColor
+HSV in dmayolo.augment; pixel values are therefore unpinned against cv2 (letterbox geometry is pinned by the
+reference's own detect log, tutorial.ipynb:474-475).  Albumentations (optional in the reference, absent here) is
+a no-op as in the reference without the package.
 """
 import glob
 import math
 import os
+import random
 from pathlib import Path
 
 import numpy as np
@@ -173,13 +176,16 @@ def _read_bgr(path):
 # ------------------------------------------------------------------ dataset / loader
 
 class LoadImagesAndLabels(torch.utils.data.Dataset):
-    """utils/datasets.py:376-656 for augment=False (validation, and rectangular training batches)."""
+    """utils/datasets.py:376-656 (box labels): validation / rect batches (augment=False) and the training
+    augmentation path (augment=True, hyp with the hsv_* / degrees / translate / scale / shear / perspective / flip* /
+    mosaic / mixup keys of data/hyps/*.yaml)."""
 
     def __init__(self, path, img_size=640, batch_size=16, augment=False, hyp=None, rect=False, stride=32, pad=0.0,
                  single_cls=False):
-        if augment:
-            raise NotImplementedError('training augmentation (mosaic / random_perspective / HSV / flips) is not built')
-        self.img_size, self.stride, self.rect, self.augment = img_size, stride, rect, augment
+        self.img_size, self.stride, self.rect, self.augment, self.hyp = img_size, stride, rect, augment, hyp
+        self.gpu_augment = False  # GpuAugmentLoader sets it: pixel work deferred to one kernel per batch
+        self.mosaic = augment and not rect  # load 4 images at a time into a mosaic (only during training)
+        self.mosaic_border = [-img_size // 2, -img_size // 2]
         f = []
         for p in path if isinstance(path, list) else [path]:
             p = Path(p)
@@ -208,6 +214,7 @@ class LoadImagesAndLabels(torch.utils.data.Dataset):
         bi = np.floor(np.arange(n) / batch_size).astype(np.int64)
         nb = bi[-1] + 1
         self.batch, self.n = bi, n
+        self.indices = range(n)
         if self.rect:  # datasets.py:461-483: sort by aspect ratio, one letterbox shape per batch
             s = self.shapes
             ar = s[:, 1] / s[:, 0]
@@ -240,42 +247,111 @@ class LoadImagesAndLabels(torch.utils.data.Dataset):
             im = resize_area(im, w, h) if (r < 1 and not self.augment) else resize_linear(im, w, h)
         return im, (h0, w0), im.shape[:2]
 
-    def __getitem__(self, index):
-        """datasets.py:552-622 (non-mosaic branch)"""
-        img, (h0, w0), (h, w) = self.load_image(index)
-        shape = self.batch_shapes[self.batch[index]] if self.rect else self.img_size
-        img, ratio, pad = letterbox(img, shape, auto=False, scaleup=self.augment)
-        shapes = (h0, w0), ((h / h0, w / w0), pad)  # for COCO mAP rescaling
-        labels = self.labels[index].copy()
-        if labels.size:
-            labels[:, 1:] = xywhn2xyxy(labels[:, 1:], ratio[0] * w, ratio[1] * h, padw=pad[0], padh=pad[1])
+    def record(self, index):
+        """datasets.py:552-622 up to the pixel work: every random draw in the reference's order (mosaic?, the mosaic
+        and its perspective draw, mixup? and its second mosaic and beta ratio, else letterbox + perspective draw,
+        HSV gains, up-down / left-right flips) and the final normalised labels.  -> dict with the canvas `img`, the
+        forward map `M`, output `size`, `persp`, `changed`, `mix`, `luts`, `flipud`, `fliplr`, `labels` [n, 5],
+        `shapes`; render_cpu / render_batch_gpu (dmayolo.augment) turn it into pixels."""
+        from .augment import mosaic_warp, perspective_matrix, warp_labels, hsv_luts
+        index = self.indices[index]
+        hyp = self.hyp
+        mix = None
+        if self.mosaic and random.random() < hyp['mosaic']:
+            img, M, size, persp, changed, labels = mosaic_warp(self, index)
+            shapes = None
+            if random.random() < hyp['mixup']:  # augmentations.py:271-276 (ratio drawn after the second mosaic)
+                img2, M2, _, persp2, changed2, labels2 = mosaic_warp(self, random.randint(0, self.n - 1))
+                mix = (img2, M2, persp2, changed2, np.random.beta(32.0, 32.0))
+                labels = np.concatenate((labels, labels2), 0)
+        else:
+            img, (h0, w0), (h, w) = self.load_image(index)
+            shape = self.batch_shapes[self.batch[index]] if self.rect else self.img_size
+            img, ratio, pad = letterbox(img, shape, auto=False, scaleup=self.augment)
+            shapes = (h0, w0), ((h / h0, w / w0), pad)  # for COCO mAP rescaling
+            labels = self.labels[index].copy()
+            if labels.size:
+                labels[:, 1:] = xywhn2xyxy(labels[:, 1:], ratio[0] * w, ratio[1] * h, padw=pad[0], padh=pad[1])
+            M, size, persp, changed = np.eye(3), (img.shape[1], img.shape[0]), 0.0, False
+            if self.augment:
+                persp = hyp['perspective']
+                M, sc, size, changed = perspective_matrix(img.shape, hyp['degrees'], hyp['translate'], hyp['scale'],
+                                                          hyp['shear'], persp)
+                labels = warp_labels(labels, M, sc, size, persp)
         nl = len(labels)
         if nl:
-            labels[:, 1:5] = xyxy2xywhn(labels[:, 1:5], w=img.shape[1], h=img.shape[0], clip=True, eps=1E-3)
+            labels[:, 1:5] = xyxy2xywhn(labels[:, 1:5], w=size[0], h=size[1], clip=True, eps=1E-3)
+        luts, fud, flr = None, False, False
+        if self.augment:
+            luts = hsv_luts(hyp['hsv_h'], hyp['hsv_s'], hyp['hsv_v'])
+            if random.random() < hyp['flipud']:
+                fud = True
+                if nl:
+                    labels[:, 2] = 1 - labels[:, 2]
+            if random.random() < hyp['fliplr']:
+                flr = True
+                if nl:
+                    labels[:, 1] = 1 - labels[:, 1]
+        return dict(img=img, M=M, size=size, persp=persp, changed=changed, mix=mix, luts=luts, flipud=fud,
+                    fliplr=flr, labels=labels, shapes=shapes)
+
+    def __getitem__(self, index):
+        """datasets.py:552-622.  With gpu_augment the pixel work is deferred: the item's image is the record
+        (collate_fn keeps it) and GpuAugmentLoader renders the batch on the GPU."""
+        from .augment import render_cpu
+        rec = self.record(index)
+        nl = len(rec['labels'])
         labels_out = torch.zeros((nl, 6))
         if nl:
-            labels_out[:, 1:] = torch.from_numpy(labels)
+            labels_out[:, 1:] = torch.from_numpy(rec['labels'])
+        if self.gpu_augment:
+            return rec, labels_out, self.img_files[self.indices[index]], rec['shapes']
+        img = render_cpu(rec)
         img = np.ascontiguousarray(img.transpose((2, 0, 1))[::-1])  # HWC to CHW, BGR to RGB
-        return torch.from_numpy(img), labels_out, self.img_files[index], shapes
+        return torch.from_numpy(img), labels_out, self.img_files[self.indices[index]], rec['shapes']
 
     @staticmethod
     def collate_fn(batch):
-        """datasets.py:624-629: stack images, image index into column 0 of the concatenated labels"""
+        """datasets.py:624-629: stack images, image index into column 0 of the concatenated labels (deferred
+        records -- gpu_augment -- are passed through as a list)"""
         img, label, path, shapes = zip(*batch)
         for i, lab in enumerate(label):
             lab[:, 0] = i
-        return torch.stack(img, 0), torch.cat(label, 0), path, shapes
+        imgs = list(img) if isinstance(img[0], dict) else torch.stack(img, 0)
+        return imgs, torch.cat(label, 0), path, shapes
+
+
+class GpuAugmentLoader:
+    """Iterates a DataLoader over deferred records (the workers decode, resize, compose mosaics and draw the random
+    parameters) and renders every batch with one dmy_augment_batch launch on `device`: yields
+    (uint8 [B, 3, H, W] on the GPU, targets [nt, 6], paths, shapes) like the host path, bit-identical to it."""
+
+    def __init__(self, loader, device):
+        self.loader, self.device = loader, device
+        self.dataset, self.sampler = loader.dataset, loader.sampler
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        from .augment import render_batch_gpu
+        for recs, targets, paths, shapes in self.loader:
+            yield render_batch_gpu(recs, self.device), targets, paths, shapes
 
 
 def create_dataloader(path, imgsz, batch_size, stride, single_cls=False, hyp=None, augment=False, pad=0.0, rect=False,
-                      rank=-1, workers=8, shuffle=False):
-    """utils/datasets.py:95-121 (torch DataLoader; DistributedSampler under DDP so ranks shard the images)"""
+                      rank=-1, workers=8, shuffle=False, gpu_augment=None):
+    """utils/datasets.py:95-121 (torch DataLoader; DistributedSampler under DDP so ranks shard the images).
+    gpu_augment=<device>: the augmentation tail runs on that GPU (GpuAugmentLoader)."""
     dataset = LoadImagesAndLabels(path, imgsz, batch_size, augment=augment, hyp=hyp, rect=rect, stride=int(stride),
                                   pad=pad, single_cls=single_cls)
+    dataset.gpu_augment = gpu_augment is not None
     batch_size = min(batch_size, len(dataset))
     nw = min([os.cpu_count() or 1, batch_size if batch_size > 1 else 0, workers])
     sampler = None if rank == -1 else torch.utils.data.distributed.DistributedSampler(dataset, shuffle=shuffle)
     loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle and sampler is None,
                                          num_workers=nw, sampler=sampler, pin_memory=True,
                                          collate_fn=LoadImagesAndLabels.collate_fn)
+    if gpu_augment is not None:
+        loader = GpuAugmentLoader(loader, gpu_augment)
     return loader, dataset

@@ -11,11 +11,14 @@ CONFIGS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'configs')
 # data/hyps/hyp.VisDrone.yaml (loss-relevant keys)
 HYP_VISDRONE = dict(lr0=0.0032, lrf=0.12, momentum=0.843, weight_decay=0.00036, warmup_epochs=2.0, warmup_momentum=0.5,
                     warmup_bias_lr=0.05, box=0.07, cls=0.18, cls_pw=0.631, obj=0.15, obj_pw=0.911, anchor_t=3.0,
-                    fl_gamma=0.0, label_smoothing=0.0)
+                    fl_gamma=0.0, label_smoothing=0.0, hsv_h=0.4, hsv_s=0.3, hsv_v=0.5, degrees=0.2, translate=0.0,
+                    scale=0.4, shear=0.0, perspective=0.0, flipud=0.0, fliplr=0.5, mosaic=1.0, mixup=0.2,
+                    copy_paste=0.0)
 # data/hyps/hyp.scratch.yaml
 HYP_SCRATCH = dict(lr0=0.01, lrf=0.1, momentum=0.937, weight_decay=0.0005, warmup_epochs=3.0, warmup_momentum=0.8,
                    warmup_bias_lr=0.1, box=0.05, cls=0.5, cls_pw=1.0, obj=1.0, obj_pw=1.0, anchor_t=4.0, fl_gamma=0.0,
-                   label_smoothing=0.0)
+                   label_smoothing=0.0, hsv_h=0.015, hsv_s=0.7, hsv_v=0.4, degrees=0.0, translate=0.1, scale=0.5,
+                   shear=0.0, perspective=0.0, flipud=0.0, fliplr=0.5, mosaic=1.0, mixup=0.0, copy_paste=0.0)
 
 
 def scaled_hyp(hyp, nc, imgsz, nl=3):

@@ -287,6 +287,13 @@ int dmy_process_batch(const float* det, const int* det_off, const float* lab, co
                       const float* iouv, int T, int* ws_lab, float* ws_iou, int* ws_win, unsigned char* correct,
                       void* stream);
 
+/* ---- training augmentation tail (augment.hip): utils/datasets.py:552-622 after the random draws -- warp
+ *      (cv2.warpAffine / warpPerspective INTER_LINEAR, border 114), mixup, augment_hsv, flips, BGR->RGB, HWC->CHW --
+ *      for n host-built descriptors (984-byte AugDesc: canvas pointers, inverse maps, mixup ratio, HSV LUTs,
+ *      flips; layout in dmayolo/augment.py AUG_DESC) into uint8 out [n, 3, OH, OW]. */
+long dmy_aug_desc_bytes(void);
+int dmy_augment_batch(const void* descs, int n, void* out, int OH, int OW, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
