@@ -11,6 +11,11 @@
 // canvases are read through L2 (4 taps x 3 bytes), the output planes are written coalesced.
 #include "common.h"
 
+// Every float / double operation here must round exactly as the host restatement's numpy ops do: this file is
+// built with -ffp-contract=off (__graft_entry__ FILE_FLAGS) -- with the library's -ffp-contract=fast, 1 - s * h
+// became one FMA and moved values on a rounding boundary by one level (234 of the 2^24 colours through HSV).
+#pragma clang fp contract(off)
+
 namespace {
 
 // Host-built descriptor, one per image (C ABI: 8-byte fields first; sizeof checked by dmy_aug_desc_bytes).

@@ -197,3 +197,10 @@ def test_mixup_blends_and_concatenates():
     la, lb = np.ones((2, 5)), np.zeros((3, 5))
     im, lab = A.mixup(a, la, b, lb)
     assert 130 <= int(im[0, 0, 0]) <= 170 and lab.shape == (5, 5)
+
+
+def test_aug_desc_layout_matches_library():
+    """the host-built descriptor (augment.AUG_DESC) has the C struct's size (the library loads without a GPU)"""
+    from dmayolo._lib import call
+    assert call('dmy_aug_desc_bytes') == A.AUG_DESC.itemsize == 984
+    assert A.AUG_DESC.fields['lut'][1] == 984 - 768 and A.AUG_DESC.fields['mix_r'][1] == 160

@@ -39,6 +39,7 @@ def _hyp(**kw):
 
 
 CASES = {
+    'mosaic_warp_only': dict(hsv_h=0, hsv_s=0, hsv_v=0, fliplr=0.0, mixup=0.0),
     'mosaic_hsv_flips': dict(fliplr=0.5, flipud=0.5, mixup=0.0),
     'mosaic_mixup': dict(mixup=1.0, degrees=5.0, shear=2.0),
     'mosaic_perspective': dict(perspective=0.0005, degrees=3.0, translate=0.1),
@@ -58,7 +59,29 @@ def test_gpu_tail_equals_host_tail(tmp_path, case):
     dev = render_batch_gpu(recs, torch.device('cuda')).cpu().numpy()
     assert dev.shape == host.shape == (8, 3, 160, 160)
     diff = dev.astype(int) != host.astype(int)
+    if diff.any():
+        for b, c, y, x in list(zip(*np.nonzero(diff)))[:8]:
+            print('diff at', (b, c, y, x), 'host', host[b, :, y, x], 'dev', dev[b, :, y, x])
     assert not diff.any(), f'{diff.sum()} of {diff.size} bytes differ'
+
+
+def test_gpu_hsv_exhaustive_colours():
+    """every 8-bit BGR colour through BGR2HSV -> LUTs -> HSV2BGR on the GPU (copy path, no warp) == the host"""
+    from dmayolo.augment import render_batch_gpu, apply_hsv, hsv_luts
+    c = np.arange(1 << 24, dtype=np.uint32)
+    canvas = np.stack([c & 255, (c >> 8) & 255, c >> 16], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    np.random.seed(1)
+    luts = hsv_luts(0.4, 0.7, 0.5)
+    rec = dict(img=canvas, M=np.eye(3), size=(4096, 4096), persp=0.0, changed=False, mix=None, luts=luts,
+               flipud=False, fliplr=False)
+    dev = render_batch_gpu([rec], torch.device('cuda'))[0].cpu().numpy()
+    host = canvas.copy()
+    apply_hsv(host, luts)
+    host = host.transpose(2, 0, 1)[::-1]
+    bad = np.nonzero((dev != host).any(0).reshape(-1))[0]
+    for i in bad[:8]:
+        print('colour', canvas.reshape(-1, 3)[i], 'host', host.reshape(3, -1)[:, i], 'dev', dev.reshape(3, -1)[:, i])
+    assert len(bad) == 0, f'{len(bad)} colours differ'
 
 
 def test_gpu_tail_copy_path_without_augmentation(tmp_path):
