@@ -991,6 +991,22 @@ struct FwdLdsB {
       boff[j] = n < g.K ? (unsigned)(n * Ktot + kl) * (unsigned)ES : kBufOob;
     }
   }
+  // advance the cursor by n K steps without loading (split-K: start at this split's first step)
+  DEV void skip(int n) {
+    kpos += n * BKE;
+    if (!P1) {
+      for (int i = 0; i < n; ++i) {
+        ci0 += BKE;
+        if (ci0 == C) {
+          ci0 = 0;
+          if (++kw == KW) {
+            kw = 0;
+            ++kh;
+          }
+        }
+      }
+    }
+  }
   DEV void issue(char* stage, int wid) {
     const int dh = S2 ? (ca + P - kh) >> 1 : DG ? -kh : kh, dw = S2 ? (cb + P - kw) >> 1 : DG ? -kw : kw;
     const int delta = P1 ? kpos + kl : (dh * W + dw) * xps + ci0 + kl;
@@ -1482,6 +1498,50 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
                                       n0, S2Cls{0, 0, 0, 0}, ep, bb);
+}
+
+// ---------------------------------------------------------------- split-K forward for small M (batch-1 inference)
+// At batch 1 the stride-16 / -32 layers have 2304..9216 output pixels: 128-row tiles give 18..72 row tiles, a
+// fraction of the 256 CUs, each walking the whole 9 * C reduction.  Split the K steps over blockIdx.y: every split
+// writes its fp32 partial tile to a workspace slab, splitk_epi_kernel sums the slabs in split order and applies
+// bias + the inference epilogue (eval BN, act, residual) to the bf16-rounded sum -- the same value contract as
+// the one-launch path (deterministic; rounding order differs from the unsplit kernel).
+template <int BM, int BN, int NS, bool P1>
+__global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                               float* __restrict__ ws, Geom g, int gm, int gn, int per,
+                                                               unsigned xbytes, unsigned wbytes) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  const int nk = g.KH * g.KW * g.C / BK, split = blockIdx.y;
+  const int k0 = split * per, steps = min(nk, k0 + per) - k0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (steps > 0) {
+    FwdLdsB<BM, BN, NS, P1, false> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+    ld.skip(k0);
+    mainloop4<BM, BN, NS, false>(ld, steps, smem, acc, wid, lane);
+  }
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  float* slab = ws + (long)split * M * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (m < M && n < g.K) slab[m * g.K + n] = acc[i][j][r];
+      }
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
@@ -2580,13 +2640,88 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   return (int)hipGetLastError();
 }
 
+// sum the split slabs in order, + bias, round to bf16, inference epilogue (or plain store)
+__global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict__ ws, int splits, long M, int K,
+                                                         const float* __restrict__ bias, bf16* __restrict__ y, long yps,
+                                                         Epi ep) {
+  const int CV = K / 8;
+  const long total = M * CV;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const long m = v / CV;
+    const int c = (int)(v - m * CV) * 8;
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4* src = reinterpret_cast<const float4*>(ws + ((long)sp * M + m) * K + c);
+      const float4 a = src[0], b = src[1];
+      f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
+      f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+    }
+    bf16 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = __float2bfloat16(f[j] + (bias != nullptr ? bias[c + j] : 0.f));
+    if (ep.on) epi_store<bf16, 8>(ep, t, y + m * yps + c, c, K, m, true);
+    else *reinterpret_cast<uint4*>(y + m * yps + c) = *reinterpret_cast<const uint4*>(t);
+  }
+}
+
+// split-K plan of a small-M bf16 forward (no BN partials): splits > 1 when the tile grid is under two blocks per CU
+// and the buffer loader applies; 0 = not split
+inline int splitk_plan(const Geom& g, const void* x, const void* w, const void* y, int& gm, int& gn, int& per) {
+  const long M = (long)g.N * g.OH * g.OW;
+  if (M >= 16384 || M == 0 || g.C % 64 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || g.K < 32 ||
+      !aligned16(x) || !aligned16(w) || !aligned16(y) || !conv_buf_mode())
+    return 0;
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
+  if (xb >= (double)v3::kBufOob || wb >= (double)v3::kBufOob) return 0;
+  const int BN = g.K > 64 ? 128 : 64;
+  gm = (int)ceil_div(M, 128);
+  gn = ceil_div(g.K, BN);
+  const int nk = g.KH * g.KW * g.C / v3::BK, tiles = gm * gn;
+  int splits = ceil_div(2 * num_cus(), tiles);
+  if (splits > nk / 2) splits = nk / 2;
+  if (splits < 2) return 0;
+  per = ceil_div(nk, splits);
+  return ceil_div(nk, per);
+}
+
+inline long splitk_elems(const Geom& g, const void* x, const void* w, const void* y) {
+  int gm, gn, per;
+  const int sp = splitk_plan(g, x, w, y, gm, gn, per);
+  return sp ? (long)sp * g.N * g.OH * g.OW * g.K : 0;
+}
+
+inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, const Geom& g, float* ws, hipStream_t st,
+                         const Epi& ep) {
+  int gm, gn, per;
+  const int sp = splitk_plan(g, x, w, y, gm, gn, per);
+  const long M = (long)g.N * g.OH * g.OW;
+  const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * g.KH * g.KW * g.C);
+  const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
+  const dim3 grid((unsigned)gm * gn, (unsigned)sp);
+  if (g.K > 64) {
+    if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+  } else {
+    if (p1) v3::conv_fwd_split<128, 64, 2, true><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    else v3::conv_fwd_split<128, 64, 2, false><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+  }
+  splitk_epi_kernel<<<grid_cap(ceil_div(M * (g.K / 8), 256), 4096), 256, 0, st>>>(ws, sp, M, g.K, b, y, g.yps, ep);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
-               const Epi& ep = Epi{}) {
+               const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
     if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
       return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
+    if (ws != nullptr && ps == nullptr && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res)))) {
+      const long need = splitk_elems(g, x, w, y);
+      if (need > 0 && need <= ws_elems) return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);
+    }
   }
   if (big_tile(M, g.K))
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
@@ -3113,6 +3248,27 @@ DMY_API int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* wt, void* d
   if ((long)N * H * W == 0 || C == 0) return 0;
   const v3::BnB bb{(const bf16*)z, zps, scale, shift, mean, invstd, act, pdb, pdg};
   return conv_dgrad_t<bf16>(dy, wt, dx, accumulate, g, (hipStream_t)stream, bb);
+}
+
+// Inference forward with a split-K workspace for small M (batch-1 detect): dmy_conv_fwd_act semantics; when
+// dmy_conv_fwd_splitk_elems > 0 for the same arguments, a workspace of that many floats lets the small-M layers
+// split their reduction over the chip (0: the call is dmy_conv_fwd_act).  scale == shift == res == nullptr and
+// act == 0 is the plain forward (no BN partials).
+DMY_API long dmy_conv_fwd_splitk_elems(int dtype, const void* x, const void* w, const void* y, int N, int H, int W,
+                                       int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps) {
+  if (!dtype) return 0;
+  return splitk_elems(make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps), x, w, y);
+}
+
+DMY_API int dmy_conv_fwd_act_ws(int dtype, const void* x, const void* w, const float* bias, void* y, int N, int H,
+                                int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
+                                const float* scale, const float* shift, int act, const void* res, long rps, float* ws,
+                                long ws_elems, void* stream) {
+  Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
+  if ((long)N * OH * OW == 0 || K == 0) return 0;
+  const Epi ep{scale, shift, res, rps, act, scale != nullptr || res != nullptr || act != 0 ? 1 : 0};
+  return dtype ? conv_fwd_t<bf16>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep, ws, ws_elems)
+               : conv_fwd_t<float>(x, w, bias, y, nullptr, nullptr, g, (hipStream_t)stream, ep);
 }
 
 DMY_API int dmy_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,

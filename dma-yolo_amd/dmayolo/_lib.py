@@ -26,6 +26,8 @@ SIGNATURES = {
     'dmy_conv_wgrad_s2d_to_oihw': [P, P, I, I, I, P],
     'dmy_image_s2d': [I, I, P, P, I, I, I, I, I, F, P],
     'dmy_conv_fwd_act': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P, P, I, P, L, P],
+    'dmy_conv_fwd_splitk_elems': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L],
+    'dmy_conv_fwd_act_ws': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P, P, I, P, L, P, L, P],
     'dmy_conv_wgrad_ex': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P],
     'dmy_conv_wgrad_ws_elems': [I, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I],
     'dmy_conv_wgrad_det': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P, L, P],

@@ -231,6 +231,22 @@ def spec_for(owner, stride, pad, act, bn):
     return sp
 
 
+_PSPECS = {}  # id(weight parameter) -> (weakref, {(stride, pad, act, id(bn)): ConvSpec}); tensors cannot be
+# WeakKeyDictionary keys (their == is elementwise)
+
+
+def _param_spec(w, stride, pad, act, bn):
+    k = id(w)
+    ent = _PSPECS.get(k)
+    if ent is None or ent[0]() is not w:
+        ent = _PSPECS[k] = (weakref.ref(w, lambda _r, k=k: _PSPECS.pop(k, None)), {})
+    key = (int(stride), int(pad), int(act), id(bn))
+    sp = ent[1].get(key)
+    if sp is None or sp.bn is not bn:
+        sp = ent[1][key] = ConvSpec(stride, pad, act, bn)
+    return sp
+
+
 def fp8_eligible(C, K, dtype, rows):
     """layers the e4m3 forward kernel takes (dmy_conv_fwd_fp8): bf16 activations, C % 128 == 0 (one 128-wide
     K step per tap), K % 8 == 0, and byte offsets of the quantised input below the buffer-descriptor range"""
@@ -365,6 +381,15 @@ def _launch_conv_fwd(x, xps, wf, bias, y, yps, psum, psq, K, k, s, p, OH, OW, Ca
         KernelTimer.run('conv_fwd_f8', fl, 'dmy_conv_fwd_fp8', ptr(x8), ptr(w8), ptr(amax), ptr(ws), ptr(bias), ptr(y),
                         ptr(psum), ptr(psq), N, H, W, C, K, k, k, s, p, OH, OW, yps, ptr(sc), ptr(sh), act, ptr(res),
                         rps, stream(), **kw)
+        return
+    ne = call('dmy_conv_fwd_splitk_elems', dcode(x), ptr(x), ptr(wf), ptr(y), N, H, W, C, xps, K, k, k, s, p, OH, OW,
+              yps) if psum is None else 0
+    if ne > 0:  # small M (batch-1 inference): split-K over the chip, reduced with the epilogue
+        sc, sh, act, res, rps = epi if epi is not None else (None, None, 0, None, 0)
+        ws = f32(ne, x.device)
+        KernelTimer.run('conv_fwd', fl, 'dmy_conv_fwd_act_ws', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), N, H, W,
+                        C, xps, K, k, k, s, p, OH, OW, yps, ptr(sc), ptr(sh), act, ptr(res), rps, ptr(ws), ne, stream(),
+                        **kw)
     elif epi is None:
         KernelTimer.run('conv_fwd', fl, 'dmy_conv_fwd', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(y), ptr(psum),
                         ptr(psq), N, H, W, C, xps, K, k, k, s, p, OH, OW, yps, stream(), **kw)
@@ -414,12 +439,15 @@ FUSE_BN_REDUCE = [os.environ.get('DMY_FUSE_BN_REDUCE', '0') == '1']
 
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None):
+    def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None, grad_on=True):
         link_in = getattr(x, '_dmy_bnlink', None)
         s2d = getattr(x, '_dmy_s2d', 0)
         K, C2, k, _ = weight.shape
         ctx.s2d = 0
-        need_grad = any(ctx.needs_input_grad[:6])
+        # ctx.needs_input_grad mirrors requires_grad even when the CALLER runs under torch.no_grad() (forward itself
+        # always runs with grad disabled): `grad_on` is the caller's grad mode, so a no-grad call (detect / val with
+        # parameters that require grad) takes the one-launch inference path
+        need_grad = grad_on and any(ctx.needs_input_grad[:6])
         bn = spec.bn
         train_bn = bn is not None and (bn.training or not bn.track_running_stats)
         infer = not need_grad and not train_bn  # one fused launch: conv + eval-BN + act (+ residual)
@@ -659,15 +687,17 @@ class ConvBNActFn(torch.autograd.Function):
         dres = None
         if ctx.has_res:
             dres = dy if ctx.rsink is None else ctx.rsink.passthrough(dy)
-        return dx, dw, dbias, dgamma, dbeta, dres, None, None, None
+        return dx, dw, dbias, dgamma, dbeta, dres, None, None, None, None
 
 
 def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None):
     """xsink / rsink: GradSinks collecting the gradient of x / of the residual (see GradSink)."""
-    spec = spec or ConvSpec(stride, pad, act, bn)
+    if spec is None:  # a persistent spec per weight PARAMETER (views made per call share their base), so the
+        # inference caches (prepped weight, eval BN coefficients) hold across calls for the Detect / Swin / CBAM convs
+        spec = _param_spec(weight._base if weight._base is not None else weight, stride, pad, act, bn)
     gamma = bn.weight if bn is not None else None
     beta = bn.bias if bn is not None else None
-    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec, xsink, rsink)
+    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec, xsink, rsink, torch.is_grad_enabled())
 
 
 # ------------------------------------------------------------------ pooling / resize / concat

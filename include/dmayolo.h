@@ -33,6 +33,13 @@ int dmy_conv_fwd(int dtype, const void* x, const void* w_ohwi, const float* bias
 int dmy_conv_fwd_act(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, int N, int H, int W,
                      int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, const float* scale,
                      const float* shift, int act, const void* res, long rps, void* stream);
+/* inference forward with a split-K workspace for small M (batch-1 detect, csrc conv_fwd_split + splitk_epi):
+ * dmy_conv_fwd_act semantics; ws of dmy_conv_fwd_splitk_elems floats (0 = no split for these arguments). */
+long dmy_conv_fwd_splitk_elems(int dtype, const void* x, const void* w_ohwi, const void* y, int N, int H, int W, int C,
+                               long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps);
+int dmy_conv_fwd_act_ws(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, int N, int H, int W,
+                        int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, const float* scale,
+                        const float* shift, int act, const void* res, long rps, float* ws, long ws_elems, void* stream);
 int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 /* data-grad + the backward-reduce partials of the train-mode BN (+ act) that produced the conv input (its z, coefficients

@@ -101,3 +101,40 @@ def test_conv_wgrad_bf16_vs_torch(N, C, H, W, K, k, s):
     call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, C, k, k, stream())
     torch.cuda.synchronize()
     assert _rel(dw, ref) < 2e-3
+
+
+# small-M forward (batch-1 inference) on the split-K path: (N, C, H, W, K, k, s)
+SPLIT_SHAPES = [(1, 512, 48, 48, 512, 3, 1), (1, 256, 96, 96, 256, 1, 1), (1, 1024, 24, 24, 512, 3, 2),
+                (1, 128, 40, 40, 64, 3, 1), (2, 192, 30, 34, 136, 3, 1)]
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', SPLIT_SHAPES)
+@pytest.mark.parametrize('epi', [False, True])
+def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    from dmayolo._lib import ACT_SILU
+    g = torch.Generator().manual_seed(N * 7 + C + K + k)
+    p = k // 2
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5
+    b = torch.randn(K, generator=g) * 0.1
+    ref = F.conv2d(x.float().cuda(), w.bfloat16().float().cuda(), b.cuda(), stride=s, padding=p)
+    OH, OW = ref.shape[2:]
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    wf, _ = prep_weight(w.cuda(), torch.bfloat16, False)
+    y = torch.empty(N, K, OH, OW, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
+    geo = (N, H, W, C, C, K, k, k, s, p, OH, OW, K)
+    ne = call('dmy_conv_fwd_splitk_elems', 1, ptr(xd), ptr(wf), ptr(y), *geo)
+    assert ne > 0, 'these shapes must take the split-K path'
+    ws = torch.empty(ne, device='cuda')
+    sc = (torch.rand(K, generator=g) + 0.5).cuda() if epi else None
+    sh = (torch.randn(K, generator=g) * 0.2).cuda() if epi else None
+    res = torch.randn(N, K, OH, OW, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last) \
+        if epi else None
+    call('dmy_conv_fwd_act_ws', 1, ptr(xd), ptr(wf), ptr(b.cuda()), ptr(y), *geo, ptr(sc), ptr(sh),
+         ACT_SILU if epi else 0, ptr(res), K if epi else 0, ptr(ws), ne, stream())
+    torch.cuda.synchronize()
+    if epi:
+        z = ref.bfloat16().float()  # the epilogue acts on the bf16-rounded conv output
+        ref = F.silu(z * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1)) + res.float()
+    assert _rel(y.float(), ref) < 1e-2

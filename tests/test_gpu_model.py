@@ -268,3 +268,32 @@ def test_jit_trace_like_reference_logger():
             got, ref = [got[0]] + list(got[1]), [ref[0]] + list(ref[1])
         for a, b in zip(got, ref):
             torch.testing.assert_close(a.float(), b.float(), rtol=0, atol=0)
+
+
+def test_no_grad_eval_takes_fused_path_with_trainable_params():
+    """a no-grad eval forward must use the one-launch conv + eval-BN + act kernels even when the parameters
+    require grad (detect.py / val on a freshly loaded model): ctx.needs_input_grad mirrors requires_grad under
+    torch.no_grad(), so it alone would send every layer down the training path (weight prep, separate BN)"""
+    import dmayolo.functional as Fn
+    from dmayolo.models.yolo import Model
+    from dmayolo.synthetic import images
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5s.yaml'), nc=10, act_dtype=torch.bfloat16).cuda().eval()
+    assert all(p.requires_grad for p in m.parameters())
+    x = images(1, 320, device='cuda')
+    counts = {}
+    orig = Fn.call
+
+    def counting(name, *a):
+        counts[name] = counts.get(name, 0) + 1
+        return orig(name, *a)
+    with torch.no_grad():
+        ref, _ = m(x)  # fills the per-layer caches
+        Fn.call = counting
+        try:
+            z, _ = m(x)
+        finally:
+            Fn.call = orig
+    assert counts.get('dmy_bn_act_fwd', 0) == 0 and counts.get('dmy_conv_wprep', 0) == 0, counts
+    assert counts.get('dmy_conv_fwd_act', 0) > 0
+    torch.testing.assert_close(z, ref, rtol=0, atol=0)
