@@ -1500,6 +1500,159 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
                                       n0, S2Cls{0, 0, 0, 0}, ep, bb);
 }
 
+// ---------------------------------------------------------------- 1x1 streaming GEMM (p1s)
+// Y[m][n] = sum_k X[m][k] W[n][k] for the stride-1 1x1 layers with a short reduction (KD = 64 / 128 / 256). Those
+// GEMMs are HBM-bound, and on the LDS-DMA tiles above they ran at 25-50 % of the HBM rate: one block per CU walks
+// 1..4 K steps, so a tile's time is its load prologue plus the LDS-staged epilogue with little else in flight.
+// Here a block stages its column group of W in LDS once (rows padded by 16 B: conflict-free fragment reads), then
+// each wave streams 64-pixel tiles with no block barrier: the X fragments come from HBM straight into registers
+// (16-B buffer loads, zeros past M), the MFMA runs transposed (D[ch][px] = W X^T) so a lane ends with 4 consecutive
+// channels of one pixel, and a permlane16 swap pairs two 16-channel tiles into 8 consecutive channels = one 16-B
+// store. BN partials (one row per 64 pixels, per 32 when the layer has <= 64 columns: dmy_conv_fwd_partial_rows)
+// are reduced over the 16 pixel lanes with DPP row shifts. Every X element is read once per column group.
+DEV float row_sum16(float v) {  // lane 15 of each 16-lane row ends with the row's total
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  return v;
+}
+DEV unsigned pk2_bf16(float a, float b) {
+  const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
+         ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
+}
+
+template <int KD, int NTH>
+__global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                const float* __restrict__ bias, bf16* __restrict__ y,
+                                                float* __restrict__ psum, float* __restrict__ psq, int accumulate,
+                                                long M, int NC, int ng, long xps, long yps, unsigned xbytes,
+                                                int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
+  constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
+  bf16* ws = reinterpret_cast<bf16*>(p1s_smem);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* red = reinterpret_cast<float*>(p1s_smem + ng * PITCH * 2) + wid * 64;  // this wave's [2][32] partials
+  const int c0 = blockIdx.y * ng;
+  const int ncols = min(ng, NC - c0);  // a multiple of 32
+  for (int e = threadIdx.x; e < ncols * (KD / 8); e += NTH) {
+    const int r = e / (KD / 8), c8 = e % (KD / 8);
+    *reinterpret_cast<uint4*>(ws + r * PITCH + c8 * 8) =
+        *reinterpret_cast<const uint4*>(w + (long)(c0 + r) * KD + c8 * 8);
+  }
+  const bool half = NC <= 64;
+  if (psum != nullptr && !half && (ntiles & 1) && blockIdx.x == 0) {  // the last 64-row partial row: no pixels
+    for (int n = threadIdx.x; n < ncols; n += NTH) {
+      psum[(long)ntiles * NC + c0 + n] = 0.f;
+      psq[(long)ntiles * NC + c0 + n] = 0.f;
+    }
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes);
+  const int q = lane >> 4, pl = lane & 15;
+  // this lane's 16-B output chunk of a 32-channel pair of 16-channel tiles (after the permlane16 swap)
+  const int chq = (q & 1) * 16 + (q >> 1) * 8;
+  for (int t = blockIdx.x * NW + wid; t < ntiles; t += gridDim.x * NW) {
+    const long p0 = (long)t * 64;
+    bf16x8 xf[4][KC];
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      const long m = p0 + pb * 16 + pl;
+      const unsigned base = m < M ? (unsigned)(m * xps + q * 8) * 2u : kBufOob;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const unsigned off = base == kBufOob ? kBufOob : base + kc * 64u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+      }
+    }
+    for (int ct = 0; ct < ncols; ct += 32) {
+      f32x4 acc[2][4];  // [16-channel block][16-pixel block]
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) acc[cb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + (ct + cb * 16 + pl) * PITCH + kc * 32 + q * 8);
+#pragma unroll
+          for (int pb = 0; pb < 4; ++pb)
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[pb][kc], acc[cb][pb], 0, 0, 0);
+        }
+      const int nb = c0 + ct;  // first column of this 32-column pass
+      if (bias != nullptr) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float bv = bias[nb + cb * 16 + q * 4 + r];
+#pragma unroll
+            for (int pb = 0; pb < 4; ++pb) acc[cb][pb][r] += bv;
+          }
+      }
+      if (psum != nullptr) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          if (!half && hh == 1) break;
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+              for (int pb = 0; pb < 4; ++pb) {
+                if (half && (pb >> 1) != hh) continue;
+                const float v = p0 + pb * 16 + pl < M ? acc[cb][pb][r] : 0.f;
+                s1 += v;
+                s2 += v * v;
+              }
+              s1 = row_sum16(s1);
+              s2 = row_sum16(s2);
+              if (pl == 15) {  // channel cb * 16 + q * 4 + r of this pass
+                red[cb * 16 + q * 4 + r] = s1;
+                red[32 + cb * 16 + q * 4 + r] = s2;
+              }
+            }
+          // one 64-lane store: lanes 0..31 the 32 channel sums, lanes 32..63 the sums of squares (the wave's own
+          // LDS rows: the lane-15 writes above are ordered before this read by the wave's lgkmcnt)
+          __builtin_amdgcn_wave_barrier();
+          const float v = red[lane];
+          const long row = half ? 2L * t + hh : (long)t;
+          (lane < 32 ? psum : psq)[row * NC + nb + (lane & 31)] = v;
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const long m = p0 + pb * 16 + pl;
+        const f32x4 &a = acc[0][pb], &b = acc[1][pb];
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
+        uint4 v;
+        v.x = s0[0];
+        v.y = s1[0];
+        v.z = s0[1];
+        v.w = s1[1];
+        if (m < M) {
+          uint4* dst = reinterpret_cast<uint4*>(y + m * yps + nb + chq);
+          if (accumulate) {
+            float f[8], o[8];
+            unpack<bf16>(v, f);
+            unpack<bf16>(*dst, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] += o[j];
+            v = pack<bf16>(f);
+          }
+          *dst = v;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- split-K forward for small M (batch-1 inference)
 // At batch 1 the stride-16 / -32 layers have 2304..9216 output pixels: 128-row tiles give 18..72 row tiles, a
 // fraction of the 256 CUs, each walking the whole 9 * C reduction.  Split the K steps over blockIdx.y: every split
@@ -2572,11 +2725,75 @@ inline int tall_mode() {
   return t;
 }
 
+// 1x1 streaming GEMM (v3::conv_p1s): DMY_P1S = 0 off / 1 (default) forward GEMMs with >= 2x as many columns as their
+// reduction (the output-heavy 1x1 layers, where it measured 1.05-1.38x the LDS-DMA tiles: profiles/r02/ab_p1s.log;
+// on the other 1x1 shapes those tiles already stream at 4.5-6 TB/s and stay faster) / 2 every eligible GEMM (A/B);
+// DMY_P1S_NTH = threads per block, DMY_P1S_LDS = KiB of W per block (column-group size), DMY_P1S_BPC = blocks per CU
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+inline int p1s_mode() {
+  static int t = env_int("DMY_P1S", 1);
+  return t;
+}
+inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
+  if (!p1s_mode() || gv.KH != 1 || gv.KW != 1 || gv.S != 1 || gv.P != 0) return false;
+  if (gv.C != 64 && gv.C != 128 && gv.C != 256) return false;
+  if (gv.K % 32 != 0 || gv.xps % 8 != 0 || gv.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
+    return false;
+  return 2.0 * ((double)gv.N * gv.OH * gv.OW * gv.xps) < (double)v3::kBufOob;
+}
+template <int KD, int NTH>
+int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
+                  const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
+  constexpr int pitch_b = (KD + 8) * 2, scratch = NTH / 64 * 256;
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  int ng = ((lds_kib * 1024 - scratch) / pitch_b) / 32 * 32;
+  if (ng < 32) ng = 32;
+  const int G = ceil_div(gv.K, ng);
+  ng = ceil_div(ceil_div(gv.K, G), 32) * 32;
+  const int lds = ng * pitch_b + scratch;
+  static bool raised = false;
+  if (!raised) {
+    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    raised = true;
+  }
+  const int ntiles = ceil_div(M, 64);
+  int nbx = ceil_div(ceil_div((long)num_cus() * bpc, G), 8) * 8;
+  const int maxb = ceil_div(ntiles, NTH / 64);
+  if (nbx > maxb) nbx = maxb;
+  const dim3 grid((unsigned)nbx, (unsigned)G);
+  v3::conv_p1s<KD, NTH><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps,
+                                                (unsigned)(2.0 * ((double)M * gv.xps)), ntiles);
+  return (int)hipGetLastError();
+}
+inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
+                      const Geom& gv, hipStream_t st) {
+  static const int nth = env_int("DMY_P1S_NTH", 512), lds = env_int("DMY_P1S_LDS", 160), bpc = env_int("DMY_P1S_BPC", 1);
+#define P1S_GO(KD_, NTH_) return launch_p1s_kd<KD_, NTH_>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc)
+  if (gv.C == 64) {
+    if (nth == 1024) P1S_GO(64, 1024);
+    if (nth == 512) P1S_GO(64, 512);
+    P1S_GO(64, 256);
+  }
+  if (gv.C == 128) {
+    if (nth == 768 || nth == 1024) P1S_GO(128, 768);
+    if (nth == 512) P1S_GO(128, 512);
+    P1S_GO(128, 256);
+  }
+  if (nth >= 512) P1S_GO(256, 512);
+  P1S_GO(256, 256);
+#undef P1S_GO
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
+  if (!ep.on && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
+    return launch_p1s(x, w, b, y, ps, pq, acc, gv, st);
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
   const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
@@ -2770,6 +2987,8 @@ inline long dgrad_bn_rows(const Geom& g, const void* dy, const void* wt, const v
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   const bool buf = conv_buf_mode() && g.K % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
   if (p1 && buf && p1_persist_mode()) return 0;
+  if (p1 && p1s_mode() == 2 && p1s_ok(make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, 1, 1, 1, 0, g.H, g.W, g.xps), dy, wt, dx))
+    return 0;
   if (p1 && p1_tile_mode() != 0) return 0;  // 128-row / 64-column tiles
   if (buf && tall_mode() && !p1 && g.C <= 128 && (long)ceil_div(M, 512) * ceil_div(g.C, 128) >= 4L * num_cus())
     return 0;  // the 512 x 128 tile (launch_v3) does not fuse them

@@ -22,7 +22,11 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           # wide 256 x 256 tiles (>= 256 GEMM columns, >= one block per CU): fwd + dgrad, and dgrad of a 1x1
           (16, 256, 64, 64, 256, 3, 1), (16, 512, 64, 64, 128, 1, 1), (17, 256, 61, 63, 264, 3, 1),
           # 512 x 128 tiles (65..128 GEMM columns, >= one block per CU), ragged M and columns
-          (32, 128, 64, 64, 128, 3, 1), (33, 128, 65, 63, 104, 1, 1)]
+          (32, 128, 64, 64, 128, 3, 1), (33, 128, 65, 63, 104, 1, 1),
+          # 1x1 streaming GEMM (conv_p1s, reduction 64 / 128 / 256): odd 64-row tile counts (zeroed pad partial row),
+          # 32-column passes, the per-32-row partials of <= 64-column layers, several column groups
+          (5, 128, 57, 63, 96, 1, 1), (6, 64, 55, 57, 64, 1, 1), (4, 256, 65, 67, 288, 1, 1), (5, 96, 57, 63, 128, 1, 1),
+          (3, 64, 97, 89, 544, 1, 1), (5, 128, 57, 63, 288, 1, 1)]
 
 
 def _rel(a, b):

@@ -28,6 +28,10 @@ SETS = {
     'c128': [(32, 128, 192, 192, 128, 3, 1), (32, 128, 384, 384, 128, 3, 1), (32, 512, 192, 192, 128, 1, 1),
              (32, 128, 192, 192, 128, 1, 1), (32, 128, 384, 384, 128, 1, 1), (8, 128, 240, 240, 128, 3, 1),
              (64, 128, 80, 80, 128, 3, 1), (64, 256, 80, 80, 128, 1, 1), (32, 256, 192, 192, 128, 1, 1)],
+    'p1s': [(32, 128, 192, 192, 512, 1, 1), (32, 512, 192, 192, 128, 1, 1), (32, 256, 96, 96, 256, 1, 1),
+            (32, 128, 192, 192, 128, 1, 1), (32, 64, 384, 384, 64, 1, 1), (32, 128, 384, 384, 64, 1, 1),
+            (32, 64, 384, 384, 128, 1, 1), (32, 128, 192, 192, 384, 1, 1), (32, 256, 192, 192, 128, 1, 1),
+            (32, 128, 192, 192, 256, 1, 1), (64, 64, 160, 160, 64, 1, 1), (64, 128, 80, 80, 128, 1, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
 }
@@ -62,6 +66,7 @@ def main():
         ps, pq = torch.empty(P * K, device='cuda'), torch.empty(P * K, device='cuda')
         dwo = torch.empty(K * C * k * k, device='cuda')
         fl = 2.0 * M * K * C * k * k
+        by = 2.0 * (N * H * W * C + M * K)  # algorithmic bytes: the gathered tensor once + the output / dy once
         fns = {
             'fwd': lambda: call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k,
                                 k, s, p, OH, OW, K, stream()),
@@ -72,7 +77,8 @@ def main():
         }
         for kind in kinds:
             us = bench(fns[kind])
-            print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s', flush=True)
+            print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s '
+                  f'{by / us / 1e3:7.0f} GB/s', flush=True)
 
 
 if __name__ == '__main__':
