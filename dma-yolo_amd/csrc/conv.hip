@@ -2892,12 +2892,18 @@ inline int splitk_plan(const Geom& g, const void* x, const void* w, const void* 
     return 0;
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
   if (xb >= (double)v3::kBufOob || wb >= (double)v3::kBufOob) return 0;
+  // tuning knobs (detect-path A/B, profiles/r02/det_splitk.log): DMY_SPLITK_PCT = target blocks in % of the CU count,
+  // DMY_SPLITK_P1 = 1 splits the 1x1 layers too (default 0: their fp32 slabs + the reduce pass cost more than the split
+  // gains; bs1 detect DMA-1536 6.68 -> 6.45 ms, yolov5s 1.035 -> 0.968 ms), DMY_SPLITK_MINK = fewest K steps per split
+  static const int pct = env_int("DMY_SPLITK_PCT", 200), sp1 = env_int("DMY_SPLITK_P1", 0),
+                   mink = env_int("DMY_SPLITK_MINK", 2);
+  if (!sp1 && g.KH == 1 && g.KW == 1) return 0;
   const int BN = g.K > 64 ? 128 : 64;
   gm = (int)ceil_div(M, 128);
   gn = ceil_div(g.K, BN);
   const int nk = g.KH * g.KW * g.C / v3::BK, tiles = gm * gn;
-  int splits = ceil_div(2 * num_cus(), tiles);
-  if (splits > nk / 2) splits = nk / 2;
+  int splits = ceil_div((long)pct * num_cus() / 100, tiles);
+  if (splits > nk / mink) splits = nk / mink;
   if (splits < 2) return 0;
   per = ceil_div(nk, splits);
   return ceil_div(nk, per);

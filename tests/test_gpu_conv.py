@@ -54,6 +54,15 @@ def test_conv_fwd_bf16_vs_torch(N, C, H, W, K, k, s):
     assert rc == 0
     torch.cuda.synchronize()
     assert _rel(y.float(), ref) < 1e-2
+
+
+def test_conv_fwd_1x1_small_m_unsplit():
+    from dmayolo.functional import call, ptr
+    x = torch.empty(1, 256, 96, 96, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
+    w = torch.empty(256, 256, dtype=torch.bfloat16, device='cuda')
+    y = torch.empty_like(x)
+    assert call('dmy_conv_fwd_splitk_elems', 1, ptr(x), ptr(w), ptr(y), 1, 96, 96, 256, 256, 256, 1, 1, 1, 0, 96, 96,
+                256) == 0
     assert torch.isfinite(ps).all() and torch.isfinite(pq).all(), 'every partial row must be written'
     s1 = ref.sum((0, 2, 3)).double()
     s2 = (ref.double() ** 2).sum((0, 2, 3))
@@ -107,8 +116,8 @@ def test_conv_wgrad_bf16_vs_torch(N, C, H, W, K, k, s):
     assert _rel(dw, ref) < 2e-3
 
 
-# small-M forward (batch-1 inference) on the split-K path: (N, C, H, W, K, k, s)
-SPLIT_SHAPES = [(1, 512, 48, 48, 512, 3, 1), (1, 256, 96, 96, 256, 1, 1), (1, 1024, 24, 24, 512, 3, 2),
+# small-M forward (batch-1 inference) on the split-K path: (N, C, H, W, K, k, s); 1x1 layers stay unsplit by default
+SPLIT_SHAPES = [(1, 512, 48, 48, 512, 3, 1), (1, 256, 96, 96, 256, 3, 1), (1, 1024, 24, 24, 512, 3, 2),
                 (1, 128, 40, 40, 64, 3, 1), (2, 192, 30, 34, 136, 3, 1)]
 
 
