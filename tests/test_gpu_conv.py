@@ -54,15 +54,6 @@ def test_conv_fwd_bf16_vs_torch(N, C, H, W, K, k, s):
     assert rc == 0
     torch.cuda.synchronize()
     assert _rel(y.float(), ref) < 1e-2
-
-
-def test_conv_fwd_1x1_small_m_unsplit():
-    from dmayolo.functional import call, ptr
-    x = torch.empty(1, 256, 96, 96, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
-    w = torch.empty(256, 256, dtype=torch.bfloat16, device='cuda')
-    y = torch.empty_like(x)
-    assert call('dmy_conv_fwd_splitk_elems', 1, ptr(x), ptr(w), ptr(y), 1, 96, 96, 256, 256, 256, 1, 1, 1, 0, 96, 96,
-                256) == 0
     assert torch.isfinite(ps).all() and torch.isfinite(pq).all(), 'every partial row must be written'
     s1 = ref.sum((0, 2, 3)).double()
     s2 = (ref.double() ** 2).sum((0, 2, 3))
@@ -151,3 +142,12 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
         z = ref.bfloat16().float()  # the epilogue acts on the bf16-rounded conv output
         ref = F.silu(z * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1)) + res.float()
     assert _rel(y.float(), ref) < 1e-2
+
+
+def test_conv_fwd_1x1_small_m_unsplit():
+    from dmayolo.functional import call, ptr
+    x = torch.empty(1, 256, 96, 96, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
+    w = torch.empty(256, 256, dtype=torch.bfloat16, device='cuda')
+    y = torch.empty_like(x)
+    assert call('dmy_conv_fwd_splitk_elems', 1, ptr(x), ptr(w), ptr(y), 1, 96, 96, 256, 256, 256, 1, 1, 1, 0, 96, 96,
+                256) == 0
