@@ -500,34 +500,20 @@ DEV void st4(bf16* dst, float a, float b, float c, float d) {
   *reinterpret_cast<uint2*>(dst) = v.u;
 }
 
-// lane t = token: gather the head slice (32 bf16 = 4 x 16 B) of `nm` matrices at column offsets
-// off[m] into LDS rows; padding tokens read as zeros.  Returns the token's pixel (-1 = padding).
-DEV long load_tok(const bf16* src, long sps, const SwinGeom& g, int b, int wr, int wc, int lane, int nm,
-                  const long* off, bf16* const* dst) {
-  const long p = tok_pixel(g, b, wr, wc, lane);
-  for (int m = 0; m < nm; ++m) {
-    const uint4* s = reinterpret_cast<const uint4*>(src + (p >= 0 ? p : 0) * sps + off[m]);
-    uint4* d = reinterpret_cast<uint4*>(dst[m] + lane * LQ);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) d[c] = p >= 0 ? s[c] : make_uint4(0, 0, 0, 0);
-  }
-  return p;
-}
-
 // S^T tiles (lane: query q = 16bq + il, keys 16bk + 4g + r) -> scaled, biased, masked -> softmax.
 // P[bq][bk][r] in fp32 on return.
-DEV void softmax_t(const bf16* Qs, const bf16* Ks, const float* tab, const SwinGeom& g, int wr, int wc, int lane,
-                   float (&P)[4][4][4]) {
+// qf[bq] / kf[bk]: the row fragments of queries / keys 16 b + (lane & 15), dims 8 (lane >> 4) .. + 8
+DEV void softmax_f(const bf16x8 (&qf)[4], const bf16x8 (&kf)[4], const float* tab, const SwinGeom& g, int wr, int wc,
+                   int lane, float (&P)[4][4][4]) {
   const int il = lane & 15, gq = lane >> 4;
 #pragma unroll
   for (int bq = 0; bq < 4; ++bq) {
-    const bf16x8 qf = fr_row(Qs, LQ, 16 * bq, 0, lane);
     const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
     const int lq = g.shift > 0 ? win_label(wr * WS + ri, wc * WS + ci, g.Rp, g.Cp, g.shift) : 0;
     float mx = -3.0e38f;
 #pragma unroll
     for (int bk = 0; bk < 4; ++bk) {
-      f32x4 acc = mma(fr_row(Ks, LQ, 16 * bk, 0, lane), qf, f32x4{0.f, 0.f, 0.f, 0.f});
+      f32x4 acc = mma(kf[bk], qf[bq], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
@@ -557,6 +543,17 @@ DEV void softmax_t(const bf16* Qs, const bf16* Ks, const float* tab, const SwinG
   }
 }
 
+DEV void softmax_t(const bf16* Qs, const bf16* Ks, const float* tab, const SwinGeom& g, int wr, int wc, int lane,
+                   float (&P)[4][4][4]) {
+  bf16x8 qf[4], kf[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    qf[b] = fr_row(Qs, LQ, 16 * b, 0, lane);
+    kf[b] = fr_row(Ks, LQ, 16 * b, 0, lane);
+  }
+  softmax_f(qf, kf, tab, g, wr, wc, lane, P);
+}
+
 // P (registers, S^T layout) -> Ps[q][k] bf16
 DEV void store_p(bf16* Ps, const float (&P)[4][4][4], int lane) {
   const int il = lane & 15, gq = lane >> 4;
@@ -567,56 +564,80 @@ DEV void store_p(bf16* Ps, const float (&P)[4][4][4], int lane) {
       st4(Ps + (16 * bq + il) * LP + 16 * bk + 4 * gq, P[bq][bk][0], P[bq][bk][1], P[bq][bk][2], P[bq][bk][3]);
 }
 
-// acc tiles X^T[d = 16dt + 4g + r][t = 16bt + il] -> Xs[t][d] (LQ rows)
-DEV void store_t(bf16* Xs, const f32x4 (&A)[2][4], float scale, int lane) {
-  const int il = lane & 15, gq = lane >> 4;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt)
-      st4(Xs + (16 * bt + il) * LQ + 16 * dt + 4 * gq, A[dt][bt][0] * scale, A[dt][bt][1] * scale,
-          A[dt][bt][2] * scale, A[dt][bt][3] * scale);
-}
+// 1-D grid of (window group, head) blocks in XCD-aware order: block id i runs on XCD i % 8 (round-robin dispatch), and
+// the nh heads of one window group are ids 8 h + (group % 8) (+ 8 nh per 8 groups), so they share an XCD and arrive
+// together: each head reads 64 B of every token's 128-B qkv lines, the other heads the rest of those lines, from L2
+// instead of HBM. Group counts are padded to a multiple of 8 (empty groups do nothing). Speed only: any order is correct.
+DEV int xhead(int nh) { return (int)(blockIdx.x >> 3) % nh; }
+DEV int xgroup(int nh) { return (int)(blockIdx.x & 7) + 8 * (int)(blockIdx.x / (8u * nh)); }
 
-// lane t = token: 4 x 16 B of the staged row -> dst[p * dps + off]
-DEV void store_tok(const bf16* Xs, bf16* dst, long dps, long off, long p, int lane) {
-  if (p < 0) return;
-  const uint4* s = reinterpret_cast<const uint4*>(Xs + lane * LQ);
-  uint4* d = reinterpret_cast<uint4*>(dst + p * dps + off);
+// X^T accumulator tiles (lane: d = 16 dt + 4 (lane >> 4) + r, token 16 bt + (lane & 15)) -> 16-B stores straight from
+// registers: a permlane16 swap pairs the two 16-dim tiles so each lane holds 8 consecutive dims of one token
+DEV unsigned pk2(float a, float b) {
+  const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (unsigned)*reinterpret_cast<const unsigned short*>(&x) | ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
+}
+DEV void store_direct(bf16* dst, long dps, const f32x4 (&A)[2][4], float scale, const long (&px)[4], int lane) {
+  const int gq = lane >> 4, chq = (gq & 1) * 16 + (gq >> 1) * 8;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) d[c] = s[c];
+  for (int bt = 0; bt < 4; ++bt) {
+    const f32x4 &a = A[0][bt], &b = A[1][bt];
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pk2(a[0] * scale, a[1] * scale), pk2(b[0] * scale, b[1] * scale),
+                                                     false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pk2(a[2] * scale, a[3] * scale), pk2(b[2] * scale, b[3] * scale),
+                                                     false, false);
+    uint4 v;
+    v.x = s0[0];
+    v.y = s1[0];
+    v.z = s0[1];
+    v.w = s1[1];
+    if (px[bt] >= 0) *reinterpret_cast<uint4*>(dst + px[bt] * dps + chq) = v;
+  }
 }
 
 template <int NW>
-__global__ void __launch_bounds__(64 * NW) winattn_fwd_mfma(const bf16* __restrict__ qkv,
+__global__ void __launch_bounds__(64 * NW, 2) winattn_fwd_mfma(const bf16* __restrict__ qkv,
                                                             const float* __restrict__ table, bf16* __restrict__ out,
-                                                            SwinGeom g, int nwin) {
-  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (3 * MATQ + MATP)];
+                                                            SwinGeom g, int nwin, int wpb) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (MATQ + MATP)];
   __shared__ float tab[NTAB];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, head = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int head = xhead(g.nh), grp = xgroup(g.nh);
+  const int il = lane & 15, gq = lane >> 4;
   for (int e = threadIdx.x; e < NTAB; e += blockDim.x) tab[e] = table[e * g.nh + head];
-  const int wid = blockIdx.x * NW + w;
-  const bool live = wid < nwin;
   const int nwr = g.Rp / WS, nwc = g.Cp / WS;
-  const int b = live ? wid / (nwr * nwc) : 0, wr = (wid / nwc) % nwr, wc = wid % nwc;
-  bf16* Qs = sm + w * (3 * MATQ + MATP);
-  bf16* Ks = Qs + MATQ;
-  bf16* Vs = Ks + MATQ;
+  bf16* Vs = sm + w * (MATQ + MATP);
   bf16* Ps = Vs + MATQ;
-  long p = -1;
-  if (live) {
-    const long off[3] = {(long)head * HD, (long)g.C + head * HD, 2L * g.C + head * HD};
-    bf16* const dst[3] = {Qs, Ks, Vs};
-    p = load_tok(qkv, 3L * g.C, g, b, wr, wc, lane, 3, off, dst);
-  }
-  __syncthreads();
-  if (live) {
+  const int w0 = grp * wpb, w1 = min(nwin, w0 + wpb);
+  const long offq = (long)head * HD;
+  uint4 pre[3][4];  // [Q, K, V][token block i]: 16 B of token 16 i + il at dims 8 gq
+  long ppre[4], px[4];
+  auto fetch = [&](int wn) {
+    const int bn = wn / (nwr * nwc), wrn = (wn / nwc) % nwr, wcn = wn % nwc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ppre[i] = tok_pixel(g, bn, wrn, wcn, 16 * i + il);
+      const uint4* src = reinterpret_cast<const uint4*>(qkv + (ppre[i] >= 0 ? ppre[i] : 0) * 3L * g.C + offq + gq * 8);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) pre[m][i] = ppre[i] >= 0 ? src[m * (g.C / 8)] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  __syncthreads();  // tab staged; the per-wave buffers below need no block barrier
+  if (w0 + w < w1) fetch(w0 + w);
+  for (int wid = w0 + w; wid < w1; wid += NW) {
+    const int wr = (wid / nwc) % nwr, wc = wid % nwc;
+    bf16x8 qf[4], kf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      px[i] = ppre[i];
+      qf[i] = *reinterpret_cast<const bf16x8*>(&pre[0][i]);
+      kf[i] = *reinterpret_cast<const bf16x8*>(&pre[1][i]);
+      *reinterpret_cast<uint4*>(Vs + (16 * i + il) * LQ + gq * 8) = pre[2][i];
+    }
+    if (wid + NW < w1) fetch(wid + NW);
     float P[4][4][4];
-    softmax_t(Qs, Ks, tab, g, wr, wc, lane, P);
+    softmax_f(qf, kf, tab, g, wr, wc, lane, P);
     store_p(Ps, P, lane);
-  }
-  __syncthreads();
-  if (live) {
     // O^T[d][q] = sum_k V[k][d] P[q][k]
     f32x4 O[2][4];
 #pragma unroll
@@ -628,31 +649,35 @@ __global__ void __launch_bounds__(64 * NW) winattn_fwd_mfma(const bf16* __restri
         for (int c = 0; c < 2; ++c) acc = mma(fr_col(Vs, LQ, 16 * dt, 32 * c, lane), fr_row(Ps, LP, 16 * bq, 32 * c, lane), acc);
         O[dt][bq] = acc;
       }
-    store_t(Qs, O, 1.f, lane);  // Q no longer needed
+    store_direct(out + offq, g.C, O, 1.f, px, lane);
   }
-  __syncthreads();
-  if (live) store_tok(Qs, out, g.C, (long)head * HD, p, lane);
 }
 
+// Backward, one wave per (window, head), walking every NW-th window of its group. Q, K, V, dO row fragments come straight
+// from the token rows (fragment pattern, fetched behind the current window's dV / dK / dQ); Q, K and dO are also written to LDS for the transposed
+// reads, V never is (it is only read by rows). dQ, dK, dV leave through store_direct, so LDS holds Q / K / dO / P-dS
+// (24 KiB per wave, was 29.7 with V and the output staging) and no block barrier is needed inside the loop.
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                            const float* __restrict__ table, bf16* __restrict__ dqkv,
-                                                            float* __restrict__ dtab_part, int nwin, int wpb, SwinGeom g) {
-  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (4 * MATQ + MATP)];
+                                                               const float* __restrict__ table, bf16* __restrict__ dqkv,
+                                                               float* __restrict__ dtab_part, int nwin, int wpb,
+                                                               SwinGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[NW * (3 * MATQ + MATP)];
   __shared__ float tab[NTAB], dtab[NTAB];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, head = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int head = xhead(g.nh), grp = xgroup(g.nh);
   const int il = lane & 15, gq = lane >> 4;
   for (int e = threadIdx.x; e < NTAB; e += blockDim.x) {
     tab[e] = table[e * g.nh + head];
     dtab[e] = 0.f;
   }
   const int nwr = g.Rp / WS, nwc = g.Cp / WS;
-  bf16* Qs = sm + w * (4 * MATQ + MATP);
+  bf16* Qs = sm + w * (3 * MATQ + MATP);
   bf16* Ks = Qs + MATQ;
-  bf16* Vs = Ks + MATQ;
-  bf16* Ds = Vs + MATQ;  // dO
+  bf16* Ds = Ks + MATQ;  // dO
   bf16* Ps = Ds + MATQ;  // P, then dS
-  const int w0 = blockIdx.x * wpb, w1 = min(nwin, w0 + wpb);
+  const int w0 = grp * wpb, w1 = min(nwin, w0 + wpb);
+  const long offq = (long)head * HD;
   // dS summed per (q, k) position over this wave's windows in registers; binned into the bias-table
   // gradient once per workgroup (the bin depends on (q, k) only, not on the window)
   float dsacc[4][4][4];
@@ -662,30 +687,69 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
     for (int bk = 0; bk < 4; ++bk)
 #pragma unroll
       for (int r = 0; r < 4; ++r) dsacc[bq][bk][r] = 0.f;
-  for (int base = w0; base < w1; base += NW) {
-    const int wid = base + w;
-    const bool live = wid < w1;
-    const int b = live ? wid / (nwr * nwc) : 0, wr = (wid / nwc) % nwr, wc = wid % nwc;
-    long p = -1;
-    __syncthreads();
-    if (live) {
-      const long off[3] = {(long)head * HD, (long)g.C + head * HD, 2L * g.C + head * HD};
-      bf16* const dst[3] = {Qs, Ks, Vs};
-      p = load_tok(qkv, 3L * g.C, g, b, wr, wc, lane, 3, off, dst);
-      const long offd[1] = {(long)head * HD};
-      bf16* const dstd[1] = {Ds};
-      load_tok(dout, g.C, g, b, wr, wc, lane, 1, offd, dstd);
+  uint4 pre[4][4];  // [Q, K, V, dO][token block i]: 16 B of token 16 i + il at dims 8 gq
+  long ppre[4], px[4];
+  auto fetch = [&](int wn) {
+    const int bn = wn / (nwr * nwc), wrn = (wn / nwc) % nwr, wcn = wn % nwc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ppre[i] = tok_pixel(g, bn, wrn, wcn, 16 * i + il);
+      const long pp = ppre[i] >= 0 ? ppre[i] : 0;
+      const uint4* src = reinterpret_cast<const uint4*>(qkv + pp * 3L * g.C + offq + gq * 8);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) pre[m][i] = ppre[i] >= 0 ? src[m * (g.C / 8)] : make_uint4(0, 0, 0, 0);
+      pre[3][i] = ppre[i] >= 0 ? *reinterpret_cast<const uint4*>(dout + pp * g.C + offq + gq * 8) : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+  };
+  __syncthreads();  // tab / dtab staged; the per-wave buffers below need no block barrier
+  if (w0 + w < w1) fetch(w0 + w);
+  for (int wid = w0 + w; wid < w1; wid += NW) {
+    const int wr = (wid / nwc) % nwr, wc = wid % nwc;
+    bf16x8 qf[4], kf[4], vf[4], df[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      px[i] = ppre[i];
+      qf[i] = *reinterpret_cast<const bf16x8*>(&pre[0][i]);
+      kf[i] = *reinterpret_cast<const bf16x8*>(&pre[1][i]);
+      vf[i] = *reinterpret_cast<const bf16x8*>(&pre[2][i]);
+      df[i] = *reinterpret_cast<const bf16x8*>(&pre[3][i]);
+      *reinterpret_cast<uint4*>(Qs + (16 * i + il) * LQ + gq * 8) = pre[0][i];
+      *reinterpret_cast<uint4*>(Ks + (16 * i + il) * LQ + gq * 8) = pre[1][i];
+      *reinterpret_cast<uint4*>(Ds + (16 * i + il) * LQ + gq * 8) = pre[3][i];
+    }
     float P[4][4][4];
-    if (live) {
-      softmax_t(Qs, Ks, tab, g, wr, wc, lane, P);
-      store_p(Ps, P, lane);
+    softmax_f(qf, kf, tab, g, wr, wc, lane, P);
+    store_p(Ps, P, lane);
+    // dP^T[k][q] = V[k] . dO[q]  (same layout as P);  dS = P (dP - sum_k P dP), P -> dS in registers
+#pragma unroll
+    for (int bq = 0; bq < 4; ++bq) {
+      float dp[4][4];
+      float rs = 0.f;
+#pragma unroll
+      for (int bk = 0; bk < 4; ++bk) {
+        f32x4 acc = mma(vf[bk], df[bq], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dp[bk][r] = acc[r];
+          rs += acc[r] * P[bq][bk][r];
+        }
+      }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+#pragma unroll
+      for (int bk = 0; bk < 4; ++bk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ds = P[bq][bk][r] * (dp[bk][r] - rs);
+          P[bq][bk][r] = ds;
+          dsacc[bq][bk][r] += ds;
+        }
     }
-    __syncthreads();
-    f32x4 dV[2][4], dQ[2][4], dK[2][4];
-    if (live) {
-      // dV^T[d][k] = sum_q dO[q][d] P[q][k]
+    // the row fragments are dead from here on: prefetch the next window behind dV / dK / dQ
+    if (wid + NW < w1) fetch(wid + NW);
+    {
+      // dV^T[d][k] = sum_q dO[q][d] P[q][k]  (Ps still holds P)
+      f32x4 A[2][4];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -693,65 +757,38 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < 2; ++c) acc = mma(fr_col(Ds, LQ, 16 * dt, 32 * c, lane), fr_col(Ps, LP, 16 * bk, 32 * c, lane), acc);
-          dV[dt][bk] = acc;
+          A[dt][bk] = acc;
         }
-      // dP^T[k][q] = V[k] . dO[q]  (same layout as P);  dS = P (dP - sum_k P dP)
-#pragma unroll
-      for (int bq = 0; bq < 4; ++bq) {
-        const bf16x8 df = fr_row(Ds, LQ, 16 * bq, 0, lane);
-        float dp[4][4];
-        float rs = 0.f;
-#pragma unroll
-        for (int bk = 0; bk < 4; ++bk) {
-          f32x4 acc = mma(fr_row(Vs, LQ, 16 * bk, 0, lane), df, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dp[bk][r] = acc[r];
-            rs += acc[r] * P[bq][bk][r];
-          }
-        }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-#pragma unroll
-        for (int bk = 0; bk < 4; ++bk)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float ds = P[bq][bk][r] * (dp[bk][r] - rs);
-            P[bq][bk][r] = ds;
-            dsacc[bq][bk][r] += ds;
-          }
-      }
+      store_direct(dqkv + 2L * g.C + offq, 3L * g.C, A, 1.f, px, lane);
     }
-    __syncthreads();  // all fr_col reads of P done before dS overwrites it
-    if (live) store_p(Ps, P, lane);
-    __syncthreads();
-    if (live) {
-      // dQ^T[d][q] = sum_k K[k][d] dS[q][k];  dK^T[d][k] = sum_q Q[q][d] dS[q][k]
+    store_p(Ps, P, lane);  // dS (after every read of P above: one wave's LDS accesses complete in order)
+    {
+      // dK^T[d][k] = sum_q Q[q][d] dS[q][k]
+      f32x4 A[2][4];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
-          f32x4 aq = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            aq = mma(fr_col(Ks, LQ, 16 * dt, 32 * c, lane), fr_row(Ps, LP, 16 * bt, 32 * c, lane), aq);
-            ak = mma(fr_col(Qs, LQ, 16 * dt, 32 * c, lane), fr_col(Ps, LP, 16 * bt, 32 * c, lane), ak);
-          }
-          dQ[dt][bt] = aq;
-          dK[dt][bt] = ak;
+          for (int c = 0; c < 2; ++c) acc = mma(fr_col(Qs, LQ, 16 * dt, 32 * c, lane), fr_col(Ps, LP, 16 * bt, 32 * c, lane), acc);
+          A[dt][bt] = acc;
         }
+      store_direct(dqkv + g.C + offq, 3L * g.C, A, g.scale, px, lane);
     }
-    __syncthreads();
-    if (live) {
-      store_t(Qs, dQ, g.scale, lane);
-      store_t(Ks, dK, g.scale, lane);
-      store_t(Vs, dV, 1.f, lane);
-    }
-    __syncthreads();
-    if (live) {
-      store_tok(Qs, dqkv, 3L * g.C, (long)head * HD, p, lane);
-      store_tok(Ks, dqkv, 3L * g.C, (long)g.C + head * HD, p, lane);
-      store_tok(Vs, dqkv, 3L * g.C, 2L * g.C + head * HD, p, lane);
+    {
+      // dQ^T[d][q] = sum_k K[k][d] dS[q][k]
+      f32x4 A[2][4];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 2; ++c) acc = mma(fr_col(Ks, LQ, 16 * dt, 32 * c, lane), fr_row(Ps, LP, 16 * bt, 32 * c, lane), acc);
+          A[dt][bt] = acc;
+        }
+      store_direct(dqkv + offq, 3L * g.C, A, g.scale, px, lane);
     }
   }
 #pragma unroll
@@ -766,7 +803,7 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
       }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) dtab_part[((long)blockIdx.x * g.nh + head) * NTAB + e] = dtab[e];
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) dtab_part[((long)grp * g.nh + head) * NTAB + e] = dtab[e];
 }
 
 SwinGeom make(int B, int H, int W, int C, int nh, int shift, float scale) {
@@ -845,8 +882,11 @@ DMY_API int dmy_winattn_fwd(int dtype, const void* qkv, const float* table, void
   dim3 grid(nwin, nh);
   if (dtype) {
     constexpr int NW = 2;
-    dim3 gm(ceil_div(nwin, NW), nh);
-    winattn_fwd_mfma<NW><<<gm, 64 * NW, 0, (hipStream_t)stream>>>((const bf16*)qkv, table, (bf16*)out, g, nwin);
+    long groups = 4096 / (nh > 0 ? nh : 1);  // ~4096 blocks: every window group keeps a prefetch chain of a few windows
+    if (groups > ceil_div(nwin, NW)) groups = ceil_div(nwin, NW);
+    const int wpb = ceil_div(nwin, groups);
+    const int g8 = ceil_div(ceil_div(nwin, wpb), 8) * 8;  // xgroup / xhead order
+    winattn_fwd_mfma<NW><<<g8 * nh, 64 * NW, 0, (hipStream_t)stream>>>((const bf16*)qkv, table, (bf16*)out, g, nwin, wpb);
   } else winattn_fwd_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)qkv, table, (float*)out, g);
   return (int)hipGetLastError();
 }
@@ -856,7 +896,7 @@ DMY_API int dmy_winattn_bwd_groups(int B, int H, int W, int nh) {
   long groups = 2048 / (nh > 0 ? nh : 1);
   if (groups < 1) groups = 1;
   if (groups > nwin) groups = nwin;
-  return (int)groups;
+  return (int)((groups + 7) / 8 * 8);  // padded for the bf16 kernel's xgroup / xhead order (empty groups write zeros)
 }
 
 // every real pixel lies in exactly one window, so dqkv is fully written (padding tokens have no storage)
@@ -870,7 +910,7 @@ DMY_API int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const 
   const int wpb = (nwin + groups - 1) / groups;
   dim3 grid(groups, nh);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype) winattn_bwd_mfma<2><<<grid, 128, 0, st>>>((const bf16*)qkv, (const bf16*)dout, table, (bf16*)dqkv, dtab_part, nwin, wpb, g);
+  if (dtype) winattn_bwd_mfma<2><<<groups * nh, 128, 0, st>>>((const bf16*)qkv, (const bf16*)dout, table, (bf16*)dqkv, dtab_part, nwin, wpb, g);
   else winattn_bwd_kernel<float><<<grid, 256, 0, st>>>((const float*)qkv, (const float*)dout, table, (float*)dqkv, dtab_part, nwin, wpb, g);
   const int ntab = (2 * WS - 1) * (2 * WS - 1) * nh;
   dtab_reduce_kernel<<<ntab, 256, 0, st>>>(dtab_part, groups, nh, dtab);
