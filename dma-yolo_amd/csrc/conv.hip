@@ -1437,6 +1437,41 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
                                     cls, ep, bb);
 }
 
+// All four output-parity classes of a stride-2 data-grad in ONE launch. Block u (XCD-contiguous order, xcd_remap) takes
+// class u % 4 and tile u / 4, so the four classes' tiles over the same dy rows run together on one XCD and share its
+// L2 (as four launches every class re-read dy: PMC traffic 1.35x the algorithmic bytes of the data-grad family), and
+// the short 1-tap class-(0,0) tiles fill in behind the 4-tap ones instead of each launch draining separately.
+// g = the layer's forward geometry; per class the GEMM view is the one launch_dgrad_s2_v3 builds on the host.
+template <int BM, int BN, int NS>
+__global__ void __launch_bounds__(BM * BN / 64) conv_dgrad_s2_v3(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
+                                                                 bf16* __restrict__ dx, int accumulate, Geom g, int gmax,
+                                                                 int gn, unsigned xbytes, unsigned wbytes) {
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int u = xcd_remap(blockIdx.x, 4 * gmax * gn);
+  const int a = (u >> 1) & 1, b = u & 1, t = u >> 2, tm = t / gn, tn = t % gn;
+  Geom gv = g;  // GEMM view of class (a, b): gather dy (OH x OW x K, stride yps), rows = the class's input pixels
+  gv.H = g.OH; gv.W = g.OW; gv.C = g.K; gv.xps = g.yps; gv.K = g.C; gv.S = 2;
+  gv.OH = (g.H - a + 1) / 2; gv.OW = (g.W - b + 1) / 2; gv.yps = g.xps;
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const long m0 = (long)tm * BM;
+  if (gv.OH <= 0 || gv.OW <= 0 || m0 >= M) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = tn * BN;
+  const S2Cls cls{a, b, g.H, g.W};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = ((gv.KH - ((a + gv.P) & 1) + 1) / 2) * ((gv.KW - ((b + gv.P) & 1) + 1) / 2) * (gv.C / BK);
+  FwdLdsB<BM, BN, NS, false, true, true> ld(dy, wt, gv, M, m0, n0, wid, lane, xbytes, wbytes, cls);
+  mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, true, 3>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr, accumulate, gv, tm,
+                                    m0, n0, cls, Epi{}, BnB{});
+}
+
 // ---------------------------------------------------------------- wide tile: 256 x 256 block, 128 x 64 per wave
 // Per K step a wave reads (128 + 64) x 64 bf16 from LDS for 64 MFMAs, against (64 + 64) x 64 for 32 in the
 // 64 x 64 wave tile: the LDS array (256 B/clk/CU) stops pacing the MFMAs on the MFMA-bound layers.  2 LDS stages
@@ -2961,6 +2996,24 @@ inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const 
 inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc, const Geom& g, hipStream_t st) {
   const unsigned xbytes = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned wbytes = (unsigned)(2.0 * g.C * g.KH * g.KW * g.K);
+  // DMY_S2_MERGE: 0 one launch per parity class, 1 (default) one launch for <= 64-channel data-grads, 2 always.
+  // Measured (profiles/r02/ab_s2_merge.log): +4..14 % at 32 / 64 channels, 16-33 % slower on the 1-block-per-CU
+  // 256 x 128 tiles of the 128 / 256-channel layers, where the per-class launches stay.
+  static const int merged = env_int("DMY_S2_MERGE", 1);
+  if (merged == 2 || (merged == 1 && g.C <= 64)) {
+    const long Mmax = (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2);  // class (0, 0) has the most rows
+    const int gmax = ceil_div(Mmax, 256);
+    if (g.C > 64) {
+      const int gn = ceil_div(g.C, 128);
+      v3::conv_dgrad_s2_v3<256, 128, 3><<<(unsigned)(4 * gmax * gn), 512, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes,
+                                                                                 wbytes);
+    } else {
+      const int gn = ceil_div(g.C, 64);
+      v3::conv_dgrad_s2_v3<256, 64, 2><<<(unsigned)(4 * gmax * gn), 256, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes,
+                                                                                wbytes);
+    }
+    return (int)hipGetLastError();
+  }
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
       const int H2 = (g.H - a + 1) / 2, W2 = (g.W - b + 1) / 2;
