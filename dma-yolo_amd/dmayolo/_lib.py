@@ -109,6 +109,8 @@ SIGNATURES = {
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
     'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P],
+    'dmy_nms_mask_rows': [],
+    'dmy_nms_greedy_mask': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P, P],
     # metrics.hip
     'dmy_process_batch': [P, P, P, P, I, P, I, P, P, P, P, P],
     # swin.hip

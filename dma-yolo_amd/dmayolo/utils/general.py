@@ -1,6 +1,7 @@
 """utils/general.py counterparts on the hot path: make_divisible, box converters, and the
 batched gfx950 non_max_suppression (utils/general.py:633-725)."""
 import math
+import os
 
 import torch
 
@@ -63,6 +64,14 @@ def _pow2(n, lo=2048):
 
 
 _CAP_HINT = {}  # (A, nc, multi) -> sort capacity that held every image's candidates last time
+_MASK_CAP = []
+
+
+def _mask_cap():
+    """largest sort capacity the bitmask NMS path (dmy_nms_greedy_mask) takes; DMY_NMS_MASK=0 keeps the lazy kernel"""
+    if not _MASK_CAP:
+        _MASK_CAP.append(call('dmy_nms_mask_rows') if os.environ.get('DMY_NMS_MASK', '1') != '0' else 0)
+    return _MASK_CAP[0]
 
 
 def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False,
@@ -105,8 +114,13 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
         call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), nimg, stream())
         boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
         out = torch.empty((nimg, max_det, 6), dtype=torch.float32, device=dev)
-        call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
-             ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
+        if cap <= _mask_cap():  # IoU bitmask + one-wave scan (same keep set and order as the lazy greedy kernel)
+            mask = torch.empty(nimg * cap * (cap // 64), dtype=torch.int64, device=dev)
+            call('dmy_nms_greedy_mask', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det),
+                 max_nms, ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(mask), ptr(out), ptr(cnt[nimg:]), stream())
+        else:
+            call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
+                 ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
         h = cnt.tolist()  # the one host synchronisation
         need = max(h[:nimg])
         if need <= cap:

@@ -194,6 +194,11 @@ int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, int nimg
 int dmy_nms_greedy(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det, int max_nms,
                    const unsigned long long* keys, long cap, const int* counts, float* boxes, float* out, int* nkeep,
                    void* stream);
+/* the same greedy keep set / order through an IoU bitmask (cap <= dmy_nms_mask_rows(); mask: nimg * cap * cap / 64 words) */
+int dmy_nms_mask_rows(void);
+int dmy_nms_greedy_mask(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det, int max_nms,
+                        const unsigned long long* keys, long cap, const int* counts, float* boxes,
+                        unsigned long long* mask, float* out, int* nkeep, void* stream);
 
 /* ---- Swin / C3STR (models/common.py:452-654): LayerNorm, shifted-window attention core with the
  *      reference's mask semantics, per-sample DropPath scale (common.py:386-403) */

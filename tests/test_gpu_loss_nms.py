@@ -114,3 +114,51 @@ def test_nms_vs_oracle_random(seed):
     ref = onms(pred, **kw)
     for a, b in zip(out, ref):
         assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize('case', [0, 1, 2, 3])
+def test_nms_bitmask_path_vs_oracle(case):
+    """Candidate counts that fit the bitmask path (sort capacity <= dmy_nms_mask_rows()): dense clusters, ties in the
+    score order, class offsets, agnostic mode and a max_det that stops inside a 64-row block; bit-exact vs oracle and
+    vs the lazy greedy kernel on the same sorted keys."""
+    from dmayolo.functional import call, ptr, stream
+    from dmayolo.utils.general import non_max_suppression
+    from oracle.general import non_max_suppression as onms
+    g = torch.Generator().manual_seed(100 + case)
+    A, nc = (3000, 5) if case < 3 else (900, 3)
+    pred = torch.rand(2, A, nc + 5, generator=g)
+    pred[..., :2] *= 200 if case != 1 else 60  # case 1: heavy overlap
+    pred[..., 2:4] = pred[..., 2:4] * 40 + 1
+    if case == 2:
+        pred[..., 4] = torch.round(pred[..., 4] * 8) / 8  # many exact score ties
+    kw = [dict(conf_thres=0.3, iou_thres=0.45, max_det=300), dict(conf_thres=0.25, iou_thres=0.5, max_det=77),
+          dict(conf_thres=0.2, iou_thres=0.6, agnostic=True, max_det=1000),
+          dict(conf_thres=0.05, iou_thres=0.45, multi_label=True, max_det=300)][case]
+    out = non_max_suppression(pred.cuda(), **kw)
+    ref = onms(pred, **kw)
+    for a, b in zip(out, ref):
+        assert torch.equal(a.cpu(), b)
+    # the two greedy kernels on identical sorted keys
+    p = pred.cuda().contiguous()
+    cap = 4096
+    cnt = torch.zeros(4, dtype=torch.int32, device='cuda')
+    keys = torch.empty((2, cap), dtype=torch.int64, device='cuda')
+    multi = int(kw.get('multi_label', False))
+    call('dmy_nms_candidates', ptr(p), 2, A, nc + 5, float(kw['conf_thres']), multi, None, ptr(keys), cap, ptr(cnt),
+         stream())
+    call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), 2, stream())
+    assert int(cnt[:2].max()) <= cap
+    res = []
+    for fn in ('dmy_nms_greedy', 'dmy_nms_greedy_mask'):
+        boxes = torch.empty((2, 30000, 5), device='cuda')
+        o = torch.full((2, kw['max_det'], 6), float('nan'), device='cuda')
+        nk = torch.zeros(2, dtype=torch.int32, device='cuda')
+        args = [ptr(p), 2, A, nc + 5, float(kw['iou_thres']), int(kw.get('agnostic', False)), kw['max_det'], 30000,
+                ptr(keys), cap, ptr(cnt), ptr(boxes)]
+        if fn.endswith('mask'):
+            args.append(ptr(torch.empty(2 * cap * (cap // 64), dtype=torch.int64, device='cuda')))
+        call(fn, *args, ptr(o), ptr(nk), stream())
+        torch.cuda.synchronize()
+        res.append([o[b, :int(nk[b])].cpu() for b in range(2)])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
