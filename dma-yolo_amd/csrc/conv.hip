@@ -1558,12 +1558,15 @@ DEV unsigned pk2_bf16(float a, float b) {
          ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
 }
 
-template <int KD, int NTH>
+// G3: the same streaming GEMM over a 3x3 stride-1 pad-1 gather of a 16-channel input (the space-to-depth stem of every
+// yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
+// 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
+template <int KD, int NTH, bool G3 = false>
 __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                 long M, int NC, int ng, long xps, long yps, unsigned xbytes,
-                                                int ntiles) {
+                                                int ntiles, int kwrow, int H, int W) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
   bf16* ws = reinterpret_cast<bf16*>(p1s_smem);
@@ -1574,7 +1577,7 @@ __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1
   for (int e = threadIdx.x; e < ncols * (KD / 8); e += NTH) {
     const int r = e / (KD / 8), c8 = e % (KD / 8);
     *reinterpret_cast<uint4*>(ws + r * PITCH + c8 * 8) =
-        *reinterpret_cast<const uint4*>(w + (long)(c0 + r) * KD + c8 * 8);
+        c8 * 8 < kwrow ? *reinterpret_cast<const uint4*>(w + (long)(c0 + r) * kwrow + c8 * 8) : make_uint4(0, 0, 0, 0);
   }
   const bool half = NC <= 64;
   if (psum != nullptr && !half && (ntiles & 1) && blockIdx.x == 0) {  // the last 64-row partial row: no pixels
@@ -1594,12 +1597,24 @@ __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1
 #pragma unroll
     for (int pb = 0; pb < 4; ++pb) {
       const long m = p0 + pb * 16 + pl;
-      const unsigned base = m < M ? (unsigned)(m * xps + q * 8) * 2u : kBufOob;
+      if constexpr (G3) {
+        const int mm = m < M ? (int)m : 0, ow = mm % W, oh = (mm / W) % H, bi = mm / (W * H);
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const unsigned off = base == kBufOob ? kBufOob : base + kc * 64u;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-        xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+        for (int kc = 0; kc < KC; ++kc) {
+          const int tap = 2 * kc + (q >> 1), kh = tap / 3, kw = tap - 3 * kh, ih = oh + kh - 1, iw = ow + kw - 1;
+          const bool ok = m < M && tap < 9 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+          const unsigned off = ok ? (unsigned)(((bi * H + ih) * W + iw) * (int)xps + 8 * (q & 1)) * 2u : kBufOob;
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+          xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+        }
+      } else {
+        const unsigned base = m < M ? (unsigned)(m * xps + q * 8) * 2u : kBufOob;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const unsigned off = base == kBufOob ? kBufOob : base + kc * 64u;
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+          xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+        }
       }
     }
     for (int ct = 0; ct < ncols; ct += 32) {
@@ -2779,7 +2794,15 @@ inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) 
     return false;
   return 2.0 * ((double)gv.N * gv.OH * gv.OW * gv.xps) < (double)v3::kBufOob;
 }
-template <int KD, int NTH>
+// the k3 s1 p1 view of the space-to-depth stem (16 input channels): DMY_P1S_STEM = 0 keeps the LDS-DMA tile
+inline bool stem_s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
+  static const int on = env_int("DMY_P1S_STEM", 1);
+  if (!on || gv.C != 16 || gv.KH != 3 || gv.KW != 3 || gv.S != 1 || gv.P != 1 || gv.OH != gv.H || gv.OW != gv.W) return false;
+  if (gv.K % 32 != 0 || gv.K > 256 || gv.xps % 8 != 0 || gv.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
+    return false;
+  return 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps) < (double)v3::kBufOob && (long)gv.N * gv.H * gv.W < (1L << 31);
+}
+template <int KD, int NTH, bool G3 = false>
 int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
                   const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
   constexpr int pitch_b = (KD + 8) * 2, scratch = NTH / 64 * 256;
@@ -2791,7 +2814,8 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   const int lds = ng * pitch_b + scratch;
   static bool raised = false;
   if (!raised) {
-    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     raised = true;
   }
   const int ntiles = ceil_div(M, 64);
@@ -2799,8 +2823,9 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   const int maxb = ceil_div(ntiles, NTH / 64);
   if (nbx > maxb) nbx = maxb;
   const dim3 grid((unsigned)nbx, (unsigned)G);
-  v3::conv_p1s<KD, NTH><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps,
-                                                (unsigned)(2.0 * ((double)M * gv.xps)), ntiles);
+  const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps);
+  v3::conv_p1s<KD, NTH, G3><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
+                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W);
   return (int)hipGetLastError();
 }
 inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
@@ -2829,6 +2854,8 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   if (!ep.on && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
     return launch_p1s(x, w, b, y, ps, pq, acc, gv, st);
+  if (!DG && !ep.on && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
+    return launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
   const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;

@@ -26,7 +26,10 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           # 1x1 streaming GEMM (conv_p1s, reduction 64 / 128 / 256): odd 64-row tile counts (zeroed pad partial row),
           # 32-column passes, the per-32-row partials of <= 64-column layers, several column groups
           (5, 128, 57, 63, 96, 1, 1), (6, 64, 55, 57, 64, 1, 1), (4, 256, 65, 67, 288, 1, 1), (5, 96, 57, 63, 128, 1, 1),
-          (3, 64, 97, 89, 544, 1, 1), (5, 128, 57, 63, 288, 1, 1)]
+          (3, 64, 97, 89, 544, 1, 1), (5, 128, 57, 63, 288, 1, 1),
+          # the 16-channel k3 view of the space-to-depth stem on the streaming GEMM's 3x3 gather (zero taps at the
+          # borders, odd tile count, 32-column pass)
+          (5, 16, 61, 67, 64, 3, 1), (8, 16, 64, 64, 32, 3, 1), (3, 16, 97, 99, 96, 3, 1)]
 
 
 def _rel(a, b):

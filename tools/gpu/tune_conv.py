@@ -32,6 +32,7 @@ SETS = {
             (32, 128, 192, 192, 128, 1, 1), (32, 64, 384, 384, 64, 1, 1), (32, 128, 384, 384, 64, 1, 1),
             (32, 64, 384, 384, 128, 1, 1), (32, 128, 192, 192, 384, 1, 1), (32, 256, 192, 192, 128, 1, 1),
             (32, 128, 192, 192, 256, 1, 1), (64, 64, 160, 160, 64, 1, 1), (64, 128, 80, 80, 128, 1, 1)],
+    'stem': [(32, 16, 768, 768, 64, 3, 1), (64, 16, 320, 320, 32, 3, 1), (8, 16, 960, 960, 64, 3, 1)],
     'one': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
