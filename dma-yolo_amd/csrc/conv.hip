@@ -3225,7 +3225,10 @@ inline bool wgrad_tap_ok(const Geom& g, const void* x, const void* dy) {
   // enough (patch, tile) work units that the per-block fp32 atomics of the 288-column tile stay a small share
   // (tools/gpu/tune_conv.py: 20^2 / 40^2 / 80^2 yolov5s layers are faster on the v3 / v4 column tiles)
   const long units = (long)g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8) * ceil_div(g.K, 128) * (g.C / 32);
-  return units >= 16384;
+  // 10000: the yolov5s 64-channel @80^2 layers (12800 units) measured 96 -> 79 us on the tap kernel, the 256-channel
+  // @20^2 ones (9216) 70 -> 106 us (profiles/r02/ab_wgrad_v5s.log)
+  static const long min_units = env_int("DMY_WGRAD_TAP_UNITS", 10000);
+  return units >= min_units;
 }
 template <int BM>
 int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
