@@ -77,6 +77,11 @@ def main():
             'wgrad': lambda: call('dmy_conv_wgrad', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s, p, OH, OW,
                                   K, stream()),
         }
+        if 'wgrad_det' in kinds:  # deterministic form: split partials to a workspace, reduced in split order
+            ne = call('dmy_conv_wgrad_ws_elems', 1, ptr(x), ptr(dy), N, H, W, C, C, K, k, k, s, p, OH, OW, K, 0)
+            wsd = torch.empty(max(ne, 1), device='cuda')
+            fns['wgrad_det'] = lambda: call('dmy_conv_wgrad_det', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s,
+                                            p, OH, OW, K, 0, ptr(wsd), ne, stream())
         for kind in kinds:
             us = bench(fns[kind])
             print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s '
