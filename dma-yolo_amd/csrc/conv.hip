@@ -2949,7 +2949,8 @@ __global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict
 // and the buffer loader applies; 0 = not split
 inline int splitk_plan(const Geom& g, const void* x, const void* w, const void* y, int& gm, int& gn, int& per) {
   const long M = (long)g.N * g.OH * g.OW;
-  if (M >= 16384 || M == 0 || g.C % 64 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || g.K < 32 ||
+  static const long maxm = env_int("DMY_SPLITK_MAXM", 16384);
+  if (M >= maxm || M == 0 || g.C % 64 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || g.K < 32 ||
       !aligned16(x) || !aligned16(w) || !aligned16(y) || !conv_buf_mode())
     return 0;
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
@@ -3001,12 +3002,12 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
-    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
-      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
     if (ws != nullptr && ps == nullptr && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res)))) {
       const long need = splitk_elems(g, x, w, y);
       if (need > 0 && need <= ws_elems) return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);
     }
+    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
+      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
   }
   if (big_tile(M, g.K))
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
