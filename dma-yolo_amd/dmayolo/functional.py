@@ -45,6 +45,24 @@ def f32(n, dev):
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
+# Output-into-slice side channel of conv_bn_act (see concat_buffer): the view is consumed by the ConvBNActFn.apply
+# that conv_bn_act issues right after setting it, and only when its shape / dtype / device match the output.
+_OUT = [None]
+
+
+def _take_out(N, K, OH, OW, like):
+    o, _OUT[0] = _OUT[0], None
+    if o is None or tuple(o.shape) != (N, K, OH, OW) or o.dtype != like.dtype or o.device != like.device:
+        return None
+    return o
+
+
+def concat_buffer(N, Ct, H, W, like):
+    """the channels_last buffer of a plain Concat whose producers write their outputs straight into its channel
+    slices (conv_bn_act(out=buf[:, c0:c1])); ConcatFn then recognises the in-place slices and copies nothing"""
+    return new_act(N, Ct, H, W, like)
+
+
 class GradSink:
     """Input-gradient accumulator for an activation with several consumers inside one module.
 
@@ -442,6 +460,7 @@ class ConvBNActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None, grad_on=True):
         link_in = getattr(x, '_dmy_bnlink', None)
         s2d = getattr(x, '_dmy_s2d', 0)
+        out_req, _OUT[0] = _OUT[0], None  # conv_bn_act's out view, checked against the output geometry below
         K, C2, k, _ = weight.shape
         ctx.s2d = 0
         # ctx.needs_input_grad mirrors requires_grad even when the CALLER runs under torch.no_grad() (forward itself
@@ -502,13 +521,16 @@ class ConvBNActFn(torch.autograd.Function):
             res, rps = pixel_stride(res)
         else:
             rps = 0
+        _OUT[0] = out_req
+        out = _take_out(N, K, OH, OW, x) if (bn is not None or spec.act != ACT_NONE or res is not None) else None
+        yps = pixel_stride(out)[1] if out is not None else K
         if infer:
-            y = new_act(N, K, OH, OW, x)
+            y = out if out is not None else new_act(N, K, OH, OW, x)
             scale, shift = eval_coef(spec, dev) if bn is not None else (None, None)
             if scale is None and spec.act == ACT_NONE and res is None:
-                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
+                _launch_conv_fwd(x, xps, wf, bias, y, yps, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             else:
-                _launch_conv_fwd(x, xps, wf, bias, y, K, None, None, K, kg, sg, pg, OH, OW, C, k,
+                _launch_conv_fwd(x, xps, wf, bias, y, yps, None, None, K, kg, sg, pg, OH, OW, C, k,
                                  epi=(scale, shift, spec.act, res, rps), f8=f8)
             return y
         z = new_act(N, K, OH, OW, x)
@@ -535,8 +557,8 @@ class ConvBNActFn(torch.autograd.Function):
                 _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
                 call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
                      float(bn.eps), K, ptr(scale), ptr(shift), stream())
-            y = new_act(N, K, OH, OW, x)
-            call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y), K,
+            y = out if out is not None else new_act(N, K, OH, OW, x)
+            call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y), yps,
                  M, K, stream())
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
             ctx.bnlink = None
@@ -545,9 +567,9 @@ class ConvBNActFn(torch.autograd.Function):
         else:
             _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             if spec.act != ACT_NONE or res is not None:
-                y = new_act(N, K, OH, OW, x)
+                y = out if out is not None else new_act(N, K, OH, OW, x)
                 one, zero = torch.ones(K, device=dev), torch.zeros(K, device=dev)
-                call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(one), ptr(zero), spec.act, ptr(res), rps, ptr(y), K,
+                call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(one), ptr(zero), spec.act, ptr(res), rps, ptr(y), yps,
                      M, K, stream())
             else:
                 y = z
@@ -690,14 +712,20 @@ class ConvBNActFn(torch.autograd.Function):
         return dx, dw, dbias, dgamma, dbeta, dres, None, None, None, None
 
 
-def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None):
-    """xsink / rsink: GradSinks collecting the gradient of x / of the residual (see GradSink)."""
+def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None, out=None):
+    """xsink / rsink: GradSinks collecting the gradient of x / of the residual (see GradSink).  out: an NHWC view
+    (a concat_buffer channel slice) the activation is written into instead of a fresh tensor, when the layer has a
+    separate activation pass (BN and / or act / residual); the returned tensor is then that view."""
     if spec is None:  # a persistent spec per weight PARAMETER (views made per call share their base), so the
         # inference caches (prepped weight, eval BN coefficients) hold across calls for the Detect / Swin / CBAM convs
         spec = _param_spec(weight._base if weight._base is not None else weight, stride, pad, act, bn)
     gamma = bn.weight if bn is not None else None
     beta = bn.bias if bn is not None else None
-    return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec, xsink, rsink, torch.is_grad_enabled())
+    _OUT[0] = out
+    try:
+        return ConvBNActFn.apply(x, weight, bias, gamma, beta, res, spec, xsink, rsink, torch.is_grad_enabled())
+    finally:
+        _OUT[0] = None
 
 
 # ------------------------------------------------------------------ pooling / resize / concat
@@ -771,13 +799,16 @@ class ConcatFn(torch.autograd.Function):
     def forward(ctx, w, eps, sinks, *xs):
         """sinks: None or one GradSink-or-None per input (the slice gradient is handed to it)"""
         ctx.sinks = sinks
+        base = _inplace_concat(xs) if w is None else None
         xs = [pixel_stride(x) for x in xs]
         N, _, H, W = xs[0][0].shape
         Ct = sum(x.shape[1] for x, _ in xs)
-        y = new_act(N, Ct, H, W, xs[0][0])
+        y = base.detach() if base is not None else new_act(N, Ct, H, W, xs[0][0])
         c0 = 0
         M = N * H * W
         for i, (x, xps) in enumerate(xs):
+            if base is not None:  # the producers wrote their slices in place (concat_buffer)
+                break
             C = x.shape[1]
             call('dmy_slice_copy', dcode(x), ptr(x), xps, ctypes_off(y, c0), Ct, M, C, ptr(w), i,
                  len(xs) if w is not None else 0, float(eps), 0, stream())
@@ -823,6 +854,21 @@ class ConcatFn(torch.autograd.Function):
         dw = torch.empty_like(w)
         call('dmy_bifpn_wgrad', ptr(part), nb, len(xs), ptr(w), float(ctx.eps), ptr(dw), stream())
         return (dw, None, None, *grads)
+
+
+def _inplace_concat(xs):
+    """the concat_buffer whose consecutive channel slices the inputs are, in order, or None"""
+    b = xs[0]._base
+    if b is None or b.dim() != 4 or not b.is_contiguous(memory_format=CL):
+        return None
+    N, Ct, H, W = b.shape
+    c0, es = 0, b.element_size()
+    for x in xs:
+        if x._base is not b or x.shape[0] != N or x.shape[2:] != b.shape[2:] or \
+                x.data_ptr() != b.data_ptr() + c0 * es or x.stride() != b.stride():
+            return None
+        c0 += x.shape[1]
+    return b if c0 == Ct else None
 
 
 def ctypes_off(t, c0):

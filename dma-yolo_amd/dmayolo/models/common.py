@@ -48,14 +48,14 @@ def _pad_int(p):
     return p if isinstance(p, int) else p[0]
 
 
-def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None):
+def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None, out=None):
     """conv (nn.Conv2d, groups=1, dilation=1) -> optional BN -> act (+ residual) on the HIP path.
     xsink / rsink: Fn.GradSink for the gradients of x / res when they have other consumers."""
     assert conv.groups == 1 and conv.dilation in (1, (1, 1)), 'grouped/dilated conv not on the DMA-YOLO path'
     s = conv.stride if isinstance(conv.stride, int) else conv.stride[0]
     pad, a = _pad_int(conv.padding), act_code(act)
     return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, pad, a, res=res, spec=Fn.spec_for(conv, s, pad, a, bn),
-                          xsink=xsink, rsink=rsink)
+                          xsink=xsink, rsink=rsink, out=out)
 
 
 class Conv(nn.Module):
@@ -67,11 +67,11 @@ class Conv(nn.Module):
         self.bn = nn.BatchNorm2d(c2)
         self.act = nn.SiLU() if act is True else (act if isinstance(act, nn.Module) else nn.Identity())
 
-    def forward(self, x, res=None, xsink=None, rsink=None):
-        return conv_forward(self.conv, self.bn, self.act, x, res, xsink, rsink)
+    def forward(self, x, res=None, xsink=None, rsink=None, out=None):
+        return conv_forward(self.conv, self.bn, self.act, x, res, xsink, rsink, out)
 
-    def forward_fuse(self, x, res=None, xsink=None, rsink=None):
-        return conv_forward(self.conv, None, self.act, x, res, xsink, rsink)
+    def forward_fuse(self, x, res=None, xsink=None, rsink=None, out=None):
+        return conv_forward(self.conv, None, self.act, x, res, xsink, rsink, out)
 
 
 class Bottleneck(nn.Module):
@@ -84,11 +84,11 @@ class Bottleneck(nn.Module):
         self.cv2 = Conv(c_, c2, 3, 1, g=g)
         self.add = shortcut and c1 == c2
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         if not self.add:
-            return self.cv2(self.cv1(x))
+            return self.cv2(self.cv1(x), out=out)
         sk = Fn.GradSink(2)  # x -> cv1 and the residual
-        return self.cv2(self.cv1(x, xsink=sk), res=x, rsink=sk)
+        return self.cv2(self.cv1(x, xsink=sk), res=x, rsink=sk, out=out)
 
 
 class C3(nn.Module):
@@ -104,7 +104,17 @@ class C3(nn.Module):
 
     def forward(self, x):
         sk = Fn.GradSink(2)  # x -> cv1 and cv2
-        return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(self.cv1(x, xsink=sk)), self.cv2(x, xsink=sk)))
+        a = self.cv1(x, xsink=sk)
+        blocks = list(self.m) if isinstance(self.m, nn.Sequential) else []
+        if not blocks or type(blocks[-1]) is not Bottleneck:
+            return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(a), self.cv2(x, xsink=sk)))
+        # the last Bottleneck and cv2 write their activations straight into the two halves of the concat buffer
+        c_ = a.shape[1]
+        cat = Fn.concat_buffer(a.shape[0], 2 * c_, a.shape[2], a.shape[3], a)
+        for b in blocks[:-1]:
+            a = b(a)
+        a = blocks[-1](a, out=cat[:, :c_])
+        return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, a, self.cv2(x, xsink=sk, out=cat[:, c_:])))
 
 
 class SPPF(nn.Module):
