@@ -8,6 +8,7 @@ forward() runs the gfx950 kernels through dmayolo.functional; there is no CPU pa
 Activation tensors are NHWC (torch.channels_last) in the model's storage dtype.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -91,6 +92,10 @@ class Bottleneck(nn.Module):
         return self.cv2(self.cv1(x, xsink=sk), res=x, rsink=sk, out=out)
 
 
+# in-place C3 concat (C3.forward): 0 off (copy), 1 Bottleneck stacks, 2 also Swin blocks (C3STR); DMY_INPLACE_CAT
+_INPLACE_CAT = int(os.environ.get('DMY_INPLACE_CAT', '2'))
+
+
 class C3(nn.Module):
     """models/common.py:159-182."""
 
@@ -106,14 +111,19 @@ class C3(nn.Module):
         sk = Fn.GradSink(2)  # x -> cv1 and cv2
         a = self.cv1(x, xsink=sk)
         blocks = list(self.m) if isinstance(self.m, nn.Sequential) else []
-        if not blocks or type(blocks[-1]) is not Bottleneck:
+        seq = bool(blocks) and type(blocks[-1]) is Bottleneck and _INPLACE_CAT >= 1
+        if not seq and not (getattr(self.m, 'dmy_out', False) and _INPLACE_CAT >= 2):
             return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(a), self.cv2(x, xsink=sk)))
-        # the last Bottleneck and cv2 write their activations straight into the two halves of the concat buffer
+        # the last Bottleneck (or the Swin block) and cv2 write their activations straight into the two halves of the
+        # concat buffer; a producer that cannot (e.g. an active DropPath) returns its own tensor and ConcatFn copies
         c_ = a.shape[1]
         cat = Fn.concat_buffer(a.shape[0], 2 * c_, a.shape[2], a.shape[3], a)
-        for b in blocks[:-1]:
-            a = b(a)
-        a = blocks[-1](a, out=cat[:, :c_])
+        if seq:
+            for b in blocks[:-1]:
+                a = b(a)
+            a = blocks[-1](a, out=cat[:, :c_])
+        else:
+            a = self.m(a, out=cat[:, :c_])
         return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, a, self.cv2(x, xsink=sk, out=cat[:, c_:])))
 
 

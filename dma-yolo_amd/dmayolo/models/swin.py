@@ -67,9 +67,10 @@ class SwinTransformerLayer(nn.Module):
         self.norm2 = norm_layer(c)
         self.mlp = Mlp(in_features=c, hidden_features=int(c * mlp_ratio), act_layer=act_layer, drop=drop)
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         """common.py:595-637 on NHWC tokens: LN -> qkv -> shifted-window attention (pad/roll/partition
-        folded into the kernel's addressing) -> proj (+ residual) -> LN -> MLP(GELU) (+ residual)."""
+        folded into the kernel's addressing) -> proj (+ residual) -> LN -> MLP(GELU) (+ residual).
+        out: a concat_buffer slice the final residual sum is written into (C3STR; not with an active DropPath)."""
         c = x.shape[1]
         a = self.attn
         s1, s2 = Fn.GradSink(2), Fn.GradSink(2)  # x -> norm1 + residual; x2 -> norm2 + residual
@@ -91,7 +92,7 @@ class SwinTransformerLayer(nn.Module):
             return Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias,
                                                                    None, 1, 0, Fn.ACT_NONE)), s2)
         return Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0, Fn.ACT_NONE, res=x,
-                              rsink=s2)
+                              rsink=s2, out=out)
 
 
 class SwinTransformerBlock(nn.Module):
@@ -105,9 +106,14 @@ class SwinTransformerBlock(nn.Module):
                                                        shift_size=0 if (i % 2 == 0) else self.shift_size)
                                   for i in range(num_layers)))
 
-    def forward(self, x):
+    dmy_out = True  # forward(x, out=view) writes its result into a concat_buffer slice when it can (C3.forward)
+
+    def forward(self, x, out=None):
         if self.conv is not None:
             x = self.conv(x)
-        return self.tr(x)
+        layers = list(self.tr)
+        for layer in layers[:-1]:
+            x = layer(x)
+        return layers[-1](x, out=out) if layers else x
 
 
