@@ -2849,7 +2849,7 @@ inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, flo
 
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-              hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}) {
+              hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}, int tov = -1) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   if (!ep.on && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
@@ -2878,7 +2878,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
   }
-  if (p1 && buf && p1_persist_mode()) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
+  if (p1 && buf && p1_persist_mode() && tov < 0) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
     const int NC = num_cus();
     if (gv.K > 64) {
       const int gm = ceil_div(M, 128), gn = ceil_div(gv.K, 128);
@@ -2900,14 +2900,14 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
                                                                                xbytes, wbytes, ep, bb);           \
     return (int)hipGetLastError();                                                                                 \
   }
-  if (buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
+  if (tov < 0 && buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
       (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus())
     W_GO(256, 256)
-  if (buf && tall_mode() && !p1 && gv.K > 64 && gv.K <= 128 &&
+  if (tov < 0 && buf && tall_mode() && !p1 && gv.K > 64 && gv.K <= 128 &&
       (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
     W_GO(512, 128)
 #undef W_GO
-  const int pt = p1 ? p1_tile_mode() : 0;
+  const int pt = tov >= 0 ? tov : p1 ? p1_tile_mode() : 0;
   if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
   else if (gv.K > 64 && pt == 2) V3_LAUNCH(128, 128, 3)
   else if (gv.K > 64 && pt == 3) V3_LAUNCH(256, 64, 2)
@@ -2997,6 +2997,25 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   return (int)hipGetLastError();
 }
 
+// small-grid tile of a forward without BN partials (eval / batch-1 inference): when the 256 x 128 tile grid leaves
+// CUs idle, run the LDS-DMA kernel on 128 x 128 (p1_tile_mode 2) or 128 x 64 (mode 4) tiles, also for M < 16384
+// (otherwise the v2 tiles).  DMY_V3_FILL = 1 on, 0 (default) off: measured SLOWER on the bs1 detect path (DMA-1536
+// conv time 5.54 -> 5.87 ms per forward, yolov5s p50 0.94 -> 1.11 ms; profiles/r02/ab_fill.log) -- twice the blocks
+// do not shorten a latency-bound 1-4 K-step tile.  Returns the tile mode or -1
+inline int fill_tile(const Geom& g, const void* x, const void* w, const void* y, const float* ps, const Epi& ep) {
+  static const int on = env_int("DMY_V3_FILL", 0);
+  const long M = (long)g.N * g.OH * g.OW;
+  if (!on || ps != nullptr || g.K <= 64 || M < 1024 || g.C % 64 != 0 || !conv_buf_mode()) return -1;
+  if (g.C % 8 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) ||
+      !aligned16(y) || (ep.res && (ep.rps % 8 != 0 || !aligned16(ep.res))))
+    return -1;
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
+  if (xb >= (double)v3::kBufOob || wb >= (double)v3::kBufOob) return -1;
+  const long NC = num_cus();
+  if (ceil_div(M, 256) * ceil_div(g.K, 128) >= NC) return -1;
+  return ceil_div(M, 128) * ceil_div(g.K, 128) >= NC ? 2 : 4;
+}
+
 template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
@@ -3006,6 +3025,8 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
       const long need = splitk_elems(g, x, w, y);
       if (need > 0 && need <= ws_elems) return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);
     }
+    const int tov = fill_tile(g, x, w, y, ps, ep);
+    if (tov >= 0) return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep, v3::BnB{}, tov);
     if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
       return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
   }

@@ -154,3 +154,42 @@ def test_conv_fwd_1x1_small_m_unsplit():
     y = torch.empty_like(x)
     assert call('dmy_conv_fwd_splitk_elems', 1, ptr(x), ptr(w), ptr(y), 1, 96, 96, 256, 256, 256, 1, 1, 1, 0, 96, 96,
                 256) == 0
+
+
+# eval forwards (dmy_conv_fwd_act) whose 256-row tile grid leaves CUs idle -- the v2 tiles, or the LDS-DMA kernel on
+# 128 x 128 / 128 x 64 tiles under DMY_V3_FILL=1 (fill_tile) -- ragged M / columns, a residual, a concat-slice output
+FILL_SHAPES = [(1, 256, 96, 96, 256, 1, 1), (1, 128, 192, 192, 128, 1, 1), (1, 128, 190, 186, 128, 3, 1),
+               (1, 512, 48, 48, 512, 1, 1), (1, 1024, 37, 41, 200, 1, 1), (2, 64, 45, 47, 136, 1, 1),
+               (1, 256, 96, 96, 1024, 1, 1), (3, 128, 65, 67, 512, 3, 2)]
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s', FILL_SHAPES)
+@pytest.mark.parametrize('res', [False, True])
+def test_conv_fwd_fill_tiles_vs_torch(N, C, H, W, K, k, s, res):
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    from dmayolo._lib import ACT_SILU
+    g = torch.Generator().manual_seed(N * 13 + C + K + k + int(res))
+    p = k // 2
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5
+    ref = F.conv2d(x.float().cuda(), w.bfloat16().float().cuda(), stride=s, padding=p)
+    OH, OW = ref.shape[2:]
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    wf, _ = prep_weight(w.cuda(), torch.bfloat16, False)
+    Kt = K + 64  # output written into the first K channels of a wider (concat) buffer
+    yb = torch.full((N, Kt, OH, OW), 7.0, dtype=torch.bfloat16, device='cuda').contiguous(
+        memory_format=torch.channels_last)
+    y = yb[:, :K]
+    sc = (torch.rand(K, generator=g) + 0.5).cuda()
+    sh = (torch.randn(K, generator=g) * 0.2).cuda()
+    r = torch.randn(N, K, OH, OW, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last) \
+        if res else None
+    rc = call('dmy_conv_fwd_act', 1, ptr(xd), ptr(wf), None, ptr(y), N, H, W, C, C, K, k, k, s, p, OH, OW, Kt, ptr(sc),
+              ptr(sh), ACT_SILU, ptr(r), K if res else 0, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    z = F.silu(ref.bfloat16().float() * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1))
+    if res:
+        z = z + r.float()
+    assert _rel(y.float(), z) < 1e-2
+    assert torch.equal(yb[:, K:].float().cpu(), torch.full((N, 64, OH, OW), 7.0)), 'columns past K must stay untouched'

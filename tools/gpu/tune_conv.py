@@ -33,6 +33,12 @@ SETS = {
             (32, 64, 384, 384, 128, 1, 1), (32, 128, 192, 192, 384, 1, 1), (32, 256, 192, 192, 128, 1, 1),
             (32, 128, 192, 192, 256, 1, 1), (64, 64, 160, 160, 64, 1, 1), (64, 128, 80, 80, 128, 1, 1)],
     'stem': [(32, 16, 768, 768, 64, 3, 1), (64, 16, 320, 320, 32, 3, 1), (8, 16, 960, 960, 64, 3, 1)],
+    # batch-1 1536 inference layers (dmy_conv_fwd_act path, 'infer' kind)
+    'det': [(1, 256, 96, 96, 256, 1, 1), (1, 128, 192, 192, 128, 1, 1), (1, 128, 192, 192, 512, 1, 1),
+            (1, 1024, 96, 96, 256, 1, 1), (1, 512, 192, 192, 128, 1, 1), (1, 256, 192, 192, 256, 1, 1),
+            (1, 256, 96, 96, 1024, 1, 1), (1, 512, 96, 96, 512, 1, 1), (1, 1024, 48, 48, 1024, 1, 1),
+            (1, 512, 48, 48, 512, 1, 1), (1, 128, 192, 192, 128, 3, 1), (1, 256, 96, 96, 256, 3, 1),
+            (1, 64, 384, 384, 64, 3, 1), (1, 512, 48, 48, 512, 3, 1), (1, 128, 384, 384, 128, 1, 1)],
     'one': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
@@ -77,6 +83,12 @@ def main():
             'wgrad': lambda: call('dmy_conv_wgrad', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s, p, OH, OW,
                                   K, stream()),
         }
+        if 'infer' in kinds:  # eval forward: BN scale / shift + SiLU epilogue, split-K workspace when the plan splits
+            ne = call('dmy_conv_fwd_splitk_elems', 1, ptr(x), ptr(wf), ptr(y), N, H, W, C, C, K, k, k, s, p, OH, OW, K)
+            wsi = torch.empty(max(ne, 1), device='cuda')
+            sc, sh = torch.rand(K, device='cuda') + 0.5, torch.randn(K, device='cuda') * 0.1
+            fns['infer'] = lambda: call('dmy_conv_fwd_act_ws', 1, ptr(x), ptr(wf), None, ptr(y), N, H, W, C, C, K, k, k,
+                                        s, p, OH, OW, K, ptr(sc), ptr(sh), 1, None, 0, ptr(wsi), ne, stream())
         if 'wgrad_det' in kinds:  # deterministic form: split partials to a workspace, reduced in split order
             ne = call('dmy_conv_wgrad_ws_elems', 1, ptr(x), ptr(dy), N, H, W, C, C, K, k, k, s, p, OH, OW, K, 0)
             wsd = torch.empty(max(ne, 1), device='cuda')
