@@ -79,6 +79,11 @@ class GradSink:
     def __init__(self, n):
         self.n, self.seen, self.buf, self.ps = n, 0, None, 0
 
+    def expect(self, k):
+        """register k more contributions (a consumer module taking this sink from its caller, in forward)"""
+        self.n += k
+        return self
+
     def _tick(self):
         self.seen += 1
         if self.seen < self.n:

@@ -190,10 +190,11 @@ class SCConv(nn.Module):
                                           bias=False),
                                 nn.BatchNorm2d(c2))
 
-    def forward(self, x):
+    def forward(self, x, xsink=None):
+        """xsink: the caller's GradSink for x (Model fan-out); this module's three contributions join it"""
         r = self.k2[0].kernel_size
         r = r if isinstance(r, int) else r[0]
-        sk = Fn.GradSink(3)  # x -> avg-pool (k2), k3, the gate
+        sk = Fn.GradSink(3) if xsink is None else xsink.expect(3)  # x -> avg-pool (k2), k3, the gate
         g = conv_forward(self.k2[1], self.k2[2], None, Fn.AvgPoolFn.apply(x, r, sk))
         u3 = conv_forward(self.k3[0], self.k3[1], None, x, xsink=sk)
         return conv_forward(self.k4[0], self.k4[1], None, Fn.SCGateFn.apply(x, u3, g, sk))
@@ -262,6 +263,13 @@ class Concat(nn.Module):
         return Fn.ConcatFn.apply(None, 0.0, None, *x)
 
 
+def _join(sinks):
+    """register one contribution with each given sink; None when there are none"""
+    if sinks is None or all(sk is None for sk in sinks):
+        return None
+    return tuple(sk.expect(1) if sk is not None else None for sk in sinks)
+
+
 class AdConcat2(nn.Module):
     """BiFPN weighted concat, models/common.py:994-1008."""
 
@@ -271,9 +279,10 @@ class AdConcat2(nn.Module):
         self.w = nn.Parameter(torch.ones(2, dtype=torch.float32), requires_grad=True)
         self.epsilon = 0.0001
 
-    def forward(self, x):
+    def forward(self, x, sinks=None):
+        """sinks: None or one GradSink-or-None per input (Model fan-out); each joins with one contribution"""
         assert self.d == 1 and len(x) == 2
-        return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
+        return Fn.ConcatFn.apply(self.w, self.epsilon, _join(sinks), *x)
 
 
 class AdConcat3(AdConcat2):
@@ -283,9 +292,9 @@ class AdConcat3(AdConcat2):
         super().__init__(dimension)
         self.w = nn.Parameter(torch.ones(3, dtype=torch.float32), requires_grad=True)
 
-    def forward(self, x):
+    def forward(self, x, sinks=None):
         assert self.d == 1 and len(x) == 3
-        return Fn.ConcatFn.apply(self.w, self.epsilon, None, *x)
+        return Fn.ConcatFn.apply(self.w, self.epsilon, _join(sinks), *x)
 
 
 class SPP(nn.Module):

@@ -7,6 +7,7 @@ Differences from the reference that do not change results:
   * activations are NHWC in `Model.act_dtype` (float32 parity / bfloat16 throughput).
 """
 import math
+import os
 import weakref
 from copy import deepcopy
 from pathlib import Path
@@ -22,6 +23,8 @@ from .common import Conv, Upsample, SCConv, autopad, space_to_depth
 from .tdetect import TDetect
 from ..utils.general import make_divisible
 from ..utils.torch_utils import initialize_weights, fuse_conv_and_bn
+
+_MODEL_SINKS = os.environ.get('DMY_MODEL_SINKS', '0') != '0'  # Model-level gradient fan-out sinks
 
 
 class Detect(nn.Module):
@@ -41,10 +44,12 @@ class Detect(nn.Module):
         self.m = nn.ModuleList(nn.Conv2d(x, self.no * self.na, 1) for x in ch)
         self.inplace = inplace
 
-    def forward(self, x):
+    def forward(self, x, sinks=None):
+        """sinks: None or one GradSink-or-None per level input (Model fan-out), one contribution each"""
         out = []
         for i in range(self.nl):
-            y = Fn.conv_bn_act(x[i], self.m[i].weight, self.m[i].bias, None, 1, 0, Fn.ACT_NONE)
+            sk = sinks[i].expect(1) if sinks is not None and sinks[i] is not None else None
+            y = Fn.conv_bn_act(x[i], self.m[i].weight, self.m[i].bias, None, 1, 0, Fn.ACT_NONE, xsink=sk)
             bs, _, ny, nx = y.shape
             # NHWC [bs, ny, nx, na*no] -> [bs, na, ny, nx, no] view (no copy)
             out.append(y.permute(0, 2, 3, 1).view(bs, ny, nx, self.na, self.no).permute(0, 3, 1, 2, 4))
@@ -219,15 +224,50 @@ class Model(nn.Module):
         if arena:
             Fn.WgradArena.current = self._wgrad_arena()
             Fn.WeightPrep.current = self._weight_prep(x.device).launch()
+        fan = self._fanout() if _MODEL_SINKS and torch.is_grad_enabled() and self.training else {}
+        sinks = {}
         try:
             for m in self.model:
                 if m.f != -1:
                     x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
-                x = m(x)
+                kw = self._sink_kw(m, sinks) if sinks else None
+                x = m(x, **kw) if kw else m(x)
                 y.append(x if m.i in self.save else None)
+                if m.i in fan:
+                    sinks[m.i] = Fn.GradSink(0)
         finally:
             Fn.WgradArena.current, Fn.WeightPrep.current = prev
         return x
+
+    # gradient fan-out: a layer output read by several layers (the BiFPN skips, the P3-P5 outputs read by a Conv and
+    # Detect) gets one GradSink that the sink-aware consumers' backward kernels write / accumulate into, so autograd
+    # does not sum their contributions with separate add kernels (DMY_MODEL_SINKS, module-level _MODEL_SINKS)
+    _SINK_TYPES = ('Conv', 'SCConv', 'AdConcat2', 'AdConcat3', 'Detect')
+
+    def _fanout(self):
+        """{layer index: consumer count} for outputs read by >= 2 layers, >= 1 of them sink-aware (cached)"""
+        if getattr(self, '_fan', None) is None:
+            cons = {}
+            for m in self.model:
+                for j in ([m.f] if isinstance(m.f, int) else m.f):
+                    cons.setdefault(m.i - 1 if j == -1 else j, []).append(type(m).__name__)
+            self._fan = {i: len(c) for i, c in cons.items() if len(c) >= 2 and any(t in self._SINK_TYPES for t in c)}
+        return self._fan
+
+    def _sink_kw(self, m, sinks):
+        """keyword arguments handing layer m its inputs' fan-out sinks, or None"""
+        name = type(m).__name__
+        if name not in self._SINK_TYPES:
+            return None
+        src = [m.i - 1 if j == -1 else j for j in ([m.f] if isinstance(m.f, int) else m.f)]
+        sk = [sinks.get(j) for j in src]
+        if all(s is None for s in sk):
+            return None
+        if name == 'Conv':
+            return {'xsink': sk[0].expect(1)}
+        if name == 'SCConv':
+            return {'xsink': sk[0]}
+        return {'sinks': sk}
 
     def _initialize_biases(self, cf=None):
         """models/yolo.py:293-301."""

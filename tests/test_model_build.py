@@ -89,3 +89,35 @@ def test_config5_in_proj_never_optimized():
     missing = [(k, p.numel()) for k, p in m.named_parameters() if id(p) not in grouped]
     assert len(missing) == 12 and all('in_proj' in k for k, _ in missing), missing
     assert sum(n for _, n in missing) == 4727808
+
+
+@pytest.mark.parametrize('cfg,plan', [('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', {4: 2, 6: 3, 10: 2, 14: 2, 18: 2, 21: 2}),
+                                      ('yolov5s.yaml', {4: 2, 6: 2, 17: 2, 20: 2})])
+def test_gradient_fanout_plan(cfg, plan):
+    """Model-level GradSinks: the layer outputs read by >= 2 layers of which >= 1 takes a sink (BiFPN skips, the
+    P3-P5 outputs read by a Conv and Detect); outputs read only by Upsample / plain Concat stay with autograd"""
+    from dmayolo.models.yolo import Model
+    import dmayolo.functional as Fn
+    m = Model(os.path.join(YAMLS, cfg), nc=10)
+    assert m._fanout() == plan
+    # consumers register their contributions in forward: SCConv 3, a Conv / Detect level / AdConcat slot 1 each
+    sinks = {i: Fn.GradSink(0) for i in plan}
+    for layer in m.model:
+        m._sink_kw(layer, sinks)
+        name = type(layer).__name__
+        if name == 'SCConv':  # SCConv.forward joins its own three
+            src = layer.f if layer.f != -1 else layer.i - 1
+            if src in sinks:
+                sinks[src].expect(3)
+        elif name in ('AdConcat2', 'AdConcat3', 'Detect'):
+            for j in layer.f:
+                j = layer.i - 1 if j == -1 else j
+                if j in sinks:
+                    sinks[j].expect(1)
+    aware = {i: sum(1 for layer in m.model for j in ([layer.f] if isinstance(layer.f, int) else layer.f)
+                    if (layer.i - 1 if j == -1 else j) == i and type(layer).__name__ in m._SINK_TYPES)
+             for i in plan}
+    for i, sk in sinks.items():
+        n_scconv = sum(2 for layer in m.model if type(layer).__name__ == 'SCConv' and
+                       (layer.f if layer.f != -1 else layer.i - 1) == i)
+        assert sk.n == aware[i] + n_scconv, (i, sk.n)
