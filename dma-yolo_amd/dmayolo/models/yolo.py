@@ -241,8 +241,13 @@ class Model(nn.Module):
 
     # gradient fan-out: a layer output read by several layers (the BiFPN skips, the P3-P5 outputs read by a Conv and
     # Detect) gets one GradSink that the sink-aware consumers' backward kernels write / accumulate into, so autograd
-    # does not sum their contributions with separate add kernels (DMY_MODEL_SINKS, module-level _MODEL_SINKS)
-    _SINK_TYPES = ('Conv', 'SCConv', 'AdConcat2', 'AdConcat3', 'Detect')
+    # does not sum their contributions with separate add kernels (DMY_MODEL_SINKS, module-level _MODEL_SINKS).
+    # Off by default: same-box A/Bs (profiles/r02/ab_model_sinks.log) put it within the ±0.5 % run-to-run noise --
+    # DMA-1536 +0.35 % with Detect included, -0.3 %..+0.05 % without; yolov5s -0.3 % with Detect (its only
+    # multi-consumer outputs are read by a Conv and Detect, whose narrow-K data-grad then accumulates), so Detect
+    # joins only under DMY_SINK_DETECT=1.  GPU model / module tests pass with it on.
+    _SINK_TYPES = ('Conv', 'SCConv', 'AdConcat2', 'AdConcat3') + (('Detect',) if os.environ.get('DMY_SINK_DETECT') == '1'
+                                                                  else ())
 
     def _fanout(self):
         """{layer index: consumer count} for outputs read by >= 2 layers, >= 1 of them sink-aware (cached)"""

@@ -95,7 +95,8 @@ def test_config5_in_proj_never_optimized():
                                       ('yolov5s.yaml', {4: 2, 6: 2, 17: 2, 20: 2})])
 def test_gradient_fanout_plan(cfg, plan):
     """Model-level GradSinks: the layer outputs read by >= 2 layers of which >= 1 takes a sink (BiFPN skips, the
-    P3-P5 outputs read by a Conv and Detect); outputs read only by Upsample / plain Concat stay with autograd"""
+    P3-P5 outputs read by a Conv and Detect); outputs read only by Upsample / plain Concat stay with autograd, and
+    Detect joins only under DMY_SINK_DETECT=1"""
     from dmayolo.models.yolo import Model
     import dmayolo.functional as Fn
     m = Model(os.path.join(YAMLS, cfg), nc=10)
@@ -109,7 +110,7 @@ def test_gradient_fanout_plan(cfg, plan):
             src = layer.f if layer.f != -1 else layer.i - 1
             if src in sinks:
                 sinks[src].expect(3)
-        elif name in ('AdConcat2', 'AdConcat3', 'Detect'):
+        elif name in ('AdConcat2', 'AdConcat3') or (name == 'Detect' and name in m._SINK_TYPES):
             for j in layer.f:
                 j = layer.i - 1 if j == -1 else j
                 if j in sinks:
