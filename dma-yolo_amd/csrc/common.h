@@ -10,6 +10,10 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+// The C ABI declarations: every DMY_API definition below must match its declaration here, so a signature that
+// drifts from include/dmayolo.h (and from the ctypes table checked against it, tests/test_abi.py) fails to compile.
+#include "../../include/dmayolo.h"
+
 typedef __hip_bfloat16 bf16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));

@@ -252,16 +252,33 @@ __global__ void loss_combine_kernel(LossCfg cfg, const int* __restrict__ tb, con
     for (int k = head[cell]; k >= 0; k = nxt[k]) mn = min(mn, k);
     if (mn != j) continue;
     float* g = G + b * cfg.sb + gj * cfg.sh + gi * cfg.sw + (long)a * cfg.sa;
+    // the cell's targets in ascending index order, collected once (insertion sort of the short list) and then summed
+    // channel by channel in that order; a cell with more than LMAX targets walks the list per channel instead
+    constexpr int LMAX = 32;
+    int ord[LMAX];
+    int L = 0;
+    for (int k = head[cell]; k >= 0; k = nxt[k]) {
+      if (L < LMAX) {
+        int q = L;
+        while (q > 0 && ord[q - 1] > k) { ord[q] = ord[q - 1]; --q; }
+        ord[q] = k;
+      }
+      ++L;
+    }
     for (int c = 0; c < ng; ++c) {
       float acc = 0.f;
-      int last = -1;
-      while (true) {  // next target of the cell in ascending index order
-        int nj = 0x7fffffff;
-        for (int k = head[cell]; k >= 0; k = nxt[k])
-          if (k > last && k < nj) nj = k;
-        if (nj == 0x7fffffff) break;
-        acc += tgrad[(long)nj * ng + c];
-        last = nj;
+      if (L <= LMAX) {
+        for (int q = 0; q < L; ++q) acc += tgrad[(long)ord[q] * ng + c];
+      } else {
+        int last = -1;
+        while (true) {  // next target of the cell in ascending index order
+          int nj = 0x7fffffff;
+          for (int k = head[cell]; k >= 0; k = nxt[k])
+            if (k > last && k < nj) nj = k;
+          if (nj == 0x7fffffff) break;
+          acc += tgrad[(long)nj * ng + c];
+          last = nj;
+        }
       }
       g[c < 4 ? c : c + 1] = acc;  // channels 0-3 box, 5.. cls (4 is objectness, written by loss_obj_kernel)
     }

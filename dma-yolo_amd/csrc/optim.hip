@@ -46,9 +46,18 @@ __global__ void sgd_kernel(TList L, float lr, float mom, float wd, int nesterov,
   }
 }
 
+// dstep (nullable): the group's step count on the device, the count BEFORE this step.  When given, the bias
+// corrections come from it (bc1 = 1 - b1^t, bc2s = sqrt(1 - b2^t), t = *dstep + 1, in double as torch.optim.Adam
+// computes them on the host) and adam_step_kernel advances it afterwards only if the step was not skipped: a step
+// the GradScaler skips does not advance Adam's t, as torch, where scaler.step() never calls optimizer.step().
 __global__ void adam_kernel(TList L, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2s,
-                            const float* scale, const float* found) {
+                            const float* scale, const float* found, const int* dstep) {
   if (amp_skip(found)) return;
+  if (dstep != nullptr) {
+    const double t = (double)(*dstep + 1);
+    bc1 = (float)(1.0 - pow((double)b1, t));
+    bc2s = (float)sqrt(1.0 - pow((double)b2, t));
+  }
   const float inv = amp_inv(scale);
   const int t = L.tid[blockIdx.x];
   const long o = L.off[blockIdx.x];
@@ -68,6 +77,10 @@ __global__ void adam_kernel(TList L, float lr, float b1, float b2, float eps, fl
     const float denom = sqrtf(vv) / bc2s + eps;
     p[i] -= step * (mv / denom);
   }
+}
+
+__global__ void adam_step_kernel(int* dstep, const float* found) {
+  if (threadIdx.x == 0 && !amp_skip(found)) *dstep += 1;
 }
 
 __global__ void ema_kernel(TList L, float d) {
@@ -143,10 +156,11 @@ DMY_API int dmy_sgd(float* const* p, const float* const* g, float* const* m, con
 
 DMY_API int dmy_adam(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n,
                      const int* tid, const long* off, int nchunks, float lr, float b1, float b2, float eps, float wd,
-                     float bc1, float bc2s, const float* scale, const float* found, void* stream) {
+                     float bc1, float bc2s, const float* scale, const float* found, int* dstep, void* stream) {
   if (nchunks == 0) return 0;
   TList L{p, g, m, v, n, tid, off};
-  adam_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, b1, b2, eps, wd, bc1, bc2s, scale, found);
+  adam_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(L, lr, b1, b2, eps, wd, bc1, bc2s, scale, found, dstep);
+  if (dstep != nullptr) adam_step_kernel<<<1, 64, 0, (hipStream_t)stream>>>(dstep, found);
   return (int)hipGetLastError();
 }
 

@@ -65,20 +65,23 @@ __global__ void ln_fwd_kernel(const T* __restrict__ x, long xps, const float* __
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partials of dw, db
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partials of dw, db.
+// Deterministic: each wave accumulates its rows into its own LDS row pair [wave][2][C], where lane l owns channels
+// l, l + 64, ... (no two lanes touch one slot), and the block partial is the sum over waves in wave order.
 template <typename T>
 __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ dy, long dps,
                               const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
                               T* __restrict__ dx, long dxps, int accumulate, long M, int C, int rows_per_block,
                               float* __restrict__ pdw, float* __restrict__ pdb) {
-  extern __shared__ float sh[];  // [2][C]
-  float* sdw = sh;
-  float* sdb = sh + C;
-  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) sh[c] = 0.f;
+  extern __shared__ float sh[];  // [waves][2][C]
+  const int nwv = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  for (int c = threadIdx.x; c < 2 * C * nwv; c += blockDim.x) sh[c] = 0.f;
   __syncthreads();
+  float* sdw = sh + (long)wv * 2 * C;
+  float* sdb = sdw + C;
   const int lane = threadIdx.x & 63;
   const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
-  for (long m = r0 + (threadIdx.x >> 6); m < r1; m += (blockDim.x >> 6)) {
+  for (long m = r0 + wv; m < r1; m += nwv) {
     const float mu = mean[m], rs = rstd[m];
     float a1 = 0.f, a2 = 0.f;
     for (int c = lane; c < C; c += 64) {
@@ -87,8 +90,8 @@ __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __rest
       const float g = gy * w[c];
       a1 += g;
       a2 += g * xh;
-      atomicAdd(&sdw[c], gy * xh);
-      atomicAdd(&sdb[c], gy);
+      sdw[c] += gy * xh;
+      sdb[c] += gy;
     }
     a1 = wave_sum(a1) / C;
     a2 = wave_sum(a2) / C;
@@ -101,8 +104,13 @@ __global__ void ln_bwd_kernel(const T* __restrict__ x, long xps, const T* __rest
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    pdw[(long)blockIdx.x * C + c] = sdw[c];
-    pdb[(long)blockIdx.x * C + c] = sdb[c];
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < nwv; ++k) {
+      a += sh[(long)k * 2 * C + c];
+      b += sh[(long)k * 2 * C + C + c];
+    }
+    pdw[(long)blockIdx.x * C + c] = a;
+    pdb[(long)blockIdx.x * C + c] = b;
   }
 }
 
@@ -168,8 +176,7 @@ __global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long 
                                                   int accumulate, long M, int C, float* __restrict__ pdw,
                                                   float* __restrict__ pdb) {
   constexpr int VW = Traits<T>::VW, RPW = 64 / L;
-  extern __shared__ float sh[];  // [2][C]
-  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) sh[c] = 0.f;
+  extern __shared__ float sh[];  // [waves][2][C]
   const int lane = threadIdx.x & 63, sub = lane % L, rw = lane / L;
   const int c0 = sub * VW;
   const bool on = c0 < C;
@@ -220,18 +227,32 @@ __global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long 
       *reinterpret_cast<uint4*>(dx + m * dxps + c0) = pack<T>(o_);
     }
   }
-  __syncthreads();
-  if (on) {
+  // deterministic block partial: the RPW row slots of a wave that share channels are folded by a fixed xor tree, the
+  // wave's row goes to LDS [wave][2][C], and the waves are summed in order (no LDS atomics)
+#pragma unroll
+  for (int o = L; o < 64; o <<= 1)
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
-      atomicAdd(&sh[c0 + j], aw[j]);
-      atomicAdd(&sh[C + c0 + j], ab[j]);
+      aw[j] += __shfl_xor(aw[j], o, 64);
+      ab[j] += __shfl_xor(ab[j], o, 64);
+    }
+  const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (on && rw == 0) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      sh[(long)wid * 2 * C + c0 + j] = aw[j];
+      sh[(long)wid * 2 * C + C + c0 + j] = ab[j];
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    pdw[(long)blockIdx.x * C + c] = sh[c];
-    pdb[(long)blockIdx.x * C + c] = sh[C + c];
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < nwv; ++k) {
+      a += sh[(long)k * 2 * C + c];
+      b += sh[(long)k * 2 * C + C + c];
+    }
+    pdw[(long)blockIdx.x * C + c] = a;
+    pdb[(long)blockIdx.x * C + c] = b;
   }
 }
 
@@ -307,6 +328,16 @@ DEV void scores_softmax(const SwinGeom& g, int wr, int wc, int head, const float
   for (int jj = 0; jj < 16; ++jj) P[i * PS + j0 + jj] = s[jj] * inv;
 }
 
+// bias-table bin e = (dr + 7) * 15 + (dc + 7) of a [64][ld] dS matrix (row = query, col = key): the sum over every
+// (q, k) with ri - rj = dr, ci - cj = dc, in ascending q (fixed order: deterministic)
+DEV float bin_dtab(const float* S, int ld, int e) {
+  const int dr = e / (2 * WS - 1) - (WS - 1), dc = e % (2 * WS - 1) - (WS - 1);
+  float a = 0.f;
+  for (int ri = max(0, dr); ri < min(WS, WS + dr); ++ri)
+    for (int ci = max(0, dc); ci < min(WS, WS + dc); ++ci) a += S[(ri * WS + ci) * ld + (ri - dr) * WS + (ci - dc)];
+  return a;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) winattn_fwd_kernel(const T* __restrict__ qkv, const float* __restrict__ table,
                                                           T* __restrict__ out, SwinGeom g) {
@@ -343,9 +374,10 @@ __global__ void __launch_bounds__(256) winattn_bwd_kernel(const T* __restrict__ 
                                                           SwinGeom g) {
   __shared__ float Q[NTOK * QS], K[NTOK * QS], V[NTOK * QS], P[NTOK * PS], D[NTOK * QS];
   __shared__ long pix[NTOK];
-  __shared__ float dtab[(2 * WS - 1) * (2 * WS - 1)];
   const int ntab = (2 * WS - 1) * (2 * WS - 1);
-  for (int e = threadIdx.x; e < ntab; e += blockDim.x) dtab[e] = 0.f;
+  float dsacc[16];
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) dsacc[jj] = 0.f;
   const int nwr = g.Rp / WS, nwc = g.Cp / WS;
   const int head = blockIdx.y;
   for (int wid = blockIdx.x * wpb; wid < min(nwin_total, (blockIdx.x + 1) * wpb); ++wid) {
@@ -396,8 +428,7 @@ __global__ void __launch_bounds__(256) winattn_bwd_kernel(const T* __restrict__ 
         const int j = j0 + jj;
         const float ds = P[i * PS + j] * (dp[jj] - rs);
         P[i * PS + j] = ds;  // P now holds dS
-        const int idx = ((i >> 3) - (j >> 3) + WS - 1) * (2 * WS - 1) + ((i & 7) - (j & 7) + WS - 1);
-        atomicAdd(&dtab[idx], ds);
+        dsacc[jj] += ds;     // this thread's (i, j) positions, summed over the block's windows in window order
       }
     }
     __syncthreads();
@@ -424,9 +455,17 @@ __global__ void __launch_bounds__(256) winattn_bwd_kernel(const T* __restrict__ 
       }
     }
   }
+  // bias-table bins, deterministic: the summed dS matrix goes to LDS (P), then bin (dr, dc) adds its (q, k) positions
+  // in ascending q order
+  __syncthreads();
+  {
+    const int i = threadIdx.x >> 2, j0 = (threadIdx.x & 3) * 16;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) P[i * PS + j0 + jj] = dsacc[jj];
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < ntab; e += blockDim.x)
-    dtab_part[((long)blockIdx.x * g.nh + head) * ntab + e] = dtab[e];
+    dtab_part[((long)blockIdx.x * g.nh + head) * ntab + e] = bin_dtab(P, PS, e);
 }
 
 // table grad [225][nh] = sum over window groups
@@ -663,14 +702,12 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
                                                                float* __restrict__ dtab_part, int nwin, int wpb,
                                                                SwinGeom g) {
   __shared__ __attribute__((aligned(16))) bf16 sm[NW * (3 * MATQ + MATP)];
-  __shared__ float tab[NTAB], dtab[NTAB];
+  __shared__ float tab[NTAB];
+  static_assert((3 * MATQ + MATP) * 2 >= NTOK * NTOK * 4, "a wave's buffers hold its fp32 [64][64] dS sum");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int head = xhead(g.nh), grp = xgroup(g.nh);
   const int il = lane & 15, gq = lane >> 4;
-  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) {
-    tab[e] = table[e * g.nh + head];
-    dtab[e] = 0.f;
-  }
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) tab[e] = table[e * g.nh + head];
   const int nwr = g.Rp / WS, nwc = g.Cp / WS;
   bf16* Qs = sm + w * (3 * MATQ + MATP);
   bf16* Ks = Qs + MATQ;
@@ -791,19 +828,22 @@ __global__ void __launch_bounds__(64 * NW) winattn_bwd_mfma(const bf16* __restri
       store_direct(dqkv + offq, 3L * g.C, A, g.scale, px, lane);
     }
   }
+  // bias-table gradient, deterministic: each wave stores its dS sums as fp32 [q][k] over its own (now dead) buffers,
+  // then bin e sums its (q, k) positions per wave and the waves in order
+  __syncthreads();
+  float* S = reinterpret_cast<float*>(Qs);
 #pragma unroll
-  for (int bq = 0; bq < 4; ++bq) {
-    const int q = 16 * bq + il, ri = q >> 3, ci = q & 7;
+  for (int bq = 0; bq < 4; ++bq)
 #pragma unroll
     for (int bk = 0; bk < 4; ++bk)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = 16 * bk + 4 * gq + r, rj = k >> 3, cj = k & 7;
-        atomicAdd(&dtab[(ri - rj + WS - 1) * (2 * WS - 1) + (ci - cj + WS - 1)], dsacc[bq][bk][r]);
-      }
-  }
+      for (int r = 0; r < 4; ++r) S[(16 * bq + il) * NTOK + 16 * bk + 4 * gq + r] = dsacc[bq][bk][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) dtab_part[((long)grp * g.nh + head) * NTAB + e] = dtab[e];
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) {
+    float a = 0.f;
+    for (int k = 0; k < NW; ++k) a += bin_dtab(reinterpret_cast<const float*>(sm + k * (3 * MATQ + MATP)), NTOK, e);
+    dtab_part[((long)grp * g.nh + head) * NTAB + e] = a;
+  }
 }
 
 SwinGeom make(int B, int H, int W, int C, int nh, int shift, float scale) {
@@ -847,7 +887,7 @@ template <typename T>
 int ln_bwd_t(const T* x, long xps, const T* dy, long dps, const float* w, const float* mean, const float* rstd, T* dx,
              long dxps, int acc, long M, int C, float* pdw, float* pdb, hipStream_t st) {
   const int P = dmy_layernorm_bwd_blocks(M);
-  const size_t lds = 2 * sizeof(float) * C;
+  const size_t lds = 4 * 2 * sizeof(float) * C;  // [4 waves][2][C]
   int L = ln_lanes<T>(C, xps, dxps, x, dx);
   if (L && (dps % Traits<T>::VW || ((uintptr_t)dy & 15))) L = 0;
   switch (L) {

@@ -455,7 +455,7 @@ inline int egrid(long n) { return grid_cap(ceil_div(n, 256), 8192); }
     __VA_ARGS__;             \
   }
 
-DMY_API int dmy_tal_workspace_bytes(int B, int A, int cap) {
+DMY_API long dmy_tal_workspace_bytes(int B, int A, int cap) {
   // gt[B][cap][5] f32, cnt[B] i32, cand[B][cap][10] i32, nclaim/owner [B][A] i32, metric/norm [B][A] f32,
   // amax_m/amax_o [B][cap] i32, pbox [B][A][4] f32, acc[4] f32
   const long b = 4L * ((long)B * cap * 5 + B + (long)B * cap * TOPK + 2L * B * A + 2L * B * A + 2L * B * cap +

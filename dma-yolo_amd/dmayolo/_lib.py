@@ -14,7 +14,9 @@ LIB_PATH = os.path.join(_HERE, 'libdmayolo_hip.so')
 
 P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_double
 
-# name -> argtypes (return type is int hipError_t unless listed in _RET)
+# name -> argtypes, exactly the header's parameter list (tests/test_abi.py derives both from include/dmayolo.h and
+# compares them); the return type is the header's: long for the *_bytes / *_elems queries and dmy_conv_dgrad_bn_rows,
+# else int (a hipError_t, or a size for the *_rows / *_blocks / *_groups queries)
 SIGNATURES = {
     # conv.hip
     'dmy_conv_fwd_partial_rows': [L, I],
@@ -124,6 +126,15 @@ SIGNATURES = {
 }
 
 
+# symbols whose argtypes dmayolo/optim.py sets itself (multi-tensor optimizer / GradScaler / EMA kernels)
+SELF_BOUND = {'dmy_chunk_size', 'dmy_sgd', 'dmy_adam', 'dmy_ema', 'dmy_amp_check', 'dmy_amp_update'}
+LONG_RET = {'dmy_conv_dgrad_bn_rows'}
+
+
+def restype(name):
+    return ctypes.c_long if name.endswith(('_bytes', '_elems')) or name in LONG_RET else ctypes.c_int
+
+
 class LibraryMissing(RuntimeError):
     pass
 
@@ -136,7 +147,7 @@ def _load():
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError = stale build: fail loudly
         fn.argtypes = argt
-        fn.restype = ctypes.c_long if name.endswith(('_bytes', '_elems')) else ctypes.c_int
+        fn.restype = restype(name)
     return lib
 
 

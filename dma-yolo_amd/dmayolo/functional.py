@@ -54,6 +54,8 @@ def _take_out(N, K, OH, OW, like):
     o, _OUT[0] = _OUT[0], None
     if o is None or tuple(o.shape) != (N, K, OH, OW) or o.dtype != like.dtype or o.device != like.device:
         return None
+    if pixel_stride(o)[0] is not o:  # not NHWC-addressable in place (pixel_stride would copy): a fresh output instead
+        return None
     return o
 
 
@@ -280,11 +282,12 @@ def set_fp8(model, on=True, min_k=3):
     """Config 5 (BASELINE configs[4]): run the forward of every eligible conv (input channels % 128 == 0, kernel
     >= min_k) on the fp8 e4m3 MFMA kernel; the backward stays bf16.  Default min_k = 3: a 1x1 layer is HBM /
     latency-bound, so its 2x MFMA rate does not pay for quantising its input (profiles/r02, c5 fp8 A/B).
-    Returns the number of convs switched."""
+    Returns the number of convs switched: those fp8_eligible's shape tests (C % 128, K % 8, K >= 32) admit; at run
+    time the layer also needs bf16 activations and a quantised input under the descriptor range."""
     n = 0
     for m in model.modules():
-        if isinstance(m, torch.nn.Conv2d) and m.groups == 1 and m.in_channels % 128 == 0 and m.out_channels % 8 == 0 \
-                and m.kernel_size[0] >= min_k:
+        if isinstance(m, torch.nn.Conv2d) and m.groups == 1 and m.kernel_size[0] >= min_k \
+                and fp8_eligible(m.in_channels, m.out_channels, torch.bfloat16, 0):
             m.dmy_fp8 = bool(on)
             n += 1
     PARAM_GEN[0] += 1  # drop cached inference weights / coefficients

@@ -17,7 +17,7 @@ lib.dmy_chunk_size.argtypes = []
 CHUNK = lib.dmy_chunk_size()
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 lib.dmy_sgd.argtypes = [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _P, _P, _P]
-lib.dmy_adam.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P]
+lib.dmy_adam.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P, _P]
 lib.dmy_ema.argtypes = [_P, _P, _P, _P, _P, _I, _F, _P]
 lib.dmy_amp_check.argtypes = [_P, _P, _P, _P, _I, _P, _P, _P]
 lib.dmy_amp_update.argtypes = [_P, _P, _P, _P, _F, _F, _F, _I, _P]
@@ -110,24 +110,26 @@ class FusedAdam(torch.optim.Optimizer):
             if not ps:
                 continue
             ms, vs = [], []
+            step = g.get('_dstep')
+            if step is None:  # the group's step count lives on the device (one int32 shared by its params' state)
+                t0 = max((int(self.state[p]['step']) for p in ps if 'step' in self.state[p]), default=0)
+                step = g['_dstep'] = torch.full((1,), t0, dtype=torch.int32, device=ps[0].device)
             for p in ps:
                 st = self.state[p]
-                if 'step' not in st:
-                    st['step'] = 0
+                if 'exp_avg' not in st:
                     st['exp_avg'] = torch.zeros_like(p)
                     st['exp_avg_sq'] = torch.zeros_like(p)
-                st['step'] += 1
+                st['step'] = step  # torch keeps Adam's step as a tensor too; read it (host sync) only to log
                 ms.append(st['exp_avg'])
                 vs.append(st['exp_avg_sq'])
-            t = self.state[ps[0]]['step']
             b1, b2 = g['betas']
-            bc1 = 1 - b1 ** t
-            bc2s = (1 - b2 ** t) ** 0.5
             tb = _Table.get([ps, [p.grad for p in ps], ms, vs], ps[0].device)
             PARAM_GEN[0] += 1
+            # bias corrections from the device count (t = count + 1), which the kernel advances unless the GradScaler
+            # found a non-finite gradient: a skipped step leaves t alone, as torch (scaler.step skips optimizer.step)
             _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
                                 float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
-                                float(bc1), float(bc2s), *_amp_ptrs(self), stream()), 'dmy_adam')
+                                0.0, 0.0, *_amp_ptrs(self), ctypes.c_void_p(step.data_ptr()), stream()), 'dmy_adam')
         return None
 
 

@@ -222,9 +222,12 @@ int dmy_chunk_size(void);
 int dmy_sgd(float* const* p, const float* const* g, float* const* m, const long* n, const int* tid, const long* off,
             int nchunks, float lr, float momentum, float weight_decay, int nesterov, const float* scale,
             const float* found, void* stream);
+/* dstep: NULL (bias corrections from the two floats) or the group's device step count before this step: the kernel
+ * derives the bias corrections from it and advances it unless the GradScaler skipped the step (as torch's Adam t). */
 int dmy_adam(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n, const int* tid,
              const long* off, int nchunks, float lr, float beta1, float beta2, float eps, float weight_decay,
-             float bias_corr1, float bias_corr2_sqrt, const float* scale, const float* found, void* stream);
+             float bias_corr1, float bias_corr2_sqrt, const float* scale, const float* found, int* dstep,
+             void* stream);
 /* scaler.unscale_ check: *found = 1 if any g * (1 / *scale) is non-finite (found is not cleared here) */
 int dmy_amp_check(const float* const* g, const long* n, const int* tid, const long* off, int nchunks,
                   const float* scale, float* found, void* stream);
@@ -239,7 +242,7 @@ int dmy_ema(float* const* ema, const float* const* src, const long* n, const int
  *      utils/tal.py:81-221 (ComputeLoss_TAL, BboxLoss, bbox2dist) and utils/tal_assign.py:54-189
  *      (TaskAlignedAssigner); models/common.py:1451-1458 (space_to_depth).  H, W, stride are HOST
  *      arrays of nl entries; box / cls are read through (batch, channel, anchor) element strides. */
-int dmy_tal_workspace_bytes(int B, int A, int cap);
+long dmy_tal_workspace_bytes(int B, int A, int cap);
 int dmy_tal_loss(int dtype, const void* box, long sbb, long sbc, long sba, const void* cls, long scb, long scc, long sca,
                  int B, int nc, int nl, const int* H, const int* W, const float* stride, const float* targets, int nt,
                  float alpha, float beta, float pos_weight, void* workspace, float* G, float* loss, float* items,

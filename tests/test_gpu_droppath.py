@@ -42,3 +42,49 @@ def test_drop_path_identity_in_eval_and_at_zero():
     x = torch.randn(4, 8, 5, 5, device='cuda')
     assert DropPath(0.5).eval()(x) is x
     assert DropPath(0.0).train()(x) is x
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_c3str_active_droppath_inplace_concat_matches_copy(dtype):
+    """with DropPath active (train mode) the last Swin layer cannot write into the C3STR concat slice, so
+    C3.forward's in-place mode (DMY_INPLACE_CAT=2) mixes a producer that returns its own tensor (Swin) with one that
+    wrote in place (cv2).  Forward, input gradient and every parameter gradient must equal the copying concat
+    (DMY_INPLACE_CAT=0) on the same DropPath draws (same CUDA seed), bit for bit: the kernels and their operands are
+    the same, only where the concat's halves come from differs."""
+    import copy
+    from dmayolo.models import common as P
+    from dmayolo.models.swin import DropPath
+    torch.manual_seed(0)
+    base = P.C3STR(64, 64, n=2)
+    for layer in base.m.tr:
+        layer.drop_path = DropPath(0.4)
+    base = base.cuda().train()
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.randn(4, 64, 16, 16, generator=g).to(dtype).cuda().contiguous(memory_format=torch.channels_last)
+    gup = torch.randn(4, 64, 16, 16, generator=g).to(dtype).cuda().contiguous(memory_format=torch.channels_last)
+    import dmayolo.functional as Fn
+    res = []
+    old = P._INPLACE_CAT
+    Fn.set_deterministic(True)  # split-K weight-grads reduced in split order: the two runs sum identically
+    try:
+        for mode in (0, 2):
+            P._INPLACE_CAT = mode
+            m = copy.deepcopy(base)
+            x = x0.clone().requires_grad_(True)
+            torch.cuda.manual_seed(321)
+            y = m(x)
+            y.backward(gup)
+            res.append((y.detach().float(), x.grad.float(), {k: p.grad.clone() for k, p in m.named_parameters()
+                                                             if p.grad is not None}))
+    finally:
+        P._INPLACE_CAT = old
+        Fn.set_deterministic(False)
+    (y0, gx0, gp0), (y2, gx2, gp2) = res
+    torch.cuda.manual_seed(321)
+    drops = [float((0.6 + torch.rand(4, device='cuda')).floor_().sum()) for _ in range(4)]
+    assert any(d < 4 for d in drops), 'the seed should drop at least one sample in some layer'
+    assert torch.equal(y0, y2)
+    assert torch.equal(gx0, gx2)
+    assert set(gp0) == set(gp2) and len(gp0) > 10
+    diff = [k for k in gp0 if not torch.equal(gp0[k], gp2[k])]
+    assert not diff, diff

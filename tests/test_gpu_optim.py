@@ -169,3 +169,31 @@ def test_trainer_steady_state_reuses_pointer_tables():
     finally:
         optim._Table.__init__ = orig
     assert built[0] == 0, (built[0], n0)
+
+
+def test_fused_adam_skipped_step_leaves_bias_correction():
+    """a step the GradScaler skips (non-finite gradient) must not advance Adam's t.  torch: scaler.step()
+    never calls optimizer.step(), so the bias corrections 1 - b^t of the next real step use the old t.  FusedAdam keeps t
+    on the device and the kernel advances it only when the step ran: steps (finite, non-finite, finite) here equal
+    torch.optim.Adam taking the two finite steps."""
+    from dmayolo.optim import FusedAdam, GradScaler
+    torch.manual_seed(0)
+    a = torch.nn.Parameter(torch.randn(10000, device='cuda'))
+    ra = torch.nn.Parameter(a.detach().cpu().clone())
+    opt = FusedAdam([a], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    ref = torch.optim.Adam([ra], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    scaler = GradScaler(a.device, enabled=True)
+    g = torch.Generator().manual_seed(3)
+    for i in range(3):
+        gr = torch.randn(10000, generator=g)
+        s = float(scaler.scale.cpu())
+        a.grad = (gr * s).cuda()
+        if i == 1:
+            a.grad[17] = float('inf')
+        scaler.step(opt)
+        scaler.update()
+        if i != 1:
+            ra.grad = gr.clone()
+            ref.step()
+    assert int(opt.state[a]['step'].cpu()) == 2
+    torch.testing.assert_close(a.detach().cpu(), ra.detach(), **TOL_ADAM)
