@@ -59,6 +59,8 @@ def parse():
     ap.add_argument('--no-detect', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--layer-report', action='store_true', help='per-conv-shape timing table on stderr')
+    ap.add_argument('--launch-table', default='', help='CSV of every timed conv launch of the roofline pass (kind, '
+                    'shape, algorithmic flops / bytes, measured us, roofline us): the table behind roofline.frac')
     ap.add_argument('--fp8', action='store_true',
                     help='config 5 (BASELINE configs[4]): e4m3 MFMA forward for every conv with C %% 128 == 0')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
@@ -143,6 +145,24 @@ def cpu_baseline(cfg, seconds):
             break
     return dict(value=n / el, unit='images/s', cores=torch.get_num_threads(), kind='port',
                 sample=f'{n} bs1 train steps of {yml} @{img} (fp32 CPU oracle, {el:.1f} s)')
+
+
+def write_launch_table(path, table, ks, cfg_name):
+    """One row per timed conv launch: T_roof = max(F / P_mfma, B / BW_hbm) (the bench's peaks), and per kind the
+    check line sum T_roof / sum t, which is roofline.frac for the dominant kind."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, 'w') as f:
+        f.write(f'# {cfg_name}: conv launches of the roofline pass; peaks {PEAK_FLOPS[torch.bfloat16] / 1e12:.0f} '
+                f'TFLOP/s bf16, {PEAK_FLOPS["fp8"] / 1e12:.0f} fp8, {PEAK_BW / 1e9:.0f} GB/s\n')
+        f.write('kind,N,C,H,W,K,k,s,flops,bytes,us,troof_us,bound\n')
+        for kind, tag, fl, nb, t, tr in table:
+            pk = PEAK_FLOPS['fp8'] if kind.endswith('_f8') else PEAK_FLOPS[torch.bfloat16]
+            f.write('%s,%s,%.0f,%.0f,%.3f,%.3f,%s\n' % (kind, ','.join(str(v) for v in tag), fl, nb, t * 1e6, tr * 1e6,
+                                                        'mfma' if fl / pk >= nb / PEAK_BW else 'hbm'))
+        for kind, d in ks.items():
+            f.write('# %s: %d launches, sum t %.3f ms, sum T_roof %.3f ms, frac %.4f\n'
+                    % (kind, d['launches'], d['seconds'] * 1e3, (d['troof_mfma'] + d['troof_hbm']) * 1e3,
+                       (d['troof_mfma'] + d['troof_hbm']) / d['seconds']))
 
 
 def roofline(ks, steps, el_events, dtype, cfg_name):
@@ -231,7 +251,11 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     el_events = time.perf_counter() - t1
     KernelTimer.enabled = False
     detail = {} if a.layer_report else None
-    ks = KernelTimer.summary(detail, PEAK_FLOPS[dtype], PEAK_BW, peak_flops_f8=PEAK_FLOPS['fp8'])
+    table = [] if a.launch_table else None
+    ks = KernelTimer.summary(detail, PEAK_FLOPS[dtype], PEAK_BW, peak_flops_f8=PEAK_FLOPS['fp8'], table=table)
+    if table is not None and rank == 0:
+        write_launch_table(a.launch_table if name == a.config else a.launch_table.replace('.csv', f'_{name}.csv'),
+                           table, ks, name)
     if detail and rank == 0:
         tot = sum(v[2] for v in detail.values())
         print(f'[{name}] kind        N    C    H    W    K  k s  launches  ms/step  TFLOP/s  share', file=sys.stderr)

@@ -132,6 +132,66 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
   }
 }
 
+// Config 5 (fp8 forward convs) with delayed scaling: the producer of an e4m3 conv's input emits the e4m3 copy itself.
+// y = act(z * scale + shift) (+ res) as bn_act_fwd_vec (bf16), plus y8[m][c] = e4m3(y * 448 / amax) dense, where amax
+// is the PREVIOUS step's max |y| (the G block maxima `pmax` it left, reduced here by every block; block 0 records it
+// in used[0] for the conv's dequantisation), and this step's block maxima go to nmax[blockIdx.x] for the next step.
+// Values above the previous amax saturate at +-448 (delayed scaling).  A NaN anywhere makes the next amax NaN.
+__global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restrict__ z, long zps,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, int act,
+                                                            const bf16* __restrict__ res, long rps, bf16* __restrict__ y,
+                                                            long yps, long M, int C, unsigned char* __restrict__ y8,
+                                                            const float* __restrict__ pmax, int G,
+                                                            float* __restrict__ nmax, float* __restrict__ used) {
+  __shared__ float red[4];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < G; i += 256) a = nanmax(a, pmax[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a = nanmax(a, __shfl_xor(a, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  a = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) used[0] = a;
+  const float inv = a > 0.f ? 448.f / a : 1.f;
+  RowMap rm(C, 8);
+  float mx = 0.f;
+  if (rm.active()) {
+    const int c0 = rm.cv * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+    for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
+      float f[8];
+      unpack<bf16>(*reinterpret_cast<const uint4*>(z + m * zps + c0), f);
+      if (res) {
+        float r[8];
+        unpack<bf16>(*reinterpret_cast<const uint4*>(res + m * rps + c0), r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+      }
+      const uint4 v = pack<bf16>(f);
+      *reinterpret_cast<uint4*>(y + m * yps + c0) = v;
+      unpack<bf16>(v, f);  // quantise the stored (bf16-rounded) value, as a separate pass over y would
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = nanmax(mx, fabsf(f[j]));
+      uint2 o;
+      o.x = pack4_e4m3(f[0] * inv, f[1] * inv, f[2] * inv, f[3] * inv);
+      o.y = pack4_e4m3(f[4] * inv, f[5] * inv, f[6] * inv, f[7] * inv);
+      *reinterpret_cast<uint2*>(y8 + m * C + c0) = o;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = nanmax(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) nmax[blockIdx.x] = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
+}
+
 template <typename T>
 __global__ void bn_act_fwd_scalar(const T* __restrict__ z, long zps, const float* __restrict__ scale,
                                   const float* __restrict__ shift, int act, const T* __restrict__ res, long rps,
@@ -408,6 +468,19 @@ DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scal
     if (dtype) bn_act_fwd_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
     else bn_act_fwd_scalar<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
   }
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_bn_act_f8_blocks(void) { return 1024; }
+
+DMY_API int dmy_bn_act_fwd_f8(const void* z, long zps, const float* scale, const float* shift, int act, const void* res,
+                              long rps, void* y, long yps, long M, int C, void* y8, const float* pmax, float* nmax,
+                              float* used, void* stream) {
+  if (C % 8 != 0 || C / 8 > 256 || !vec_ok(8, C, zps, yps, res ? rps : 0, z, y, res) || ((uintptr_t)y8 & 7))
+    return (int)hipErrorInvalidValue;
+  const int G = dmy_bn_act_f8_blocks();
+  bn_act_fwd_f8_kernel<<<G, 256, 0, (hipStream_t)stream>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps,
+                                                          (bf16*)y, yps, M, C, (unsigned char*)y8, pmax, G, nmax, used);
   return (int)hipGetLastError();
 }
 

@@ -99,6 +99,17 @@ DEV float wave_max(float v) {
   return v;
 }
 
+DEV unsigned pack4_e4m3(float a, float b, float c, float d) {  // OCP e4m3fn, round to nearest even, saturated
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+DEV float nanmax(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b); }
+
 #define HIP_LAUNCH_CHECK() return (int)hipGetLastError()
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

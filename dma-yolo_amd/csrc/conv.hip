@@ -1397,6 +1397,197 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_p1_persist(const bf16* __re
   }
 }
 
+// Persistent 1x1 GEMM with a register epilogue (stride-1 1x1 forward / data-grad, DMY_P1P).  The 1x1 layers are
+// HBM-bound with 1..8 K steps per tile; on the one-tile blocks above every tile pays its load prologue and an
+// LDS-staged epilogue (tile -> LDS -> barrier -> stores) with nothing else in flight, and they stream at 2.5-3.5 TB/s
+// in the training step.  Here each block walks tiles t = b, b + G, ... (XCD-contiguous order) through ONE LDS-DMA
+// ring that runs ahead across tile boundaries, and the epilogue never touches the ring: the MFMA runs transposed
+// (D[channel][pixel] = W X^T, so a lane ends with 4 consecutive channels of one pixel), a permlane16 swap pairs two
+// 16-channel tiles into 8 consecutive channels = one 16-B buffer store straight from registers, and the BN partials
+// are reduced over the 16 pixel lanes with DPP and transposed through a 512-B per-wave LDS scratch.  Every memory
+// operation of the epilogue is an unconditional buffer instruction (masked rows / columns get an out-of-range
+// offset), so the counted vmcnt waits of the next tile's first steps know exactly how many stores are younger than
+// the stage they wait for, and the stores drain under the next tile's MFMAs.
+DEV float row_sum16(float v) {  // lane 15 of each 16-lane row ends with the row's total
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0.f, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  return v;
+}
+DEV unsigned pk2_bf16(float a, float b) {
+  const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
+         ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
+}
+
+template <int BM, int BN, int NS, int WTR>
+struct P1P {
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
+  static constexpr int NW = C3_::NW, NTH = C3_::NTH, PER = C3_::APW + C3_::BPW;
+  static constexpr int NI = WTR / 16;      // 16-pixel blocks per wave
+  static constexpr int NST = NI * 2;       // 16-B output stores per lane per tile (two 32-channel halves per block)
+  static constexpr int LDS = NS * C3_::STAGE + NW * 512;
+};
+
+template <int BM, int BN, int NS, int WTR, bool DG>
+__global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
+    const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias, bf16* __restrict__ y,
+    float* __restrict__ psum, float* __restrict__ psq, int /*accumulate: 0*/, Geom g, int gm, int gn, unsigned xbytes,
+    unsigned wbytes, unsigned ybytes, int nprow) {
+  using PP = P1P<BM, BN, NS, WTR>;
+  using C3_ = typename PP::C3_;
+  constexpr int PER = PP::PER, NI = PP::NI;
+  // epilogue VMEM instructions per lane (all unconditional): NST stores (+ NST loads when accumulating), and with BN
+  // partials 2 stores per partial row the wave covers
+  static_assert(NS == 2 || NS == 3, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[PP::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  const int q = lane >> 4, pl = lane & 15;
+  float* red = reinterpret_cast<float*>(smem + NS * C3_::STAGE) + wid * 128;
+  const long M = (long)g.N * g.OH * g.OW;
+  const int ntiles = gm * gn, nk = g.C / BK, G = gridDim.x;
+  if ((int)blockIdx.x >= ntiles) return;
+  const bool half = g.K <= 64;
+  const int PR = half ? 32 : 64;                 // pixels per BN partial row (dmy_conv_fwd_partial_rows)
+  const int ngrp = psum != nullptr ? WTR / PR : 0;
+  const int nepi = PP::NST + 2 * ngrp;  // this wave's epilogue VMEM ops per tile (no accumulate: the host routes it away)
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, ybytes);
+  const __amdgpu_buffer_rsrc_t rps = make_rsrc(psum, psum != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t rpq = make_rsrc(psq, psq != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
+  using LD = FwdLdsB<BM, BN, NS, true, DG, false, 2, WTR>;
+  auto tile_of = [&](int L) { return xcd_remap(L, ntiles); };
+  // issue cursor: (round, k step) of the next stage to load
+  int lr = 0, lk = 0;
+  int lt = tile_of(blockIdx.x);
+  LD ld(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
+  const int my_tiles = (ntiles - 1 - (int)blockIdx.x) / G + 1, total = my_tiles * nk;
+  auto issue = [&](int st) {
+    ld.issue(smem + (st % NS) * C3_::STAGE, wid);
+    if (++lk == nk) {
+      lk = 0;
+      ++lr;
+      const int L = lr * G + (int)blockIdx.x;
+      if (L < ntiles) {
+        lt = tile_of(L);
+        ld = LD(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
+      }
+    }
+  };
+  issue(0);
+  if (NS == 3 && total > 1) issue(1);
+  int s = 0;
+  for (int r = 0; r < my_tiles; ++r) {
+    const int t = tile_of(r * G + (int)blockIdx.x);
+    const int tm = t / gn, tn = t % gn;
+    const long m0 = (long)tm * BM;
+    const int n0 = tn * BN;
+    f32x4 acc[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++s) {
+      // stage s landed: younger VMEM ops allowed in flight = the next stage (NS = 3, if issued) + the previous tile's
+      // epilogue when it was issued after stage s (kt < NS - 1 on every tile but the block's first)
+      const bool nxt = NS == 3 && s + 1 < total;
+      const bool epi = r > 0 && kt < NS - 1;
+      if (!epi) {
+        if (nxt) vm_wait<PER>();
+        else vm_wait<0>();
+      } else if (nepi == PP::NST) {
+        if (nxt) vm_wait<PER + PP::NST>();
+        else vm_wait<PP::NST>();
+      } else if (nepi == PP::NST + 2 * (WTR / 64)) {
+        if (nxt) vm_wait<PER + PP::NST + 2 * (WTR / 64)>();
+        else vm_wait<PP::NST + 2 * (WTR / 64)>();
+      } else if (nepi == PP::NST + 2 * (WTR / 32)) {
+        if (nxt) vm_wait<PER + PP::NST + 2 * (WTR / 32)>();
+        else vm_wait<PP::NST + 2 * (WTR / 32)>();
+      } else {
+        vm_wait<0>();  // other epilogue shapes (accumulate, 32-pixel partial rows): wait for everything
+      }
+      __builtin_amdgcn_s_barrier();
+      if (s + NS - 1 < total) issue(s + NS - 1);
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
+      const bf16* Bs = As + BM * BK;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[NI], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) a[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    // ---- register epilogue: acc[i][j][r] = Y[pixel m0 + wm WTR + 16 i + pl][channel n0 + wn 64 + 16 j + 4 q + r]
+    const long mw = m0 + wm * WTR;
+    const int nw = n0 + wn * 64;
+    if (bias != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int n = nw + 16 * j + 4 * q + rr;
+          const float bv = n < g.K ? bias[n] : 0.f;
+#pragma unroll
+          for (int i = 0; i < NI; ++i) acc[i][j][rr] += bv;
+        }
+    }
+    if (psum != nullptr) {
+      for (int gi = 0; gi < ngrp; ++gi) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              if (i * 16 / PR != gi) continue;
+              const float v = mw + 16 * i + pl < M ? acc[i][j][rr] : 0.f;
+              s1 += v;
+              s2 += v * v;
+            }
+            s1 = row_sum16(s1);
+            s2 = row_sum16(s2);
+            if (pl == 15) {
+              red[16 * j + 4 * q + rr] = s1;
+              red[64 + 16 * j + 4 * q + rr] = s2;
+            }
+          }
+        __builtin_amdgcn_wave_barrier();
+        const float v1 = red[lane], v2 = red[64 + lane];
+        __builtin_amdgcn_wave_barrier();
+        const long prow = (mw + gi * PR) / PR;
+        const bool ok = prow < nprow && nw + lane < g.K;
+        const unsigned off = ok ? (unsigned)((prow * g.K + nw + lane) * 4) : kBufOob;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1), rps, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v2), rpq, off, 0, 0);
+      }
+    }
+    const int chq = (q & 1) * 16 + (q >> 1) * 8;
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const f32x4 &a = acc[i][2 * jp], &b = acc[i][2 * jp + 1];
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
+        u4 v = {s0[0], s1[0], s0[1], s1[1]};
+        const long m = mw + 16 * i + pl;
+        const int n = nw + 32 * jp + chq;
+        const unsigned off = (m < M && n < g.K) ? (unsigned)((m * g.yps + n) * 2) : kBufOob;
+        __builtin_amdgcn_raw_buffer_store_b128(v, ry, off, 0, 0);
+      }
+  }
+}
+
 // Forward (DG = false) or stride-1 data-grad (DG = true; `g` is the GEMM view built by the host:
 // rows = input pixels, columns = input channels, gather = dy) with the BN-partial / accumulate epilogue.
 template <int BM, int BN, int NS, bool P1, bool DG, int BUF>
@@ -1545,19 +1736,6 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
 // channels of one pixel, and a permlane16 swap pairs two 16-channel tiles into 8 consecutive channels = one 16-B
 // store. BN partials (one row per 64 pixels, per 32 when the layer has <= 64 columns: dmy_conv_fwd_partial_rows)
 // are reduced over the 16 pixel lanes with DPP row shifts. Every X element is read once per column group.
-DEV float row_sum16(float v) {  // lane 15 of each 16-lane row ends with the row's total
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x111, 0xf, 0xf, true);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x112, 0xf, 0xf, true);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x114, 0xf, 0xf, true);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x118, 0xf, 0xf, true);  // row_shr:8
-  return v;
-}
-DEV unsigned pk2_bf16(float a, float b) {
-  const bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
-  return (unsigned)*reinterpret_cast<const unsigned short*>(&x) |
-         ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
-}
-
 // G3: the same streaming GEMM over a 3x3 stride-1 pad-1 gather of a 16-channel input (the space-to-depth stem of every
 // yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
 // 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
@@ -2847,6 +3025,52 @@ inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, flo
 #undef P1S_GO
 }
 
+// persistent 1x1 GEMM with the register epilogue (v3::conv_p1p): DMY_P1P = 0 off, 1 (default) = 256 x 128 tiles (3
+// stages) for <= p1p_maxn() columns, 2 = 256 x 256 (2 stages, 128-row wave tiles) for >= 256 columns, 3 = 128 x 128 (2 stages, 2 blocks
+// per CU).  Not for the inference epilogue, the fused producer-BN reduce or an accumulating data-grad.
+inline int p1p_mode() {
+  static const int t = env_int("DMY_P1P", 1);
+  return t;
+}
+// default routing: GEMM views with <= DMY_P1P_MAXN columns (cold-cache A/B on the DMA-YOLO 1x1 shapes,
+// profiles/r03/ab_p1p.log: 256 -> 256 @96^2 fwd 118.7 -> 94.8 us, 128 -> 128 @384^2 636 -> 492 us, 4..23 % on every
+// <= 256-column view; 7..15 % SLOWER on the 512..1280-column views, where the 256 x 256 wide tile reads each input
+// row once)
+inline int p1p_maxn() {
+  static const int t = env_int("DMY_P1P_MAXN", 256);
+  return t;
+}
+template <bool DG>
+int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
+               hipStream_t st, unsigned xbytes, unsigned wbytes) {
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const int nk = gv.C / v3::BK, mode = p1p_mode();
+  const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
+  if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || nk < 1 || (mode == 1 && gv.K > p1p_maxn())) return -1;
+  const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
+  const int NC = num_cus();
+#define P1P_GO(BM, BN, NS, WTR)                                                                                  \
+  {                                                                                                              \
+    using PP = v3::P1P<BM, BN, NS, WTR>;                                                                         \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN), ntiles = gm * gn;                                   \
+    const int bpc = (160 * 1024) / PP::LDS;                                                                      \
+    int G = NC * (bpc < 1 ? 1 : bpc);                                                                            \
+    if (G > ntiles) G = ntiles;                                                                                  \
+    else G = G / 8 * 8;                                                                                          \
+    v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
+                                                                      wbytes, (unsigned)yb, nprow);              \
+    return (int)hipGetLastError();                                                                               \
+  }
+  if (mode == 3 && gv.K > 64) P1P_GO(128, 128, 2, 64)
+  if (mode == 2 && gv.K >= 256) P1P_GO(256, 256, 2, 128)
+  if (gv.K > 64) {
+    if (nk >= 2) P1P_GO(256, 128, 3, 64)
+    P1P_GO(256, 128, 2, 64)
+  }
+  P1P_GO(256, 64, 2, 64)
+#undef P1P_GO
+}
+
 template <bool DG>
 int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
               hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}, int tov = -1) {
@@ -2877,6 +3101,10 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       if (p1) V3_GO(BM, BN, NS, true, 0);                    \
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
+  }
+  if (p1 && buf && p1p_mode() && tov < 0 && !ep.on && bb.z == nullptr) {  // persistent 1x1, register epilogue
+    const int r = launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes);
+    if (r >= 0) return r;
   }
   if (p1 && buf && p1_persist_mode() && tov < 0) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
     const int NC = num_cus();
@@ -3387,23 +3615,12 @@ DMY_API int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* d
 // BN partial rows of the forward epilogue: 2 per 128 (big tile) or 64 rows of M.  The v3 kernel's
 // 64-row wave rows number the same way (wave row wm of 256-row tile tm = row 4 tm + wm).
 // ---------------------------------------------------------------- fp8 operand preparation
-DEV unsigned pack4_e4m3(float a, float b, float c, float d) {  // OCP e4m3fn, round to nearest even, saturated
-  a = fminf(fmaxf(a, -448.f), 448.f);
-  b = fminf(fmaxf(b, -448.f), 448.f);
-  c = fminf(fmaxf(c, -448.f), 448.f);
-  d = fminf(fmaxf(d, -448.f), 448.f);
-  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-  return (unsigned)v;
-}
-
 // Per-tensor activation scaling in two passes without atomics: fp8_blockmax_kernel writes one max per block
 // (grid G <= kF8Blocks), fp8_quant_kernel reduces those G maxima in every block (G floats from L2), records the
 // amax it used for the conv's dequantisation and writes x8[row][c] = e4m3(x * 448 / amax) densely.  A NaN
 // anywhere makes amax NaN (and so the conv output), as an unquantised conv would propagate it.
 constexpr int kF8Blocks = 1024;
 
-DEV float nanmax(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b); }
 
 DEV float block_nanmax(float m, float* red) {  // 256 threads
 #pragma unroll

@@ -235,11 +235,11 @@ class WeightPrep:
 class ConvSpec:
     """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None).
     wcache / ecache: inference-only caches of the prepped weight and the eval BN coefficients."""
-    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', 'fp8', 'f8cache', '__weakref__')
+    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', 'fp8', 'f8cache', 'f8_emit', '__weakref__')
 
     def __init__(self, stride, pad, act, bn=None):
         self.stride, self.pad, self.act, self.bn = int(stride), int(pad), int(act), bn
-        self.wcache = self.ecache = self.f8cache = None
+        self.wcache = self.ecache = self.f8cache = self.f8_emit = None
         self.fp8 = False
 
 
@@ -302,12 +302,56 @@ def _f8_ws():
     return _F8_WS[0]
 
 
-def _fp8_operands(x, xps, weight, spec, wkey):
-    """per-tensor e4m3 copy of the activation (current amax, dmy_fp8_quant) and the per-output-channel e4m3
-    weight (cached on the spec until the weight changes)"""
+# delayed (previous-step) activation scaling for the fp8 convs: the producing layer emits the e4m3 copy of its
+# output in its BN-act pass (dmy_bn_act_fwd_f8) instead of two quantisation passes over it (dmy_fp8_quant).
+# DMY_F8_DELAYED=0 keeps the just-in-time quantisation with the current amax.
+F8_DELAYED = [os.environ.get('DMY_F8_DELAYED', '1') == '1']
+
+
+class F8Emit:
+    """Per producer layer: two ping-pong arrays of block maxima (this step's |y| maxima become the next step's
+    quantisation amax).  The first step only records maxima (its consumer quantises just in time)."""
+    __slots__ = ('buf', 'p', 'valid')
+
+    def __init__(self, dev):
+        nb = call('dmy_bn_act_f8_blocks')
+        self.buf = torch.zeros(2, nb, dtype=torch.float32, device=dev)
+        self.p, self.valid = 0, False
+
+    def run(self, z, scale, shift, act, res, rps, y, yps, M, K):
+        """BN-act of the producer with the e4m3 side output; returns (y8, used amax) or None on the first step"""
+        y8 = torch.empty(M * K, dtype=torch.uint8, device=z.device)
+        used = f32(1, z.device)
+        call('dmy_bn_act_fwd_f8', ptr(z), K, ptr(scale), ptr(shift), act, ptr(res), rps, ptr(y), yps, M, K, ptr(y8),
+             ptr(self.buf[self.p]), ptr(self.buf[1 - self.p]), ptr(used), stream())
+        self.p ^= 1
+        out = (y8, used) if self.valid else None
+        self.valid = True
+        return out
+
+
+def _fp8_weight(weight, spec, wkey, dev):
+    K, C, KH, KW = weight.shape
+    fc = spec.f8cache
+    if fc is not None and fc[0] == wkey:
+        return fc[1], fc[2]
+    w8 = torch.empty(weight.numel(), dtype=torch.uint8, device=dev)
+    ws = f32(K, dev)
+    call('dmy_conv_wprep_fp8', ptr(weight.detach().contiguous()), ptr(w8), ptr(ws), K, C, KH, KW, stream())
+    spec.f8cache = (wkey, w8, ws)
+    return w8, ws
+
+
+def _fp8_operands(x, xps, weight, spec, wkey, f8in=None):
+    """per-tensor e4m3 copy of the activation and the per-output-channel e4m3 weight (cached on the spec until the
+    weight changes).  f8in = (x8, amax) emitted by the producer (delayed scaling), else dmy_fp8_quant with the
+    current amax"""
     N, C, H, W = x.shape
     K, _, KH, KW = weight.shape
     rows = N * H * W
+    if f8in is not None:
+        w8, ws = _fp8_weight(weight, spec, wkey, x.device)
+        return f8in[0], f8in[1], w8, ws
     x8 = torch.empty(rows * C, dtype=torch.uint8, device=x.device)
     amax = f32(_F8_WS[0] or _f8_ws(), x.device)  # [0] = the amax the quantisation used
     call('dmy_fp8_quant', ptr(x), rows, C, xps, ptr(x8), ptr(amax), stream())
@@ -363,15 +407,18 @@ class KernelTimer:
         cls.records.append((kind, flops, nbytes, e0, e1, tag))
 
     @classmethod
-    def summary(cls, detail=None, peak_flops=2.5e15, peak_bw=8.0e12, peak_flops_f8=5.0e15):
+    def summary(cls, detail=None, peak_flops=2.5e15, peak_bw=8.0e12, peak_flops_f8=5.0e15, table=None):
         """Per-kind totals: launches, flops, seconds, bytes, and the roofline time sum_launches max(F / peak_flops,
         B / peak_bw) split by the binding resource (troof_mfma / troof_hbm).  When `detail` is a dict it also
-        receives per-(kind, shape) [launches, flops, seconds, bytes]."""
+        receives per-(kind, shape) [launches, flops, seconds, bytes]; when `table` is a list it receives one
+        (kind, shape tag, flops, bytes, seconds, roofline seconds) tuple per launch, in launch order."""
         torch.cuda.synchronize()
         out = {}
         for kind, fl, nb, e0, e1, tag in cls.records:
             t = e0.elapsed_time(e1) * 1e-3
             tm, th = fl / (peak_flops_f8 if kind.endswith('_f8') else peak_flops), nb / peak_bw
+            if table is not None:
+                table.append((kind, tag, fl, nb, t, max(tm, th)))
             d = out.setdefault(kind, [0, 0.0, 0.0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += fl
@@ -468,6 +515,7 @@ class ConvBNActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None, grad_on=True):
         link_in = getattr(x, '_dmy_bnlink', None)
         s2d = getattr(x, '_dmy_s2d', 0)
+        f8in, prod = getattr(x, '_dmy_f8', None), getattr(x, '_dmy_prod', None)
         out_req, _OUT[0] = _OUT[0], None  # conv_bn_act's out view, checked against the output geometry below
         K, C2, k, _ = weight.shape
         ctx.s2d = 0
@@ -524,7 +572,11 @@ class ConvBNActFn(torch.autograd.Function):
         M = N * OH * OW
         f8 = None
         if spec.fp8 and not s2d and Cp == C and fp8_eligible(C, K, dt, N * H * W):
-            f8 = _fp8_operands(x, xps, weight, spec, wkey)
+            if f8in is not None and (f8in[0].numel() != N * H * W * C or not F8_DELAYED[0]):
+                f8in = None
+            f8 = _fp8_operands(x, xps, weight, spec, wkey, f8in)
+            if f8in is None and prod is not None and prod.f8_emit is None and F8_DELAYED[0] and not infer:
+                prod.f8_emit = F8Emit(dev)  # from the next step on, the producer emits this input's e4m3 copy
         if res is not None:
             res, rps = pixel_stride(res)
         else:
@@ -566,8 +618,17 @@ class ConvBNActFn(torch.autograd.Function):
                 call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
                      float(bn.eps), K, ptr(scale), ptr(shift), stream())
             y = out if out is not None else new_act(N, K, OH, OW, x)
-            call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y), yps,
-                 M, K, stream())
+            emit = spec.f8_emit if (F8_DELAYED[0] and dt == torch.bfloat16 and K % 8 == 0 and yps % 8 == 0 and
+                                    (res is None or rps % 8 == 0)) else None
+            if emit is not None and not torch.cuda.is_current_stream_capturing():
+                e8 = emit.run(z, scale, shift, spec.act, res, rps, y, yps, M, K)
+                if e8 is not None:
+                    y._dmy_f8 = e8
+            else:
+                call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(scale), ptr(shift), spec.act, ptr(res), rps, ptr(y),
+                     yps, M, K, stream())
+            if dt == torch.bfloat16 and K % 128 == 0 and train_bn:
+                y._dmy_prod = spec  # an fp8 consumer may ask this layer to emit its e4m3 copy (F8Emit)
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
             ctx.bnlink = None
             if train_bn and need_grad and dt == torch.bfloat16 and FUSE_BN_REDUCE[0]:

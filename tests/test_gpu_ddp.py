@@ -128,7 +128,7 @@ def test_product_ddp_world2_matches_accumulated_single_process(topology):
     assert set(got) == set(exp)
     moved = 0
     dmax = max(float((exp[k] - init[k]).norm()) for k in exp)
-    worst = (0.0, None)
+    worst = (-1.0, '')
     for k, v in got.items():
         torch.testing.assert_close(v, exp[k], rtol=1e-4, atol=1e-6, msg=lambda s: f'{k}: {s}')
         de, dg = exp[k] - init[k], v - init[k]

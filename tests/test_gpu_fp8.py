@@ -174,3 +174,108 @@ def test_config5_fp8_forward_close_to_bf16():
         assert _rel(a, b) < 0.15 and cos > 0.98
     print(f'loss bf16 {lref:.5f} fp8 {lgot:.5f}')
     assert abs(lgot - lref) < 0.05 * abs(lref)
+
+
+def test_fp8_delayed_scaling_equals_jit_on_repeated_batch():
+    """Delayed scaling (functional.F8Emit): from the third train-mode forward on, each fp8 conv's producer emits the
+    e4m3 copy of its output in its BN-act pass with the previous step's amax (dmy_bn_act_fwd_f8) instead of the two
+    dmy_fp8_quant passes.  On a repeated batch with unchanged weights the previous amax IS the current one, so the
+    outputs must equal the just-in-time quantisation bit for bit, and the quantisation passes must be gone."""
+    import dmayolo.functional as Fn
+    from dmayolo.models.yolo import Model
+    from dmayolo.synthetic import images
+    cfg = os.path.join(ROOT, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5l-xs-tr-cbam-spp-bifpn.yaml')
+    x = images(2, 256, device='cuda')
+
+    def run(delayed):
+        Fn.F8_DELAYED[0] = delayed
+        torch.manual_seed(0)
+        m = Model(cfg, nc=3, act_dtype=torch.bfloat16).cuda().train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = 0.0
+        assert Fn.set_fp8(m, True) >= 10
+        counts = {}
+        orig = Fn.call
+
+        def counting(name, *a):
+            counts[name] = counts.get(name, 0) + 1
+            return orig(name, *a)
+        with torch.no_grad():
+            for i in range(3):
+                if i == 2:
+                    Fn.call = counting
+                try:
+                    out = m(x)
+                finally:
+                    Fn.call = orig
+        return [o.float() for o in out], counts
+
+    try:
+        jit, cj = run(False)
+        dly, cd = run(True)
+    finally:
+        Fn.F8_DELAYED[0] = True
+    print('jit', {k: v for k, v in cj.items() if 'f8' in k or 'fp8' in k}, 'delayed',
+          {k: v for k, v in cd.items() if 'f8' in k or 'fp8' in k})
+    assert cd.get('dmy_bn_act_fwd_f8', 0) >= 8
+    assert cd.get('dmy_fp8_quant', 0) <= cj['dmy_fp8_quant'] - cd['dmy_bn_act_fwd_f8']
+    for a, b in zip(dly, jit):
+        assert torch.equal(a, b)
+
+
+def test_config5_fp8_step_vs_fp32_oracle():
+    """BASELINE config 5's fp8 leg against the fp32 CPU oracle (full-width yolov5l-xs-tr-cbam-spp-bifpn @256, bs 2):
+    the product with every eligible conv forward on the e4m3 kernel, and the oracle under the matching storage
+    emulation (tests/precision_emu.py 'fp8': bf16 storage + e4m3 forward operands with the product's per-tensor /
+    per-channel scales, bf16 backward).  Bounds on what the e4m3 kernel computes, the forward: Detect outputs relative
+    L2 per level <= 1.1 * emu + 2e-3 and loss <= 1.1 * emu + 5e-3 (round 3, measured: product 2.43/3.39/1.48/6.54e-2 vs
+    emu 2.28/3.36/1.50/6.48e-2).  The gradient metrics are printed, not bounded: at random init this config's gradient
+    is chaotic under ANY rounding (its CBAM channel maxima, SPP / SPPF argmaxes and global attention route on
+    near-ties) -- the bf16 emulation alone has whole-gradient cosine -0.11 against fp32, the fp8 one 0.007 -- so no
+    gradient bound separates a correct kernel from a wrong one here; the fp8 kernels' backward is bf16 and is pinned
+    by the bf16 tests.  The bf16 emulation's numbers are printed beside them (the e4m3 forward's cost on top of bf16)."""
+    import dmayolo.functional as Fn
+    from dmayolo.models.yolo import Model
+    from dmayolo.utils.loss import ComputeLoss
+    from dmayolo.synthetic import images, targets, HYP_SCRATCH, scaled_hyp
+    from precision_emu import oracle_run, grad_metrics
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = os.path.join(ROOT, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5l-xs-tr-cbam-spp-bifpn.yaml')
+    nc, img, bs = 3, 256, 2
+    torch.manual_seed(0)
+    m = Model(cfg, nc=nc, act_dtype=torch.bfloat16)
+    # anchors: 4 placeholders (range(8), one of zero width): pin real ones as bench.py does, from the label statistics
+    m.model[-1].anchors[:] = torch.tensor([[10, 13], [16, 30], [33, 23], [30, 61]], dtype=torch.float32).view(1, 4, 2) \
+        / m.model[-1].stride.view(-1, 1, 1) * torch.tensor([1.0, 2.0, 4.0, 8.0]).view(-1, 1, 1)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    hyp = scaled_hyp(HYP_SCRATCH, nc, img, m.model[-1].nl)
+    m.hyp = hyp
+    m = m.cuda().train()
+    assert Fn.set_fp8(m, True) >= 10
+    x, t = images(bs, img, seed=1), targets(bs, nc, per_image=20, seed=1)
+    anchors = m.model[-1].anchors.cpu()
+    p = m(x.cuda())
+    loss, items = ComputeLoss(m)(p, t.cuda())
+    loss.backward()
+    runs = {mode: oracle_run(cfg, nc, sd, x, t, anchors, hyp, mode) for mode in (None, 'fp8', 'bf16')}
+    ref, pr, lr_, _ = runs[None]
+    rg = dict(ref.named_parameters())
+    names = [k for k in rg if rg[k].grad is not None]
+
+    def errs(outs, lo, params):
+        o = [_rel(a.detach().float().cpu(), b.detach()) for a, b in zip(outs, pr)]
+        gn, cos = grad_metrics(params, rg, names)
+        return o, abs(float(lo) - float(lr_)) / abs(float(lr_)), gn, cos
+    got = errs(p, loss, dict(m.named_parameters()))
+    e8 = errs(runs['fp8'][1], runs['fp8'][2], dict(runs['fp8'][0].named_parameters()))
+    e16 = errs(runs['bf16'][1], runs['bf16'][2], dict(runs['bf16'][0].named_parameters()))
+    f = lambda r: 'outputs %s loss %.2e grad-norm vector %.2e cos %.4f' % (['%.2e' % v for v in r[0]], r[1], r[2], r[3])  # noqa: E731
+    print(f'config 5 fp8 product: {f(got)}\n  fp8 emulation: {f(e8)}\n  bf16 emulation: {f(e16)}')
+    for a, e in zip(got[0], e8[0]):
+        assert a <= 1.1 * e + 2e-3, (got[0], e8[0])
+    assert got[1] <= 1.1 * e8[1] + 5e-3, (got[1], e8[1])
+    assert max(e8[0]) > 0 and all(a < 0.15 for a in got[0])  # the e4m3 forward really ran and stayed close
