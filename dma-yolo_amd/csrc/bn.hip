@@ -20,6 +20,8 @@ __global__ void bn_stats_kernel(const T* __restrict__ z, long zps, long M, int C
   if (c < C) {
     const long r0 = (long)blockIdx.x * rows_per_block;
     const long r1 = min(M, r0 + rows_per_block);
+    // independent loads in flight: the sums stay sequential per thread (same order)
+#pragma unroll 8
     for (long m = r0 + ty; m < r1; m += 4) {
       float v = to_f(z[m * zps + c]);
       a += v;
@@ -45,6 +47,8 @@ __global__ void bn_finalize_kernel(const float* __restrict__ psum, const float* 
   const int c = blockIdx.x;
   __shared__ double sa[256], sb[256];
   double a = 0.0, b = 0.0;
+  // independent loads in flight: the sums stay sequential per thread (same order)
+#pragma unroll 8
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     a += (double)psum[(long)p * C + c];
     b += (double)psq[(long)p * C + c];
@@ -355,6 +359,8 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdb, const floa
   const int c = blockIdx.x;
   __shared__ double sa[256], sb[256];
   double a = 0.0, b = 0.0;
+  // independent loads in flight: the sums stay sequential per thread (same order)
+#pragma unroll 8
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     a += (double)pdb[(long)p * C + c];
     b += (double)pdg[(long)p * C + c];
@@ -390,6 +396,8 @@ __global__ void colsum2_kernel(const float* __restrict__ a, const float* __restr
   double x = 0.0, y = 0.0;
   if (c < C) {
     const long r0 = (long)blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+    // independent loads in flight: the sums stay sequential per thread (same order)
+#pragma unroll 8
     for (long r = r0 + ty; r < r1; r += 4) {
       x += a[r * C + c];
       y += b[r * C + c];
@@ -552,6 +560,8 @@ __global__ void reduce_rows_kernel(const float* __restrict__ part, int P, int C,
   const int c = blockIdx.x;
   __shared__ double s[256];
   double a = 0.0;
+  // independent loads in flight: the sums stay sequential per thread (same order)
+#pragma unroll 8
   for (int p = threadIdx.x; p < P; p += blockDim.x) a += (double)part[(long)p * C + c];
   s[threadIdx.x] = a;
   __syncthreads();

@@ -1434,7 +1434,7 @@ template <int BM, int BN, int NS, int WTR, bool DG>
 __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
     const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias, bf16* __restrict__ y,
     float* __restrict__ psum, float* __restrict__ psq, int /*accumulate: 0*/, Geom g, int gm, int gn, unsigned xbytes,
-    unsigned wbytes, unsigned ybytes, int nprow) {
+    unsigned wbytes, unsigned ybytes, int nprow, Epi ep, unsigned rbytes) {
   using PP = P1P<BM, BN, NS, WTR>;
   using C3_ = typename PP::C3_;
   constexpr int PER = PP::PER, NI = PP::NI;
@@ -1452,10 +1452,22 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
   const bool half = g.K <= 64;
   const int PR = half ? 32 : 64;                 // pixels per BN partial row (dmy_conv_fwd_partial_rows)
   const int ngrp = psum != nullptr ? WTR / PR : 0;
-  const int nepi = PP::NST + 2 * ngrp;  // this wave's epilogue VMEM ops per tile (no accumulate: the host routes it away)
+  // this wave's epilogue VMEM ops per tile (no accumulate: the host routes it away; the inference epilogue's residual
+  // adds one 16-B load per store)
+  const int nepi = PP::NST * (ep.on && ep.res != nullptr ? 2 : 1) + 2 * ngrp;
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(ep.res, ep.res != nullptr ? rbytes : 0u);
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, ybytes);
   const __amdgpu_buffer_rsrc_t rps = make_rsrc(psum, psum != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
   const __amdgpu_buffer_rsrc_t rpq = make_rsrc(psq, psq != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
+  if (psum != nullptr && BM < 2 * PR && blockIdx.x == 0) {
+    // dmy_conv_fwd_partial_rows rounds the partial rows up to an even count; with 64-row tiles the last one can lie
+    // past every tile: it holds no pixels and must still read as zero (plain stores, older than any stage load)
+    for (long pr = (long)gm * BM / PR + threadIdx.x / 64; pr < nprow; pr += PP::NW)
+      for (int c = lane; c < g.K; c += 64) {
+        psum[pr * g.K + c] = 0.f;
+        psq[pr * g.K + c] = 0.f;
+      }
+  }
   using LD = FwdLdsB<BM, BN, NS, true, DG, false, 2, WTR>;
   auto tile_of = [&](int L) { return xcd_remap(L, ntiles); };
   // issue cursor: (round, k step) of the next stage to load
@@ -1505,6 +1517,9 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
       } else if (nepi == PP::NST + 2 * (WTR / 32)) {
         if (nxt) vm_wait<PER + PP::NST + 2 * (WTR / 32)>();
         else vm_wait<PP::NST + 2 * (WTR / 32)>();
+      } else if (nepi == 2 * PP::NST) {
+        if (nxt) vm_wait<PER + 2 * PP::NST>();
+        else vm_wait<2 * PP::NST>();
       } else {
         vm_wait<0>();  // other epilogue shapes (accumulate, 32-pixel partial rows): wait for everything
       }
@@ -1582,6 +1597,22 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         u4 v = {s0[0], s1[0], s0[1], s1[1]};
         const long m = mw + 16 * i + pl;
         const int n = nw + 32 * jp + chq;
+        if (ep.on) {  // eval BN scale / shift + act (+ residual) on the bf16-rounded conv output, as epi_store
+          u4 rv = {0u, 0u, 0u, 0u};
+          if (ep.res != nullptr)
+            rv = __builtin_amdgcn_raw_buffer_load_b128(rr, (m < M && n < g.K) ? (unsigned)((m * ep.rps + n) * 2) : kBufOob, 0, 0);
+          float f[8], r8[8];
+          unpack<bf16>(make_uint4(v[0], v[1], v[2], v[3]), f);
+          unpack<bf16>(make_uint4(rv[0], rv[1], rv[2], rv[3]), r8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int c = n + e < g.K ? n + e : 0;
+            const float sc = ep.scale ? ep.scale[c] : 1.f, sh = ep.shift ? ep.shift[c] : 0.f;
+            f[e] = act_fwd(ep.act, f[e] * sc + sh) + (ep.res != nullptr ? r8[e] : 0.f);
+          }
+          const uint4 o = pack<bf16>(f);
+          v = u4{o.x, o.y, o.z, o.w};
+        }
         const unsigned off = (m < M && n < g.K) ? (unsigned)((m * g.yps + n) * 2) : kBufOob;
         __builtin_amdgcn_raw_buffer_store_b128(v, ry, off, 0, 0);
       }
@@ -3036,17 +3067,27 @@ inline int p1p_mode() {
 // profiles/r03/ab_p1p.log: 256 -> 256 @96^2 fwd 118.7 -> 94.8 us, 128 -> 128 @384^2 636 -> 492 us, 4..23 % on every
 // <= 256-column view; 7..15 % SLOWER on the 512..1280-column views, where the 256 x 256 wide tile reads each input
 // row once)
+// small-M (M < 65536: batch-1 detect) 1x1 forwards on conv_p1p's one-wave 64 x 64 tiles: DMY_P1P_SMALL = 1 (off by
+// default: measured SLOWER -- bs1 DMA-1536 detect conv time 5.87 -> 6.45 ms, profiles/r03/det_layers_p1p_small.log;
+// that run also left the trailing zero-pixel BN partial row of 64-row tiles unwritten, fixed since)
+inline int p1p_small() {
+  static const int t = env_int("DMY_P1P_SMALL", 0);
+  return t;
+}
 inline int p1p_maxn() {
   static const int t = env_int("DMY_P1P_MAXN", 256);
   return t;
 }
 template <bool DG>
 int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-               hipStream_t st, unsigned xbytes, unsigned wbytes) {
+               hipStream_t st, unsigned xbytes, unsigned wbytes, const Epi& ep = Epi{}, bool small = false) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const int nk = gv.C / v3::BK, mode = p1p_mode();
   const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
-  if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || nk < 1 || (mode == 1 && gv.K > p1p_maxn())) return -1;
+  const double rb = ep.res != nullptr ? 2.0 * ((double)(M - 1) * ep.rps + gv.K) : 0.0;
+  if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || rb >= (double)v3::kBufOob || nk < 1 ||
+      (ep.res != nullptr && (ep.rps % 8 != 0 || !aligned16(ep.res))) || (mode == 1 && !small && gv.K > p1p_maxn()))
+    return -1;
   const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
   const int NC = num_cus();
 #define P1P_GO(BM, BN, NS, WTR)                                                                                  \
@@ -3058,8 +3099,12 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
     if (G > ntiles) G = ntiles;                                                                                  \
     else G = G / 8 * 8;                                                                                          \
     v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
-                                                                      wbytes, (unsigned)yb, nprow);              \
+                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb); \
     return (int)hipGetLastError();                                                                               \
+  }
+  if (small) {  // small M (batch-1 inference): one-wave 64 x 64 tiles, several blocks per CU, the short K ring
+    if (nk >= 2) P1P_GO(64, 64, 3, 64)
+    P1P_GO(64, 64, 2, 64)
   }
   if (mode == 3 && gv.K > 64) P1P_GO(128, 128, 2, 64)
   if (mode == 2 && gv.K >= 256) P1P_GO(256, 256, 2, 128)
@@ -3102,8 +3147,8 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
   }
-  if (p1 && buf && p1p_mode() && tov < 0 && !ep.on && bb.z == nullptr) {  // persistent 1x1, register epilogue
-    const int r = launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes);
+  if (p1 && buf && p1p_mode() && tov < 0 && bb.z == nullptr && !ep.on) {  // persistent 1x1, register epilogue
+    const int r = launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes, ep);
     if (r >= 0) return r;
   }
   if (p1 && buf && p1_persist_mode() && tov < 0) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
@@ -3249,6 +3294,17 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
+    // small-M 1x1 layers (batch-1 inference: M < 65536): the register-epilogue GEMM on one-wave 64 x 64 tiles
+    if (M < 65536 && M >= 64 && p1p_small() && g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0 && g.C % 64 == 0 &&
+        g.xps % 8 == 0 && g.yps % 8 == 0 && g.K % 8 == 0 && g.K >= 32 && aligned16(x) && aligned16(w) &&
+        aligned16(y) && conv_buf_mode()) {
+      const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.C;
+      if (xb < (double)v3::kBufOob && wb < (double)v3::kBufOob) {
+        const int r = launch_p1p<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, (unsigned)xb,
+                                        (unsigned)wb, ep, true);
+        if (r >= 0) return r;
+      }
+    }
     if (ws != nullptr && ps == nullptr && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res)))) {
       const long need = splitk_elems(g, x, w, y);
       if (need > 0 && need <= ws_elems) return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);

@@ -29,6 +29,18 @@ for part in ${PARTS:-p1ptest p1pab fp8 diag}; do
     diag)
       DIAG_ALL=0 timeout -k 10 300 python -u tools/gpu/diag_precision.py yolov5s.yaml 640 16 > gpurun_out/diag_prec_v5s_b.log 2>&1
       rc=$?; echo "diag rc=$rc"; grep -v amdgpu gpurun_out/diag_prec_v5s_b.log | head -12;;
+    convtests)
+      timeout -k 10 500 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_modules.py tests/test_gpu_model.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/conv_tests.log 2>&1
+      rc=$?; echo "convtests rc=$rc"; tail -2 gpurun_out/conv_tests.log; grep -E "^FAILED" gpurun_out/conv_tests.log | head -20;;
+    det)
+      timeout -k 10 300 python tools/gpu/det_layers.py dma-1536 5 > gpurun_out/det_layers_r3.log 2>&1
+      rc=$?; echo "det rc=$rc"; grep -v amdgpu gpurun_out/det_layers_r3.log | head -40;;
+    c5)
+      for a in "" "--fp8"; do
+        timeout -k 10 400 python bench.py --config c5-1920 --also none --steps 10 --warmup 3 --no-cpu-baseline $a > gpurun_out/bench_c5${a}_r3.log 2> gpurun_out/bench_c5${a}_r3.err
+        rc=$?; echo "c5 $a rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/bench_c5${a}_r3.err; break; }
+        python -c "import json,sys; d=json.loads(open('gpurun_out/bench_c5${a}_r3.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d.get('detect_p50_ms'))"
+      done;;
     bench)
       timeout -k 10 600 python bench.py --steps ${STEPS:-10} --warmup 3 ${BENCHARGS} > gpurun_out/bench_$TAG.log 2> gpurun_out/bench_$TAG.err
       rc=$?; echo "bench rc=$rc"; tail -c 600 gpurun_out/bench_$TAG.log;;
