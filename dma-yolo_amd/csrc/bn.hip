@@ -109,7 +109,9 @@ struct RowMap {
 };
 
 // -------- y = act(z * scale + shift) (+ res)
-template <typename T>
+// U rows per thread and iteration, all loads issued before the arithmetic: U x 16 B (x2 with a residual) in flight
+// per lane, where one row per iteration left the streaming kernels at 4.6-5.4 TB/s
+template <typename T, int U = 1>
 __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, long zps, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, int act, const T* __restrict__ res,
                                                       long rps, T* __restrict__ y, long yps, long M, int C) {
@@ -120,19 +122,34 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
   float sc[VW], sh[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
-  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
-    float f[VW];
-    unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), f);
-    if (res) {
-      float r[VW];
-      unpack<T>(*reinterpret_cast<const uint4*>(res + m * rps + c0), r);
+  const long S = (long)gridDim.x * rm.RB;
+  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {
+    uint4 zv[U], rv[U];
 #pragma unroll
-      for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+    for (int u = 0; u < U; ++u) {
+      const long mu = m + u * S;
+      if (mu < M) {
+        zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
+        if (res) rv[u] = *reinterpret_cast<const uint4*>(res + mu * rps + c0);
+      }
     }
-    *reinterpret_cast<uint4*>(y + m * yps + c0) = pack<T>(f);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long mu = m + u * S;
+      if (mu >= M) break;
+      float f[VW];
+      unpack<T>(zv[u], f);
+      if (res) {
+        float r[VW];
+        unpack<T>(rv[u], r);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+      }
+      *reinterpret_cast<uint4*>(y + mu * yps + c0) = pack<T>(f);
+    }
   }
 }
 
@@ -212,7 +229,7 @@ __global__ void bn_act_fwd_scalar(const T* __restrict__ z, long zps, const float
 
 // -------- backward reduce: per channel  sum(du), sum(du * xhat), du = dy * act'(u)
 // also used (dy = z, act none, scale 1, shift 0, mean 0, invstd 1) as plain column sums
-template <typename T, bool STATS>
+template <typename T, bool STATS, int U = 1>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z, long zps, const T* __restrict__ dy,
                                                          long dps, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, const float* __restrict__ mean,
@@ -234,19 +251,33 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
       mu[j] = STATS ? 0.f : mean[c0 + j];
       is[j] = STATS ? 1.f : invstd[c0 + j];
     }
-    for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
-      float zf[VW], gf[VW];
-      unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
-      unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
+    const long S = (long)gridDim.x * rm.RB;
+    for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {
+      uint4 zv[U], gv[U];
 #pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        if (STATS) {  // plain column sums of z and z^2 (batch statistics / bias gradients)
-          a[j] += zf[j];
-          b[j] += zf[j] * zf[j];
-        } else {
-          const float du = gf[j] * act_grad(act, zf[j] * sc[j] + sh[j]);
-          a[j] += du;
-          b[j] += du * (zf[j] - mu[j]) * is[j];
+      for (int u = 0; u < U; ++u) {
+        const long mu = m + u * S;
+        if (mu < M) {
+          zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
+          if (!STATS) gv[u] = *reinterpret_cast<const uint4*>(dy + mu * dps + c0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // rows summed in the same order as one row per iteration
+        if (m + u * S >= M) break;
+        float zf[VW], gf[VW];
+        unpack<T>(zv[u], zf);
+        if (!STATS) unpack<T>(gv[u], gf);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          if (STATS) {  // plain column sums of z and z^2 (batch statistics / bias gradients)
+            a[j] += zf[j];
+            b[j] += zf[j] * zf[j];
+          } else {
+            const float du = gf[j] * act_grad(act, zf[j] * sc[j] + sh[j]);
+            a[j] += du;
+            b[j] += du * (zf[j] - mu[j]) * is[j];
+          }
         }
       }
     }
@@ -272,7 +303,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
 }
 
 // dz = ca*du + cb + cc*xhat   (train);  eval: cb = cc = 0, ca = scale
-template <typename T>
+template <typename T, int U = 1>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z, long zps, const T* __restrict__ dy,
                                                         long dps, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const float* __restrict__ mean,
@@ -294,13 +325,28 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z,
     k2[j] = cc[c0 + j] * invstd[c0 + j];
     k0[j] = cb[c0 + j] - k2[j] * mean[c0 + j];
   }
-  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
-    float zf[VW], gf[VW], o[VW];
-    unpack<T>(*reinterpret_cast<const uint4*>(z + m * zps + c0), zf);
-    unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c0), gf);
+  const long S = (long)gridDim.x * rm.RB;
+  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {
+    uint4 zv[U], gv[U];
 #pragma unroll
-    for (int j = 0; j < VW; ++j) o[j] = k1[j] * (gf[j] * act_grad(act, zf[j] * sc[j] + sh[j])) + k0[j] + k2[j] * zf[j];
-    *reinterpret_cast<uint4*>(dz + m * dzps + c0) = pack<T>(o);
+    for (int u = 0; u < U; ++u) {
+      const long mu = m + u * S;
+      if (mu < M) {
+        zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
+        gv[u] = *reinterpret_cast<const uint4*>(dy + mu * dps + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long mu = m + u * S;
+      if (mu >= M) break;
+      float zf[VW], gf[VW], o[VW];
+      unpack<T>(zv[u], zf);
+      unpack<T>(gv[u], gf);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) o[j] = k1[j] * (gf[j] * act_grad(act, zf[j] * sc[j] + sh[j])) + k0[j] + k2[j] * zf[j];
+      *reinterpret_cast<uint4*>(dz + mu * dzps + c0) = pack<T>(o);
+    }
   }
 }
 
@@ -420,10 +466,27 @@ inline bool vec_ok(int VW, int C, long s1, long s2, long s3, const void* p1, con
 
 }  // namespace
 
-inline int vec_grid(long M, int C, int VW) {
-  const int RB = 256 / (C / VW);
-  return grid_cap(ceil_div(M, (long)RB * 8), 4096);
+inline int env_knob(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
+// rows per thread and loop iteration of the bf16 streaming kernels (DMY_BN_UNROLL: 1, 2 or 4) and the grid cap
+// (DMY_BN_GRID blocks of 256 threads)
+inline int bn_unroll() {
+  static const int u = env_knob("DMY_BN_UNROLL", 1);
+  return u;
+}
+inline int vec_grid(long M, int C, int VW) {
+  static const int cap = env_knob("DMY_BN_GRID", 4096);
+  const int RB = 256 / (C / VW);
+  return grid_cap(ceil_div(M, (long)RB * 8), cap);
+}
+#define BN_UNROLL(KERNEL, ...)                                   \
+  switch (bn_unroll()) {                                         \
+    case 4: KERNEL(4, __VA_ARGS__); break;                       \
+    case 2: KERNEL(2, __VA_ARGS__); break;                       \
+    default: KERNEL(1, __VA_ARGS__); break;                      \
+  }
 
 DMY_API int dmy_bn_partial_rows(long M) {
   long p = (M + 255) / 256;
@@ -469,7 +532,9 @@ DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scal
   const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res) && C / VW <= 256;
   if (vec) {
     const int g = vec_grid(M, C, VW);
-    if (dtype) bn_act_fwd_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
+#define ACT_GO(U_, ...) bn_act_fwd_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C)
+    if (dtype) { BN_UNROLL(ACT_GO, 0) }
+#undef ACT_GO
     else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);
@@ -506,7 +571,9 @@ DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, 0, z, dy, nullptr) && C / VW <= 256) {
     const int g = vec_grid(M, C, VW);
-    if (dtype) bn_bwd_reduce_vec<bf16, false><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg);
+#define RED_GO(U_, ...) bn_bwd_reduce_vec<bf16, false, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg)
+    if (dtype) { BN_UNROLL(RED_GO, 0) }
+#undef RED_GO
     else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg);
     return (int)hipGetLastError();
   }
@@ -545,7 +612,9 @@ DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy,
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, dzps, z, dy, dz) && C / VW <= 256) {
     const int g = vec_grid(M, C, VW);
-    if (dtype) bn_bwd_apply_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);
+#define APP_GO(U_, ...) bn_bwd_apply_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C)
+    if (dtype) { BN_UNROLL(APP_GO, 0) }
+#undef APP_GO
     else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);

@@ -1912,6 +1912,118 @@ __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1
   }
 }
 
+// ---------------------------------------------------------------- small-M inference GEMM (conv_sk)
+// Batch-1 eval forwards (M = 2,304 .. 147,456 output pixels) are latency-bound: on the 256-row LDS-DMA tiles a 1x1
+// 96^2 256 -> 256 layer (4.7 MB in, 4.7 MB out) took 25-35 us of GPU time for ~2 us of HBM traffic.  Here a block is
+// 4 waves x 16 output pixels x BN channels: the X fragments of a wave's 16 pixels go from HBM straight into registers
+// (16-B buffer loads; a k x k gather with the tap's range check for 3x3 / strided layers, zeros past the reduction),
+// the block's BN x KC slice of W is LDS-DMA'd into the swizzled 128-B-row image of the v3 kernels, double-buffered over
+// KC-deep chunks (one chunk = the whole reduction of a <= KC-channel 1x1 layer: one memory round trip), and the MFMA runs
+// transposed (D[ch][px] = W X^T) so a lane ends with 4 consecutive channels of one pixel: a permlane16 swap pairs two
+// 16-channel blocks into 8 consecutive channels, and the inference epilogue (bias, bf16 rounding, eval-BN scale /
+// shift, activation, residual) is applied in registers before one 16-B store -- the value contract of the other paths
+// (conv output rounded to bf16, then the epilogue in fp32).  Grid = (M / 64) x (K / BN) blocks, XCD-contiguous.
+template <int BN, int KC>
+__global__ void __launch_bounds__(256) conv_sk(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                               const float* __restrict__ bias, bf16* __restrict__ y, Geom g, Epi ep,
+                                               int gm, int gn, unsigned xbytes, unsigned wbytes) {
+  constexpr int NCB = BN / 16, KS = KC / 32, SUB = KC / 64;
+  constexpr int CHUNK = BN * KC * 2, PIECES = CHUNK / 1024 / 4;  // 1-KiB LDS-DMA pieces per wave per chunk
+  static_assert(PIECES * 4 * 1024 == CHUNK && NCB % 2 == 0, "conv_sk tile");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * CHUNK];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, pl = lane & 15, q = lane >> 4;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const int Ktot = g.KH * g.KW * g.C, n0 = tn * BN, nch = (Ktot + KC - 1) / KC;
+  const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rw = make_rsrc(w, wbytes);
+  // this lane's pixel (X fragments: B operand column pl, k chunk q)
+  const long m = (long)tm * 64 + wid * 16 + pl;
+  const bool mv = m < M;
+  const int mm = mv ? (int)m : 0, ow = mm % g.OW, oh = (mm / g.OW) % g.OH, bi = mm / (g.OW * g.OH);
+  const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
+  // W pieces: piece pi = wid * PIECES + j covers sub-block pi / (BN / 8), rows (pi % (BN / 8)) * 8 + lane / 8; the lane
+  // reads the logical 16-B chunk (lane & 7) ^ (row & 6) of its row (frag_sw's swizzle on a lane-linear image)
+  const int wl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
+  auto issue = [&](int ck, char* buf, bf16x8 (&xr)[KS]) {
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      const int pi = wid * PIECES + j, sb = pi / (BN / 8), row = (pi % (BN / 8)) * 8 + (lane >> 3);
+      const int k = ck * KC + sb * 64 + wl, n = n0 + row;
+      blds16(rw, (n < g.K && k < Ktot) ? (unsigned)(n * Ktot + k) * 2u : kBufOob, buf + pi * 1024);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ck * KC + ks * 32 + q * 8;
+      unsigned off = kBufOob;
+      if (mv && k < Ktot) {
+        if (p1) {
+          off = (unsigned)(m * g.xps + k) * 2u;
+        } else {
+          const int tap = k / g.C, c = k - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int ih = ih0 + kh, iw = iw0 + kw;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            off = (unsigned)(((bi * g.H + ih) * g.W + iw) * (int)g.xps + c) * 2u;
+        }
+      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+      xr[ks] = *reinterpret_cast<const bf16x8*>(&v);
+    }
+  };
+  f32x4 acc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 xc[KS], xn[KS];
+  issue(0, smem, xc);
+  for (int ck = 0; ck < nch; ++ck) {
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();  // chunk ck's W image complete; every wave is done with the other buffer
+    if (ck + 1 < nch) issue(ck + 1, smem + ((ck + 1) & 1) * CHUNK, xn);
+    const bf16* ws = reinterpret_cast<const bf16*>(smem + (ck & 1) * CHUNK);
+    const int kv = Ktot - ck * KC;  // live k in this chunk (zero-filled past it: skip those MFMAs)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks * 32 >= kv) break;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const bf16x8 wf = frag_sw(ws + (ks >> 1) * BN * 64, cb * 16, (ks & 1) * 32, lane);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xc[ks], acc[cb], 0, 0, 0);
+      }
+    }
+    if (ck + 1 < nch) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xc[ks] = xn[ks];
+    }
+  }
+  // epilogue: lane holds channels n0 + cb * 16 + q * 4 + r of pixel m
+  const int chq = (q & 1) * 16 + (q >> 1) * 8;
+#pragma unroll
+  for (int pr = 0; pr < NCB / 2; ++pr) {
+    f32x4 a = acc[2 * pr], b = acc[2 * pr + 1];
+    const int nb = n0 + pr * 32;
+    if (bias != nullptr && nb < g.K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] += bias[nb + q * 4 + r];
+        b[r] += bias[nb + 16 + q * 4 + r];
+      }
+    }
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
+    uint4 v;
+    v.x = s0[0];
+    v.y = s1[0];
+    v.z = s0[1];
+    v.w = s1[1];
+    const int n = nb + chq;  // 8 consecutive channels
+    if (mv && nb < g.K) {
+      if (ep.on) epi_store<bf16, 8>(ep, reinterpret_cast<const bf16*>(&v), y + m * g.yps + n, n, g.K, m, true);
+      else *reinterpret_cast<uint4*>(y + m * g.yps + n) = v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- split-K forward for small M (batch-1 inference)
 // At batch 1 the stride-16 / -32 layers have 2304..9216 output pixels: 128-row tiles give 18..72 row tiles, a
 // fraction of the 256 CUs, each walking the whole 9 * C reduction.  Split the K steps over blockIdx.y: every split
@@ -3289,11 +3401,47 @@ inline int fill_tile(const Geom& g, const void* x, const void* w, const void* y,
   return ceil_div(M, 128) * ceil_div(g.K, 128) >= NC ? 2 : 4;
 }
 
+// small-M inference GEMM (v3::conv_sk): DMY_SK = 0 off, 1 (default) eval forwards without BN partials with M <= DMY_SK_MAXM
+// output pixels (batch-1 detect), channel counts multiples of 32
+inline int sk_mode() {
+  static const int t = env_int("DMY_SK", 1);
+  return t;
+}
+inline bool sk_ok(const Geom& g, const void* x, const void* w, const void* y, const float* ps, const Epi& ep) {
+  static const long maxm = env_int("DMY_SK_MAXM", 65536);
+  const long M = (long)g.N * g.OH * g.OW;
+  if (!sk_mode() || ps != nullptr || M == 0 || M > maxm || g.C % 32 != 0 || g.K % 32 != 0 || g.xps % 8 != 0 ||
+      g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y) || (ep.res && (ep.rps % 8 != 0 || !aligned16(ep.res))))
+    return false;
+  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
+  return xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
+}
+inline int launch_sk(const bf16* x, const bf16* w, const float* b, bf16* y, const Geom& g, hipStream_t st, const Epi& ep) {
+  const long M = (long)g.N * g.OH * g.OW;
+  const int Ktot = g.KH * g.KW * g.C, gm = (int)ceil_div(M, 64);
+  const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * Ktot);
+#define SK_GO(BN_, KC_)                                                                                            \
+  {                                                                                                                \
+    const int gn = ceil_div(g.K, BN_);                                                                             \
+    v3::conv_sk<BN_, KC_><<<(unsigned)gm * gn, 256, 0, st>>>(x, w, b, y, g, ep, gm, gn, xb, wb);                   \
+    return (int)hipGetLastError();                                                                                 \
+  }
+  if (g.K >= 128) {
+    if (Ktot <= 128) SK_GO(128, 128)
+    SK_GO(128, 256)
+  }
+  if (Ktot <= 128) SK_GO(64, 128)
+  SK_GO(64, 256)
+#undef SK_GO
+}
+
 template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
+    if (conv_buf_mode() && sk_ok(g, x, w, y, ps, ep))
+      return launch_sk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, st, ep);
     // small-M 1x1 layers (batch-1 inference: M < 65536): the register-epilogue GEMM on one-wave 64 x 64 tiles
     if (M < 65536 && M >= 64 && p1p_small() && g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0 && g.C % 64 == 0 &&
         g.xps % 8 == 0 && g.yps % 8 == 0 && g.K % 8 == 0 && g.K >= 32 && aligned16(x) && aligned16(w) &&

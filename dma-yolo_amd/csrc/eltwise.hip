@@ -647,34 +647,28 @@ __global__ void __launch_bounds__(256) cbam_in_fwd_kernel(const T* __restrict__ 
 }
 
 // backward: d_out1 total = d_out1 + d_mean / C + [c == am] d_max;  dx = total * ca;
-// dca[n][c] += sum over this wave's pixels of total * x  (fp32 atomics once per wave and channel)
+// wave w takes pixels [(w % wpi) * ppw, +ppw) of image w / wpi and writes its partial sum over them of total * x to
+// part[w][c]; cbam_fold_kernel adds an image's wpi partials in wave order (deterministic, no float atomics)
 template <typename T, int NV>
 __global__ void __launch_bounds__(256) cbam_in_bwd_kernel(const T* __restrict__ x, long xps, const T* __restrict__ ca,
                                                           const T* __restrict__ dout1, long dps, const T* __restrict__ ds2,
                                                           const int* __restrict__ am, int N, int HW, int C, int ppw,
-                                                          T* __restrict__ dx, long dxps, int accumulate,
-                                                          float* __restrict__ dca) {
+                                                          int wpi, T* __restrict__ dx, long dxps, int accumulate,
+                                                          float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
-  const long P = (long)N * HW;
   const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
-  const long p0 = w * ppw;
-  if (p0 >= P) return;
-  const long p1 = min(P, p0 + ppw);
+  if (w >= (long)N * wpi) return;
+  const int n = (int)(w / wpi);
+  const long p0 = (long)n * HW + (w % wpi) * (long)ppw;
+  const long p1 = min((long)(n + 1) * HW, p0 + ppw);
   for (int c0 = lane * NV; c0 < C; c0 += 64 * NV) {
-    float acc[NV];
+    float acc[NV], cv[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) acc[j] = 0.f;
-    int n = (int)(p0 / HW);
+    ldv<T, NV>(ca + (long)n * C + c0, cv);
     for (long pix = p0; pix < p1; ++pix) {
-      const int pn = (int)(pix / HW);
-      if (pn != n) {  // image boundary inside this wave's run: flush
-#pragma unroll
-        for (int j = 0; j < NV; ++j) { atomicAdd(dca + (long)n * C + c0 + j, acc[j]); acc[j] = 0.f; }
-        n = pn;
-      }
-      float xv[NV], cv[NV], gv[NV];
+      float xv[NV], gv[NV];
       ldv<T, NV>(x + pix * xps + c0, xv);
-      ldv<T, NV>(ca + (long)n * C + c0, cv);
       ldv<T, NV>(dout1 + pix * dps + c0, gv);
       const float gm = to_f(ds2[pix * 2]) / C, gx = to_f(ds2[pix * 2 + 1]);
       const int a = am[pix];
@@ -689,7 +683,18 @@ __global__ void __launch_bounds__(256) cbam_in_bwd_kernel(const T* __restrict__ 
       stv<T, NV>(dx + pix * dxps + c0, o);
     }
 #pragma unroll
-    for (int j = 0; j < NV; ++j) atomicAdd(dca + (long)n * C + c0 + j, acc[j]);
+    for (int j = 0; j < NV; ++j) part[w * C + c0 + j] = acc[j];
+  }
+}
+
+__global__ void cbam_fold_kernel(const float* __restrict__ part, int N, int C, int wpi, float* __restrict__ dca) {
+  const long total = (long)N * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / C), c = (int)(i % C);
+    const float* q = part + (long)n * wpi * C + c;
+    float s = 0.f;
+    for (int j = 0; j < wpi; ++j) s += q[(long)j * C];
+    dca[i] = s;
   }
 }
 
@@ -1242,15 +1247,19 @@ DMY_API int dmy_cbam_in_fwd(int dtype, const void* x, long xps, const void* ca, 
   DISPATCH_TV(dtype, v, cbam_in_fwd_kernel<T, NV><<<grid_cap(ceil_div((long)N * HW, 4), 8192), 256, 0, st>>>((const T*)x, xps, (const T*)ca, N, HW, C, (T*)out1, (T*)s2, am));
   return (int)hipGetLastError();
 }
+static const int kCbamPpw = 64;  // pixels per wave of cbam_in_bwd_kernel
+DMY_API long dmy_cbam_in_bwd_ws_elems(int N, int HW, int C) {
+  return (long)N * ceil_div((long)HW, kCbamPpw) * C;
+}
 DMY_API int dmy_cbam_in_bwd(int dtype, const void* x, long xps, const void* ca, const void* dout1, long dps,
                             const void* ds2, const int* am, int N, int HW, int C, void* dx, long dxps, int accumulate,
-                            float* dca, void* stream) {
+                            float* dca, float* ws, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(dtype, {C, xps, dps, dxps}, {x, ca, dout1, dx});
-  const int ppw = 64;
-  const long waves = ceil_div((long)N * HW, ppw);
-  (void)hipMemsetAsync(dca, 0, sizeof(float) * (size_t)N * C, st);
-  DISPATCH_TV(dtype, v, cbam_in_bwd_kernel<T, NV><<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>((const T*)x, xps, (const T*)ca, (const T*)dout1, dps, (const T*)ds2, am, N, HW, C, ppw, (T*)dx, dxps, accumulate, dca));
+  const int wpi = (int)ceil_div((long)HW, kCbamPpw);
+  const long waves = (long)N * wpi;
+  DISPATCH_TV(dtype, v, cbam_in_bwd_kernel<T, NV><<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>((const T*)x, xps, (const T*)ca, (const T*)dout1, dps, (const T*)ds2, am, N, HW, C, kCbamPpw, wpi, (T*)dx, dxps, accumulate, ws));
+  cbam_fold_kernel<<<grid_cap(ceil_div((long)N * C, 256)), 256, 0, st>>>(ws, N, C, wpi, dca);
   return (int)hipGetLastError();
 }
 DMY_API int dmy_pixscale(int dtype, const void* out1, const void* sa, long sps, int N, int HW, int C, void* out, long ops,

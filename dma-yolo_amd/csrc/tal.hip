@@ -285,10 +285,27 @@ __global__ void tal_resolve_kernel(const T* __restrict__ cls, long scb, long scc
   }
 }
 
+// a 256-thread block's sums of V values, written to part[blockIdx.x * V + v]: waves combined in wave order
+template <int V>
+__device__ void block_partials(float* v, float* __restrict__ part) {
+  __shared__ float red[4][V];
+  const int wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const float t = wave_sum(v[k]);
+    if ((threadIdx.x & 63) == 0) red[wv][k] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < V) {
+    const int k = threadIdx.x;
+    part[(long)blockIdx.x * V + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+  }
+}
+
 // norm per anchor + tss
 __global__ void tal_norm_kernel(const int* __restrict__ owner, const float* __restrict__ metric,
                                 const int* __restrict__ amax_m, const int* __restrict__ amax_o, int B, int A, int cap,
-                                float* __restrict__ norm, float* __restrict__ acc) {
+                                float* __restrict__ norm, float* __restrict__ part) {
   const long n = (long)B * A;
   float s = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -301,8 +318,25 @@ __global__ void tal_norm_kernel(const int* __restrict__ owner, const float* __re
     norm[i] = v;
     s += v;
   }
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) atomicAdd(acc + 3, s);
+  block_partials<1>(&s, part);
+}
+
+// acc[a0 + v] = sum over blocks b < nb of part[b * V + v], in block order (one 256-thread block; fixed tree)
+template <int V>
+__global__ void tal_fold_kernel(const float* __restrict__ part, int nb, float* __restrict__ acc, int a0) {
+  __shared__ float red[256];
+  for (int k = 0; k < V; ++k) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < nb; b += 256) s += part[(long)b * V + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) acc[a0 + k] = red[0];
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- losses + gradients
@@ -312,7 +346,7 @@ template <typename T>
 __global__ void tal_loss_kernel(const T* __restrict__ box, long sbb, long sbc, long sba, const T* __restrict__ cls,
                                 long scb, long scc, long sca, const float* __restrict__ gt, const int* __restrict__ owner,
                                 const float* __restrict__ norm, int B, int A, int nc, int cap, LevelTab lt, float pw,
-                                float* __restrict__ acc, float* __restrict__ G) {
+                                const float* __restrict__ acc, float* __restrict__ part, float* __restrict__ G) {
   const long n = (long)B * A;
   const float tss = acc[3];
   const float kb = 7.5f * B / tss, kc = 0.5f * B / tss, kd = 1.5f * B / tss;
@@ -370,14 +404,8 @@ __global__ void tal_loss_kernel(const T* __restrict__ box, long sbb, long sbc, l
     }
     ld += dsum * 0.25f * w;
   }
-  lb = wave_sum(lb);
-  lc = wave_sum(lc);
-  ld = wave_sum(ld);
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(acc + 0, lb);
-    atomicAdd(acc + 1, lc);
-    atomicAdd(acc + 2, ld);
-  }
+  float v[3] = {lb, lc, ld};
+  block_partials<3>(v, part);
 }
 
 __global__ void tal_finalize_kernel(const float* __restrict__ acc, float bs, float* __restrict__ loss,
@@ -457,9 +485,9 @@ inline int egrid(long n) { return grid_cap(ceil_div(n, 256), 8192); }
 
 DMY_API long dmy_tal_workspace_bytes(int B, int A, int cap) {
   // gt[B][cap][5] f32, cnt[B] i32, cand[B][cap][10] i32, nclaim/owner [B][A] i32, metric/norm [B][A] f32,
-  // amax_m/amax_o [B][cap] i32, pbox [B][A][4] f32, acc[4] f32
+  // amax_m/amax_o [B][cap] i32, pbox [B][A][4] f32, acc[4] f32, per-block loss partials [8192][4] f32
   const long b = 4L * ((long)B * cap * 5 + B + (long)B * cap * TOPK + 2L * B * A + 2L * B * A + 2L * B * cap +
-                       4L * B * A + 4) + 16 * 256;  // + per-buffer 256-B alignment
+                       4L * B * A + 4 + 4L * 8192) + 16 * 256;  // + per-buffer 256-B alignment
   return b > 0x7fffffffL ? -1 : (int)b;
 }
 
@@ -487,6 +515,7 @@ DMY_API int dmy_tal_loss(int dtype, const void* box, long sbb, long sbc, long sb
   int* amax_o = (int*)take(4L * B * cap);
   float* pbox = (float*)take(16L * B * A);
   float* acc = (float*)take(16);
+  float* part = (float*)take(16L * 8192);  // egrid() caps the grid at 8192 blocks
   (void)hipMemsetAsync(nclaim, 0, 4L * B * A, st);
   (void)hipMemsetAsync(owner, 0xff, 4L * B * A, st);
   (void)hipMemsetAsync(amax_m, 0, 4L * B * cap, st);
@@ -503,9 +532,13 @@ DMY_API int dmy_tal_loss(int dtype, const void* box, long sbb, long sbc, long sb
     tal_claim_kernel<<<egrid((long)B * cap * TOPK), 256, 0, st>>>(cand, cnt, B, A, cap, nclaim, owner);
     tal_resolve_kernel<T><<<egrid((long)B * A), 256, 0, st>>>(cl, scb, scc, sca, pbox, gt, cnt, nclaim, owner, B, A, cap,
                                                               lt, alpha, beta, metric, amax_m, amax_o);
-    tal_norm_kernel<<<egrid((long)B * A), 256, 0, st>>>(owner, metric, amax_m, amax_o, B, A, cap, norm, acc);
-    tal_loss_kernel<T><<<egrid((long)B * A), 256, 0, st>>>(bx, sbb, sbc, sba, cl, scb, scc, sca, gt, owner, norm, B, A,
-                                                           nc, cap, lt, pos_weight, acc, G);
+    // loss sums: per-block partials folded in block order (deterministic, no float atomics)
+    const int nb = egrid((long)B * A);
+    tal_norm_kernel<<<nb, 256, 0, st>>>(owner, metric, amax_m, amax_o, B, A, cap, norm, part);
+    tal_fold_kernel<1><<<1, 256, 0, st>>>(part, nb, acc, 3);
+    tal_loss_kernel<T><<<nb, 256, 0, st>>>(bx, sbb, sbc, sba, cl, scb, scc, sca, gt, owner, norm, B, A, nc, cap, lt,
+                                           pos_weight, acc, part, G);
+    tal_fold_kernel<3><<<1, 256, 0, st>>>(part, nb, acc, 0);
   });
   tal_finalize_kernel<<<1, 1, 0, st>>>(acc, (float)B, loss, items);
   return (int)hipGetLastError();

@@ -101,7 +101,8 @@ SIGNATURES = {
     'dmy_gpool_bwd': [I, P, P, P, L, I, I, I, I, P],
     'dmy_halves_sigmoid': [I, P, I, I, P, P, P, P],
     'dmy_cbam_in_fwd': [I, P, L, P, I, I, I, P, P, P, P],
-    'dmy_cbam_in_bwd': [I, P, L, P, P, L, P, P, I, I, I, P, L, I, P, P],
+    'dmy_cbam_in_bwd_ws_elems': [I, I, I],
+    'dmy_cbam_in_bwd': [I, P, L, P, P, L, P, P, I, I, I, P, L, I, P, P, P],
     'dmy_pixscale': [I, P, P, L, I, I, I, P, L, P, L, P, P, P],
     # mha.hip
     'dmy_mha_fwd': [I, P, L, P, L, P, L, P, L, P, I, I, I, I, F, P],

@@ -1392,8 +1392,9 @@ class CBAMInFn(torch.autograd.Function):
             ds2.contiguous(memory_format=CL)
         buf, bps, acc = sink_target(ctx.sink, N, C, H, W, x)
         dca = f32(N * C, x.device)
+        ws = f32(call('dmy_cbam_in_bwd_ws_elems', N, H * W, C), x.device)  # per-wave partials, folded in order
         call('dmy_cbam_in_bwd', dcode(x), ptr(x), ctx.xps, ptr(ca), ptr(dout1), dps, ptr(ds2), ptr(am), N, H * W, C,
-             ptr(buf), bps, acc, ptr(dca), stream())
+             ptr(buf), bps, acc, ptr(dca), ptr(ws), stream())
         return sink_result(ctx.sink, buf), dca.view(N, C, 1, 1).to(ca.dtype), None
 
 

@@ -275,8 +275,10 @@ int dmy_gpool_bwd(int dtype, const void* dz, const int* arg, void* dx, long dxps
 int dmy_halves_sigmoid(int dtype, const void* z, int N, int C, void* ca, const void* dca, void* dz, void* stream);
 int dmy_cbam_in_fwd(int dtype, const void* x, long xps, const void* ca, int N, int HW, int C, void* out1, void* s2,
                     int* am, void* stream);
+long dmy_cbam_in_bwd_ws_elems(int N, int HW, int C);
 int dmy_cbam_in_bwd(int dtype, const void* x, long xps, const void* ca, const void* dout1, long dps, const void* ds2,
-                    const int* am, int N, int HW, int C, void* dx, long dxps, int accumulate, float* dca, void* stream);
+                    const int* am, int N, int HW, int C, void* dx, long dxps, int accumulate, float* dca, float* ws,
+                    void* stream);
 int dmy_pixscale(int dtype, const void* out1, const void* sa, long sps, int N, int HW, int C, void* out, long ops,
                  const void* dout, long dps, void* dout1, void* dsa, void* stream);
 

@@ -193,3 +193,46 @@ def test_conv_fwd_fill_tiles_vs_torch(N, C, H, W, K, k, s, res):
         z = z + r.float()
     assert _rel(y.float(), z) < 1e-2
     assert torch.equal(yb[:, K:].float().cpu(), torch.full((N, 64, OH, OW), 7.0)), 'columns past K must stay untouched'
+
+
+# small-M eval forwards on the register-epilogue GEMM (v3::conv_sk, M <= 65536, channels % 32): 1x1 with one and several
+# KC chunks, 3x3 stride 1 / 2 gathers with a partial last chunk, channel tiles past K (K % BN != 0), C % 64 != 0,
+# M not a multiple of 64, bias + eval-BN + SiLU + residual, output into a concat-buffer slice
+SK_SHAPES = [(1, 256, 96, 96, 256, 1, 1, True), (1, 1024, 48, 48, 1024, 1, 1, False), (1, 64, 97, 95, 64, 3, 1, True),
+             (1, 128, 61, 59, 256, 3, 2, False), (2, 96, 33, 35, 96, 3, 1, True), (1, 32, 70, 66, 32, 1, 1, False),
+             (1, 512, 24, 26, 160, 3, 1, True), (3, 192, 21, 23, 352, 1, 1, True), (1, 2048, 12, 12, 512, 1, 1, False)]
+
+
+@pytest.mark.parametrize('N,C,H,W,K,k,s,res', SK_SHAPES)
+def test_conv_fwd_small_m_sk_vs_torch(N, C, H, W, K, k, s, res):
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    from dmayolo._lib import ACT_SILU
+    g = torch.Generator().manual_seed(N * 31 + C + 3 * K + k + int(res))
+    p = k // 2
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    w = torch.randn(K, C, k, k, generator=g) / (C * k * k) ** 0.5
+    b = torch.randn(K, generator=g) * 0.1
+    ref = F.conv2d(x.float().cuda(), w.bfloat16().float().cuda(), b.cuda(), stride=s, padding=p)
+    OH, OW = ref.shape[2:]
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    wf, _ = prep_weight(w.cuda(), torch.bfloat16, False)
+    Kt = K + 32
+    yb = torch.full((N, Kt, OH, OW), 7.0, dtype=torch.bfloat16, device='cuda').contiguous(
+        memory_format=torch.channels_last)
+    y = yb[:, :K]
+    sc = (torch.rand(K, generator=g) + 0.5).cuda()
+    sh = (torch.randn(K, generator=g) * 0.2).cuda()
+    r = torch.randn(N, K, OH, OW, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last) \
+        if res else None
+    rc = call('dmy_conv_fwd_act', 1, ptr(xd), ptr(wf), ptr(b.cuda()), ptr(y), N, H, W, C, C, K, k, k, s, p, OH, OW, Kt,
+              ptr(sc), ptr(sh), ACT_SILU, ptr(r), K if res else 0, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    z = F.silu(ref.bfloat16().float() * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1))
+    if res:
+        z = z + r.float()
+    assert _rel(y.float(), z) < 1e-2
+    # elementwise: within 2 bf16 ulps of the reference almost everywhere (fp32 sums in another order)
+    bad = ((y.float() - z).abs() > 2 ** -6 * z.abs() + 1e-2).float().mean().item()
+    assert bad < 1e-3, bad
+    assert torch.equal(yb[:, K:].float().cpu(), torch.full((N, 32, OH, OW), 7.0)), 'columns past K must stay untouched'

@@ -66,9 +66,37 @@ def bench_cold(fn, n=10):
     return tot / n * 1e3
 
 
+def bench_graph(fn, n=50):
+    """n launches captured in one HIP graph and replayed: the GPU-side time per launch without the host launch cost
+    (TUNE_GRAPH=1; the batch-1 shapes are otherwise CPU launch-bound under ~20 us)"""
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(n):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / n * 1e3)
+    return best
+
+
 def bench(fn, n=20):
     if os.environ.get('TUNE_COLD'):
         return bench_cold(fn)
+    if os.environ.get('TUNE_GRAPH'):
+        return bench_graph(fn)
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
