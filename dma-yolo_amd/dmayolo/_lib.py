@@ -20,6 +20,7 @@ P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 SIGNATURES = {
     # conv.hip
     'dmy_conv_fwd_partial_rows': [L, I],
+    'dmy_conv_fwd_bn_rows': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L],
     'dmy_conv_fwd': [I, P, P, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_dgrad': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_wgrad': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],

@@ -597,7 +597,11 @@ class ConvBNActFn(torch.autograd.Function):
         if bn is not None:
             scale, shift, mean, invstd = f32(K, dev), f32(K, dev), f32(K, dev), f32(K, dev)
             if train_bn:
-                P = call('dmy_conv_fwd_fp8_partial_rows' if f8 is not None else 'dmy_conv_fwd_partial_rows', M, K)
+                if f8 is not None:
+                    P = call('dmy_conv_fwd_fp8_partial_rows', M, K)
+                else:  # the row count of the kernel the dispatch picks for exactly this launch (halo: per wave)
+                    P = call('dmy_conv_fwd_bn_rows', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(z), N, Hg, Wg, Cg,
+                             xps, K, kg, kg, sg, pg, OH, OW, K)
                 psum, psq = f32(P * K, dev), f32(P * K, dev)
                 _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, kg, sg, pg, OH, OW, C, k, f8=f8)
                 if P > 256:  # two-stage column reduction of the epilogue partials

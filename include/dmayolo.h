@@ -24,6 +24,12 @@ extern "C" {
  *      :1283-1304 (SCConv k2/k3/k4), :1172-1178 (CoorAttention conv1/conv_h/conv_w), models/yolo.py:63
  *      (Detect.m), and nn.Linear (common.py:105-108, 483-484) as a 1x1 conv over tokens. */
 int dmy_conv_fwd_partial_rows(long M, int K);
+/* BN partial rows dmy_conv_fwd writes for exactly these arguments (psum / psq must hold that many rows of K floats):
+ * the per-tile count of dmy_conv_fwd_partial_rows, or one row per wave of the persistent halo kernel
+ * (3x3 stride-1 64 -> 64-channel layers, csrc/conv.hip conv3_halo64) */
+int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w_ohwi, const float* bias, const void* y, int N,
+                                int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW,
+                                long yps);
 int dmy_conv_fwd(int dtype, const void* x, const void* w_ohwi, const float* bias, void* y, float* psum, float* psq,
                  int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
                  void* stream);

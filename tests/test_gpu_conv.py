@@ -29,7 +29,10 @@ SHAPES = [(2, 16, 20, 18, 24, 3, 1), (4, 64, 40, 40, 64, 3, 2), (8, 64, 40, 40, 
           (3, 64, 97, 89, 544, 1, 1), (5, 128, 57, 63, 288, 1, 1),
           # the 16-channel k3 view of the space-to-depth stem on the streaming GEMM's 3x3 gather (zero taps at the
           # borders, odd tile count, 32-column pass)
-          (5, 16, 61, 67, 64, 3, 1), (8, 16, 64, 64, 32, 3, 1), (3, 16, 97, 99, 96, 3, 1)]
+          (5, 16, 61, 67, 64, 3, 1), (8, 16, 64, 64, 32, 3, 1), (3, 16, 97, 99, 96, 3, 1),
+          # 3x3 64 -> 64 halo kernel (whole 8 x 32 tiles, >= one tile per CU): one tile per block, two per block with
+          # idle tail blocks, 8 tile rows per image
+          (8, 64, 64, 128, 64, 3, 1), (10, 64, 64, 128, 64, 3, 1), (4, 64, 96, 256, 64, 3, 1)]
 
 
 def _rel(a, b):
@@ -49,7 +52,7 @@ def test_conv_fwd_bf16_vs_torch(N, C, H, W, K, k, s):
     wf, _ = prep_weight(w.cuda(), torch.bfloat16, False)
     y = torch.empty(N, K, OH, OW, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
     M = N * OH * OW
-    P = call('dmy_conv_fwd_partial_rows', M, K)
+    P = call('dmy_conv_fwd_bn_rows', 1, ptr(xd), ptr(wf), None, ptr(y), N, H, W, C, C, K, k, k, s, p, OH, OW, K)
     ps = torch.full((P, K), float('nan'), device='cuda')
     pq = torch.full((P, K), float('nan'), device='cuda')
     rc = call('dmy_conv_fwd', 1, ptr(xd), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k, k, s, p, OH,
@@ -236,3 +239,38 @@ def test_conv_fwd_small_m_sk_vs_torch(N, C, H, W, K, k, s, res):
     bad = ((y.float() - z).abs() > 2 ** -6 * z.abs() + 1e-2).float().mean().item()
     assert bad < 1e-3, bad
     assert torch.equal(yb[:, K:].float().cpu(), torch.full((N, 32, OH, OW), 7.0)), 'columns past K must stay untouched'
+
+
+@pytest.mark.parametrize('DG', [False, True])
+def test_halo_conv_strided_views(DG):
+    """3x3 64 -> 64 halo kernel reading / writing channel slices of wider NHWC buffers (pixel strides 96 / 80), with
+    the per-wave BN partial rows dmy_conv_fwd_bn_rows reports (forward) and the data-grad tap flip"""
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    N, C, H, W, K = 8, 64, 64, 128, 64
+    g = torch.Generator().manual_seed(77 + DG)
+    xb = torch.randn(N, 96, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    yb = torch.zeros(N, 80, H, W, dtype=torch.bfloat16, device='cuda').contiguous(memory_format=torch.channels_last)
+    x, y = xb[:, 16:80], yb[:, 8:72]
+    w = (torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5).cuda()
+    wf, wt = prep_weight(w, torch.bfloat16, True)
+    if not DG:
+        ref = F.conv2d(x.float(), w.bfloat16().float(), padding=1)
+        P = call('dmy_conv_fwd_bn_rows', 1, ptr(x), ptr(wf), None, ptr(y), N, H, W, C, 96, K, 3, 3, 1, 1, H, W, 80)
+        assert P == 8 * 256 or P < 2 * N * H * W // 64, P
+        ps = torch.full((P, K), float('nan'), device='cuda')
+        pq = torch.full((P, K), float('nan'), device='cuda')
+        rc = call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, 96, K, 3, 3, 1, 1, H,
+                  W, 80, stream())
+    else:
+        ref = torch.nn.grad.conv2d_input((N, C, H, W), w.bfloat16().float(), x.float(), padding=1)
+        rc = call('dmy_conv_dgrad', 1, ptr(x), ptr(wt), ptr(y), 0, N, H, W, C, 80, K, 3, 3, 1, 1, H, W, 96, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+    assert float(yb[:, :8].float().abs().max()) == 0 and float(yb[:, 72:].float().abs().max()) == 0, 'slice overrun'
+    if not DG:
+        assert torch.isfinite(ps).all() and torch.isfinite(pq).all(), 'every partial row must be written'
+        s1 = ref.sum((0, 2, 3)).double()
+        assert float((ps.sum(0).double() - s1).abs().max()) < 1e-2 * (N * H * W) ** 0.5
+        assert _rel(pq.sum(0), (ref.double() ** 2).sum((0, 2, 3))) < 1e-3
+

@@ -39,6 +39,7 @@ SETS = {
             (1, 256, 96, 96, 1024, 1, 1), (1, 512, 96, 96, 512, 1, 1), (1, 1024, 48, 48, 1024, 1, 1),
             (1, 512, 48, 48, 512, 1, 1), (1, 128, 192, 192, 128, 3, 1), (1, 256, 96, 96, 256, 3, 1),
             (1, 64, 384, 384, 64, 3, 1), (1, 512, 48, 48, 512, 3, 1), (1, 128, 384, 384, 128, 1, 1)],
+    'halo': [(32, 64, 768, 768, 64, 3, 1), (32, 64, 384, 384, 64, 3, 1), (8, 64, 256, 256, 64, 3, 1)],
     'one': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
@@ -121,7 +122,7 @@ def main():
         y = torch.empty_like(dy)
         dx = torch.empty_like(x)
         M = N * OH * OW
-        P = call('dmy_conv_fwd_partial_rows', M, K)
+        P = call('dmy_conv_fwd_bn_rows', 1, ptr(x), ptr(wf), None, ptr(y), N, H, W, C, C, K, k, k, s, p, OH, OW, K)
         ps, pq = torch.empty(P * K, device='cuda'), torch.empty(P * K, device='cuda')
         dwo = torch.empty(K * C * k * k, device='cuda')
         fl = 2.0 * M * K * C * k * k
