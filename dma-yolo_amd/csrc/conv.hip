@@ -2932,62 +2932,78 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- 3x3 stride-1 halo kernel, 64 -> 64 channels
-// The 64-channel 3x3 layers (DMA-YOLO's C3 bottlenecks at 768^2 / 384^2) ran at 20-26 % of the MFMA peak on the
-// implicit-GEMM tiles: with 64 output columns every gathered A byte feeds only 128 flops, and the tap gather re-reads
+// The 64-channel 3x3 layers (DMA-YOLO's C3 bottlenecks at 384^2, SCConv k3 at 768^2) ran at 20-26 % of the MFMA peak on
+// the implicit-GEMM tiles: with 64 output columns every gathered A byte feeds only 128 flops, and the tap gather re-reads
 // each input pixel 9 times from L2 (256 x 64 A rows per K step, 9 K steps per tile), so the tiles wait on L2 -> LDS
 // traffic and on a 9-step pipeline's prologue / epilogue.  Here a block owns the whole layer's weights in LDS (9 taps
 // x 64 x 64 bf16 = 72 KiB, loaded once: persistent grid, one block per CU) and walks output tiles of 8 image rows x
 // 32 pixels: per tile ONE LDS-DMA load of the 10 x 34-pixel input halo (43 KiB, double-buffered so the next tile's
 // halo streams in under this tile's MFMAs), then all 9 taps read the halo through shifted LDS addresses.  L2 -> LDS
 // traffic per output pixel drops from 9 x 128 B to ~1.33 x 128 B.
-//   MFMA v_mfma_f32_32x32x16_bf16, transposed (D[channel][pixel] = W X^T): wave w computes image row w of the tile
-//   (32 pixels on the lanes) x 64 channels (2 accumulators of 32).  A 16-B fragment is (row = l & 31, k chunk
-//   2s + (l >> 5)) of a 128-B LDS row (a pixel of the halo, or a (tap, channel) row of W), 16-B chunks XOR-swizzled by
-//   (row >> 1) & 7: for every 32-row window, aligned or not, each ds_read_b128 lane group hits 16 distinct bank quads.
-//   Epilogue from registers: bf16 pairs, v_permlane32_swap -> 8 consecutive channels per lane, 4 x 16-B buffer stores
-//   per lane (they drain under the next tile's MFMAs: the next halo's wait counts exactly these 4 as younger).
+//   MFMA v_mfma_f32_32x32x16_bf16, transposed (D[channel][pixel] = W X^T): 4 waves (one per SIMD), wave w computes
+//   image rows 2w, 2w + 1 of the tile (32 pixels on the lanes each) x 64 channels = 2 x 2 accumulators, so per
+//   (tap, 16-deep k step) 2 halo + 2 weight fragments feed 4 MFMAs (1 KiB of LDS reads per 32-cycle MFMA: half the
+//   LDS array's 256 B/clk; a first version with 8 waves of one row each read 1.5 KiB per MFMA and ran at 34 % of the
+//   MFMA peak).  A 16-B fragment is (row = l & 31, k chunk 2s + (l >> 5)) of a 128-B LDS row (a halo pixel, or a
+//   (tap, channel) row of W), 16-B chunks XOR-swizzled by (row >> 1) & 7: for every 32-row window, aligned or not,
+//   each ds_read_b128 lane group hits 16 distinct bank quads.
+//   Epilogue from registers: bf16 pairs, v_permlane32_swap -> 8 consecutive channels per lane, 8 x 16-B buffer stores
+//   per lane (they drain under the next tile's MFMAs: the next halo's wait counts exactly these 8 as younger).
 //   BN partials: each lane accumulates sum z and sum z^2 of its pixel column over all tiles of the block in fp32;
-//   after the last tile the block writes ONE partial row per wave (rows blockIdx.x * 8 + wave, fixed order, no
+//   after the last tile the block writes ONE partial row per wave (rows blockIdx.x * 4 + wave, fixed order, no
 //   atomics): dmy_conv_fwd_bn_rows reports that row count to the host.
-//   DG = true: stride-1 data-grad, same gather with the tap sign flipped (dy halo, IHWO weight copy).
+//   DG = true: stride-1 data-grad, same gather with the tap sign flipped (dy halo, IHWO weight copy); accumulate adds
+//   the previous dx (loaded before the tile's MFMAs) as v3_epilogue does.
 namespace halo {
-constexpr int TH = 8, TW = 32;            // output tile: 8 image rows (one per wave) x 32 pixels
+constexpr int TH = 8, TW = 32;            // output tile: 8 image rows (two per wave) x 32 pixels
 constexpr int HW = TW + 2;                // halo row width (34 pixels); 10 halo rows
 constexpr int HPIX = (TH + 2) * HW;       // 340 pixels
 constexpr int HPIECES = (HPIX + 7) / 8;   // 43 LDS-DMA pieces of 8 pixel rows (1 KiB)
 constexpr int HBYTES = HPIECES * 1024;
 constexpr int WBYTES = 9 * 64 * 128;      // [tap][n][64 channels]
 constexpr int LDS = WBYTES + 2 * HBYTES;  // 161792 B
-constexpr int NPC = (HPIECES + 7) / 8;    // halo pieces per wave (waves >= HPIECES % 8 issue one fewer)
+constexpr int NW = 4;
+constexpr int NPC = (HPIECES + NW - 1) / NW;  // halo pieces per wave (waves >= HPIECES % NW issue one fewer)
 }  // namespace halo
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 DEV int hsw(int row) { return (row >> 1) & 7; }
+// accumulate epilogue: (bf16-rounded new value) + previous bf16 value, rounded once more -- the sum v3_epilogue forms
+DEV u4 add_bf16x8(u4 a, u4 b) {
+  float fa[8], fb[8];
+  unpack<bf16>(make_uint4(a[0], a[1], a[2], a[3]), fa);
+  unpack<bf16>(make_uint4(b[0], b[1], b[2], b[3]), fb);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fa[e] += fb[e];
+  const uint4 o = pack<bf16>(fa);
+  return u4{o.x, o.y, o.z, o.w};
+}
 
 template <bool DG>
-__global__ void __launch_bounds__(512, 1) conv3_halo64(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                        bf16* __restrict__ y,
-                                                        float* __restrict__ psum, float* __restrict__ psq, Geom g,
-                                                        int twn, int thn, int ntiles, int per, unsigned xbytes,
-                                                        unsigned wbytes, unsigned ybytes) {
+__global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                        bf16* __restrict__ y, float* __restrict__ psum,
+                                                        float* __restrict__ psq, Geom g, int twn, int thn, int ntiles,
+                                                        int per, unsigned xbytes, unsigned wbytes, unsigned ybytes,
+                                                        int accumulate) {
   __shared__ __attribute__((aligned(1024))) char smem[halo::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, px = lane & 31, hf = lane >> 5;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rw = make_rsrc(w, wbytes), ry = make_rsrc(y, ybytes);
   char* const wl = smem;
   const int u0 = blockIdx.x * per, u1 = min(u0 + per, ntiles);
   if (u0 >= u1) return;
-  // weights: 72 pieces, 9 per wave; row r = tap * 64 + n holds chunk (lane & 7) ^ hsw(r) of its 64 channels
+  // weights: 72 pieces, 18 per wave; row r = tap * 64 + n holds chunk (lane & 7) ^ hsw(r) of its 64 channels
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int pc = wid * 9 + i, r = pc * 8 + (lane >> 3), tap = r >> 6, n = r & 63;
+  for (int i = 0; i < 18; ++i) {
+    const int pc = wid * 18 + i, r = pc * 8 + (lane >> 3), tap = r >> 6, n = r & 63;
     const int c = (lane & 7) ^ hsw(r);
     blds16(rw, (unsigned)((n * 576 + tap * 64 + c * 8) * 2), wl + pc * 1024);
   }
   // this lane's halo pieces: pixel slot p = 8 pc + (lane >> 3) -> halo (hr, hc), source chunk (lane & 7) ^ hsw(p)
-  const int npc = wid < halo::HPIECES - 8 * (halo::NPC - 1) ? halo::NPC : halo::NPC - 1;
+  const int npc = wid < halo::HPIECES - halo::NW * (halo::NPC - 1) ? halo::NPC : halo::NPC - 1;
   int hr[halo::NPC], hc[halo::NPC], rel[halo::NPC];
 #pragma unroll
   for (int i = 0; i < halo::NPC; ++i) {
-    const int p = (wid + 8 * i) * 8 + (lane >> 3);
+    const int p = (wid + halo::NW * i) * 8 + (lane >> 3);
     const bool in = p < halo::HPIX;
     hr[i] = in ? p / halo::HW : -1000000;  // slots past the halo load zeros
     hc[i] = p % halo::HW;
@@ -3008,95 +3024,129 @@ __global__ void __launch_bounds__(512, 1) conv3_halo64(const bf16* __restrict__ 
       if (i < npc) {
         const int ih = oh0 - 1 + hr[i], iw = ow0 - 1 + hc[i];
         const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        blds16(rx, ok ? (unsigned)(base + rel[i]) * 2u : kBufOob, hl + (wid + 8 * i) * 1024);
+        blds16(rx, ok ? (unsigned)(base + rel[i]) * 2u : kBufOob, hl + (wid + halo::NW * i) * 1024);
       }
     }
   };
   issue_halo(u0, smem + halo::WBYTES);
   vm_wait<0>();
   const bool stats = psum != nullptr;
-  f32x16 s1[2], s2[2];
+  f32x16 s1[2], s2[2];  // per channel block j: this lane's pixel column summed over both rows and every tile
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) s1[j][r] = s2[j][r] = 0.f;
-  typedef unsigned u4 __attribute__((ext_vector_type(4)));
   for (int u = u0, it = 0; u < u1; ++u, ++it) {
     __builtin_amdgcn_s_barrier();  // halo(u) landed for every wave; every wave is done with the other buffer
-    char* const hl = smem + halo::WBYTES + (it & 1) * halo::HBYTES;
+    const char* const hl = smem + halo::WBYTES + (it & 1) * halo::HBYTES;
     if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
-    f32x16 acc[2];
+    int b, oh0, ow0;
+    tile_pos(u, b, oh0, ow0);
+    unsigned mrow[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < 2; ++i)
+      mrow[i] = (unsigned)((((long)b * g.OH + oh0 + 2 * wid + i) * g.OW + ow0 + px) * g.yps);
+    u4 prev[2][2][2];  // accumulate: this lane's eight 16-B output vectors, loaded before the MFMAs
+    if (accumulate) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kh = tap / 3, kw = tap % 3;
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int gq = 0; gq < 2; ++gq)
+            prev[i][j][gq] =
+                __builtin_amdgcn_raw_buffer_load_b128(ry, (mrow[i] + (unsigned)(32 * j + 16 * gq + 8 * hf)) * 2u, 0, 0);
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // 18 half-taps (tap, k steps 2 hs .. 2 hs + 1), software-pipelined: the 8 fragment reads of half-tap h + 1 are
+    // issued before the 8 MFMAs of half-tap h (one wave per SIMD: nothing else hides the LDS latency)
+    bf16x8 fa[2][2][2], fb[2][2][2];  // [buffer][k step][row i / channel block j]
+    auto load_half = [&](int h, bf16x8 (&a)[2][2], bf16x8 (&bw)[2][2]) {
+      const int tap = h >> 1, kh = tap / 3, kw = tap % 3;
       const int dh = DG ? 1 - kh : kh - 1, dw = DG ? 1 - kw : kw - 1;
-      const int p = (wid + 1 + dh) * halo::HW + px + 1 + dw;
-      const char* ap = hl + p * 128;
-      const int sw = hsw(p);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int c = 2 * s + hf;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + ((c ^ sw) << 4));
+      for (int ss = 0; ss < 2; ++ss) {
+        const int c = 2 * (2 * (h & 1) + ss) + hf;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int p = (2 * wid + i + 1 + dh) * halo::HW + px + 1 + dw;
+          a[ss][i] = *reinterpret_cast<const bf16x8*>(hl + p * 128 + ((c ^ hsw(p)) << 4));
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int n = 32 * j + px;
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wl + (tap * 64 + n) * 128 + ((c ^ hsw(n)) << 4));
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw, a, acc[j], 0, 0, 0);
+          bw[ss][j] = *reinterpret_cast<const bf16x8*>(wl + (tap * 64 + n) * 128 + ((c ^ hsw(n)) << 4));
         }
       }
+    };
+    load_half(0, fa[0], fb[0]);
+#pragma unroll
+    for (int h = 0; h < 18; ++h) {
+      if (h + 1 < 18) load_half(h + 1, fa[(h + 1) & 1], fb[(h + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[h & 1][ss][j], fa[h & 1][ss][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- epilogue: acc[j][r] = Y[pixel (row wid, column px)][channel 32 j + (r & 3) + 8 (r >> 2) + 4 hf]
-    int b, oh0, ow0;
-    tile_pos(u, b, oh0, ow0);
-    const unsigned mrow = (unsigned)((((long)b * g.OH + oh0 + wid) * g.OW + ow0 + px) * g.yps);
+    // ---- epilogue: acc[i][j][r] = Y[pixel (row 2 wid + i, column px)][channel 32 j + (r & 3) + 8 (r >> 2) + 4 hf]
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float v[16];
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        v[r] = acc[j][r];
-        if (stats) {
-          s1[j][r] += v[r];
-          s2[j][r] += v[r] * v[r];
+      for (int j = 0; j < 2; ++j) {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          v[r] = acc[i][j][r];
+          if (stats) {
+            s1[j][r] += v[r];
+            s2[j][r] += v[r] * v[r];
+          }
+        }
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {  // channel groups (gp, gp + 1) -> 8 consecutive channels per lane
+          const unsigned a0 = pk2_bf16(v[4 * gp], v[4 * gp + 1]), a1 = pk2_bf16(v[4 * gp + 2], v[4 * gp + 3]);
+          const unsigned b0 = pk2_bf16(v[4 * gp + 4], v[4 * gp + 5]), b1 = pk2_bf16(v[4 * gp + 6], v[4 * gp + 7]);
+          const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+          u4 o = {r0[0], r1[0], r0[1], r1[1]};
+          if (accumulate) o = add_bf16x8(o, prev[i][j][gp >> 1]);
+          const unsigned off = (mrow[i] + (unsigned)(32 * j + 8 * gp + 8 * hf)) * 2u;
+          __builtin_amdgcn_raw_buffer_store_b128(o, ry, off, 0, 0);
         }
       }
-#pragma unroll
-      for (int gp = 0; gp < 4; gp += 2) {  // channel groups (gp, gp + 1) -> 8 consecutive channels per lane
-        unsigned a0 = pk2_bf16(v[4 * gp], v[4 * gp + 1]), a1 = pk2_bf16(v[4 * gp + 2], v[4 * gp + 3]);
-        unsigned b0 = pk2_bf16(v[4 * gp + 4], v[4 * gp + 5]), b1 = pk2_bf16(v[4 * gp + 6], v[4 * gp + 7]);
-        const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-        const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-        const u4 o = {r0[0], r1[0], r0[1], r1[1]};
-        const unsigned off = (mrow + (unsigned)(32 * j + 8 * gp + 8 * hf)) * 2u;
-        __builtin_amdgcn_raw_buffer_store_b128(o, ry, off, 0, 0);
-      }
-    }
-    if (u + 1 < u1) vm_wait<4>();  // the next halo landed (only this tile's 4 stores are younger)
+    if (u + 1 < u1) vm_wait<8>();  // the next halo landed (only this tile's 8 stores are younger)
   }
   if (!stats) return;
   // ---- one BN partial row per wave: sum the 32 pixel lanes of each channel in a fixed order (through LDS)
   vm_wait<0>();
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [2][8 waves][64 channels][33]
+  float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][64 channels][33]
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ch = 32 * j + (r & 3) + 8 * (r >> 2) + 4 * hf;
       red[(wid * 64 + ch) * 33 + px] = s1[j][r];
-      red[((8 + wid) * 64 + ch) * 33 + px] = s2[j][r];
+      red[((halo::NW + wid) * 64 + ch) * 33 + px] = s2[j][r];
     }
   __syncthreads();
   float t1 = 0.f, t2 = 0.f;
   for (int q = 0; q < 32; ++q) {
     t1 += red[(wid * 64 + lane) * 33 + q];
-    t2 += red[((8 + wid) * 64 + lane) * 33 + q];
+    t2 += red[((halo::NW + wid) * 64 + lane) * 33 + q];
   }
-  const long row = (long)blockIdx.x * 8 + wid;
+  const long row = (long)blockIdx.x * halo::NW + wid;
   psum[row * 64 + lane] = t1;
   psq[row * 64 + lane] = t2;
 }
@@ -3400,35 +3450,39 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
 
 // 3x3 stride-1 64 -> 64-channel layers on the persistent halo kernel (v3::conv3_halo64): DMY_HALO = 0 off, 1 (default)
 // on.  g = the GEMM view (gathered H x W x C with pixel stride xps, output OH x OW x K with stride yps); whole 8 x 32
-// output tiles only, at least one tile per CU, no bias / inference epilogue / accumulate (the callers check those).
+// output tiles only, at least one tile per CU, no bias / inference epilogue (the callers check those).
 inline int halo_mode() {
   static const int t = env_int("DMY_HALO", 1);
   return t;
 }
+inline long halo_units(const Geom& g) { return (long)g.N * (g.H / v3::halo::TH) * (g.W / v3::halo::TW); }
 inline bool halo_ok(const Geom& g, const void* x, const void* w, const void* y) {
   if (!halo_mode() || !conv_buf_mode() || g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.C != 64 || g.K != 64 ||
       g.OH != g.H || g.OW != g.W || g.H % v3::halo::TH != 0 || g.W % v3::halo::TW != 0 || g.xps % 8 != 0 ||
       g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
     return false;
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), yb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
-  return xb < (double)v3::kBufOob && yb < (double)v3::kBufOob &&
-         (long)g.N * (g.H / v3::halo::TH) * (g.W / v3::halo::TW) >= num_cus();
+  return xb < (double)v3::kBufOob && yb < (double)v3::kBufOob && halo_units(g) >= num_cus();
 }
-// persistent grid: per = tiles per block, every block gets at least one tile (so every BN partial row is written)
+// persistent grid: per = tiles per block, every block gets at least one (so every BN partial row is written)
 inline int halo_blocks(const Geom& g, int* per_out = nullptr) {
-  const long nt = (long)g.N * (g.H / v3::halo::TH) * (g.W / v3::halo::TW);
+  const long nt = halo_units(g);
   const int per = ceil_div(nt, num_cus());
   if (per_out) *per_out = per;
   return ceil_div(nt, per);
 }
+// BN partial rows the halo kernel writes: one per wave
+inline int halo_rows(const Geom& g) { return v3::halo::NW * halo_blocks(g); }
 template <bool DG>
-int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, const Geom& g, hipStream_t st) {
-  const int thn = g.H / v3::halo::TH, twn = g.W / v3::halo::TW, nt = g.N * thn * twn;
+int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, const Geom& g, hipStream_t st,
+                int acc = 0) {
+  const int thn = g.H / v3::halo::TH, twn = g.W / v3::halo::TW, nt = (int)halo_units(g);
   int per = 1;
   const int G = halo_blocks(g, &per);
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps));
   const unsigned yb = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
-  v3::conv3_halo64<DG><<<(unsigned)G, 512, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb, 2u * 64 * 576, yb);
+  v3::conv3_halo64<DG><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb,
+                                                                  2u * 64 * 576, yb, acc);
   return (int)hipGetLastError();
 }
 
@@ -3754,8 +3808,8 @@ int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& 
         v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M)) {
       // GEMM view: rows = input pixels (N, H, W), columns = C, gather dy (OH x OW x K, stride yps)
       Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 1, g.P, g.H, g.W, g.xps);
-      if (!acc && bb.z == nullptr && halo_ok(gv, dy, wt, dx))
-        return launch_halo<true>((const bf16*)dy, (const bf16*)wt, (bf16*)dx, nullptr, nullptr, gv, st);
+      if (bb.z == nullptr && halo_ok(gv, dy, wt, dx))
+        return launch_halo<true>((const bf16*)dy, (const bf16*)wt, (bf16*)dx, nullptr, nullptr, gv, st, acc);
       return launch_v3<true>((const bf16*)dy, (const bf16*)wt, nullptr, (bf16*)dx, nullptr, nullptr, acc, gv, st,
                              Epi{}, bb);
     }
@@ -4117,7 +4171,7 @@ DMY_API int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w, const 
                                         int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P,
                                         int OH, int OW, long yps) {
   const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  if (dtype && bias == nullptr && halo_ok(g, x, w, y)) return 8 * halo_blocks(g);  // one row per wave (conv3_halo64)
+  if (dtype && bias == nullptr && halo_ok(g, x, w, y)) return halo_rows(g);  // one row per wave (conv3_halo64)
   return dmy_conv_fwd_partial_rows((long)N * OH * OW, K);
 }
 
