@@ -156,9 +156,68 @@ __global__ void __launch_bounds__(256) augment_batch_kernel(const AugDesc* __res
   o[2 * plane] = (unsigned char)bgr[0];
 }
 
+// ---- mosaic composition (datasets.py:680-724, load_image :659-675): the 2s x 2s canvas of a 4-image mosaic, built
+// on the GPU from the DECODED images (the workers only decode and draw).  Each quadrant is a rectangle
+// [y1a, y2a) x [x1a, x2a) of the canvas filled from the image resized to (h, w) by cv2 INTER_LINEAR (resize_linear:
+// 11-bit fixed-point coefficients, built on the host per axis exactly as data._linear_coeffs does), offset by
+// (y1b - y1a, x1b - x1a); the four rectangles are disjoint; everything else is 114.  Integer arithmetic only, so the
+// canvas equals the host restatement's bit for bit (tests/test_gpu_augment.py).
+struct MosaicQuad {
+  const unsigned char* src;  // decoded image, HWC BGR uint8, H0 x W0
+  const int* xt;             // [4][w]: x0, x1, a0, a1 of the resized columns
+  const int* yt;             // [4][h]: y0, y1, b0, b1 of the resized rows
+  int H0, W0, h, w;
+  int x1a, y1a, x2a, y2a, x1b, y1b, pad0, pad1;
+};
+struct MosaicDesc {
+  unsigned char* dst;  // canvas, HWC BGR uint8, S2 x S2
+  int S2, pad;
+  MosaicQuad q[4];
+};
+static_assert(sizeof(MosaicQuad) == 72 && sizeof(MosaicDesc) == 304, "MosaicDesc layout is part of the C ABI");
+
+__global__ void __launch_bounds__(256) mosaic_compose_kernel(const MosaicDesc* __restrict__ descs) {
+  const MosaicDesc& d = descs[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= d.S2 * d.S2) return;
+  const int y = i / d.S2, x = i - y * d.S2;
+  int bgr[3] = {114, 114, 114};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const MosaicQuad& q = d.q[k];
+    if (x < q.x1a || x >= q.x2a || y < q.y1a || y >= q.y2a) continue;
+    const int xr = x - q.x1a + q.x1b, yr = y - q.y1a + q.y1b;  // pixel of the resized image
+    const int x0 = q.xt[xr], x1 = q.xt[q.w + xr], a0 = q.xt[2 * q.w + xr], a1 = q.xt[3 * q.w + xr];
+    const int y0 = q.yt[yr], y1 = q.yt[q.h + yr], b0 = q.yt[2 * q.h + yr], b1 = q.yt[3 * q.h + yr];
+    const unsigned char* r0 = q.src + (long long)y0 * q.W0 * 3;
+    const unsigned char* r1 = q.src + (long long)y1 * q.W0 * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const long long h0 = (long long)r0[x0 * 3 + c] * a0 + (long long)r0[x1 * 3 + c] * a1;
+      const long long h1 = (long long)r1[x0 * 3 + c] * a0 + (long long)r1[x1 * 3 + c] * a1;
+      const long long v = (h0 * b0 + h1 * b1 + (1LL << 21)) >> 22;
+      bgr[c] = v < 0 ? 0 : (v > 255 ? 255 : (int)v);
+    }
+  }
+  unsigned char* o = d.dst + (long long)i * 3;
+  o[0] = (unsigned char)bgr[0];
+  o[1] = (unsigned char)bgr[1];
+  o[2] = (unsigned char)bgr[2];
+}
+
 bool tables_ready = false;
 
 }  // namespace
+
+DMY_API long dmy_mosaic_desc_bytes() { return (long)sizeof(MosaicDesc); }
+
+// descs: device array of n MosaicDesc (S2 = the largest canvas side); each canvas written into its dst
+DMY_API int dmy_mosaic_compose(const void* descs, int n, int S2, void* stream) {
+  if (n <= 0 || S2 <= 0) return 0;
+  const dim3 grid((unsigned)(((long)S2 * S2 + 255) / 256), (unsigned)n);
+  mosaic_compose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const MosaicDesc*)descs);
+  return (int)hipGetLastError();
+}
 
 DMY_API long dmy_aug_desc_bytes() { return (long)sizeof(AugDesc); }
 

@@ -38,6 +38,8 @@ SIGNATURES = {
     # augment.hip
     'dmy_aug_desc_bytes': [],
     'dmy_augment_batch': [P, I, P, I, I, P],
+    'dmy_mosaic_desc_bytes': [],
+    'dmy_mosaic_compose': [P, I, I, P],
     'dmy_fp8_quant_ws_elems': [],
     'dmy_fp8_quant': [P, L, I, L, P, P, P],
     'dmy_conv_wprep_fp8': [P, P, P, I, I, I, I, P],

@@ -284,10 +284,13 @@ def mosaic_canvas(ds, index):
     indices = [index] + random.choices(ds.indices, k=3)
     random.shuffle(indices)
     img4 = None
+    deferred = getattr(ds, 'gpu_compose', False)  # a MosaicSpec for dmy_mosaic_compose instead of the pixels
+    quads = []
     for i, idx in enumerate(indices):
-        img, _, (h, w) = ds.load_image(idx)
+        img, _, (h, w) = ds.load_image_raw(idx) if deferred else ds.load_image(idx)
         if i == 0:  # top left
-            img4 = np.full((s * 2, s * 2, img.shape[2]), BORDER, dtype=np.uint8)
+            if not deferred:
+                img4 = np.full((s * 2, s * 2, img.shape[2]), BORDER, dtype=np.uint8)
             x1a, y1a, x2a, y2a = max(xc - w, 0), max(yc - h, 0), xc, yc
             x1b, y1b, x2b, y2b = w - (x2a - x1a), h - (y2a - y1a), w, h
         elif i == 1:  # top right
@@ -299,7 +302,10 @@ def mosaic_canvas(ds, index):
         else:  # bottom right
             x1a, y1a, x2a, y2a = xc, yc, min(xc + w, s * 2), min(s * 2, yc + h)
             x1b, y1b, x2b, y2b = 0, 0, min(w, x2a - x1a), min(y2a - y1a, h)
-        img4[y1a:y2a, x1a:x2a] = img[y1b:y2b, x1b:x2b]
+        if deferred:
+            quads.append((img, (h, w), (x1a, y1a, x2a, y2a, x1b, y1b)))
+        else:
+            img4[y1a:y2a, x1a:x2a] = img[y1b:y2b, x1b:x2b]
         padw, padh = x1a - x1b, y1a - y1b
         labels = ds.labels[idx].copy()
         if labels.size:
@@ -307,7 +313,82 @@ def mosaic_canvas(ds, index):
         labels4.append(labels)
     labels4 = np.concatenate(labels4, 0)
     np.clip(labels4[:, 1:], 0, 2 * s, out=labels4[:, 1:])
-    return img4, labels4
+    return (MosaicSpec(2 * s, quads) if deferred else img4), labels4
+
+
+class MosaicSpec:
+    """a mosaic canvas not yet composed: its side S2 and per quadrant (decoded image, resized (h, w), canvas
+    rectangle (x1a, y1a, x2a, y2a) and source offset (x1b, y1b) in the resized image).  compose_cpu() / the GPU
+    (render_batch_gpu -> dmy_mosaic_compose) turn it into the uint8 canvas of datasets.py:680-724."""
+    __slots__ = ('S2', 'quads')
+
+    def __init__(self, S2, quads):
+        self.S2, self.quads = S2, quads
+
+    @property
+    def shape(self):
+        return (self.S2, self.S2, 3)
+
+
+def compose_cpu(spec):
+    """host restatement of the mosaic canvas from a MosaicSpec (resize_linear + placement, as mosaic_canvas)"""
+    from .data import resize_linear
+    img4 = np.full((spec.S2, spec.S2, 3), BORDER, dtype=np.uint8)
+    for img, (h, w), (x1a, y1a, x2a, y2a, x1b, y1b) in spec.quads:
+        im = resize_linear(img, w, h) if img.shape[:2] != (h, w) else img
+        img4[y1a:y2a, x1a:x2a] = im[y1b:y1b + (y2a - y1a), x1b:x1b + (x2a - x1a)]
+    return img4
+
+
+def _canvas(img):
+    return compose_cpu(img) if isinstance(img, MosaicSpec) else img
+
+
+MOSAIC_QUAD = np.dtype([('src', '<u8'), ('xt', '<u8'), ('yt', '<u8'), ('H0', '<i4'), ('W0', '<i4'), ('h', '<i4'),
+                        ('w', '<i4'), ('x1a', '<i4'), ('y1a', '<i4'), ('x2a', '<i4'), ('y2a', '<i4'), ('x1b', '<i4'),
+                        ('y1b', '<i4'), ('pad0', '<i4'), ('pad1', '<i4')])
+MOSAIC_DESC = np.dtype([('dst', '<u8'), ('S2', '<i4'), ('pad', '<i4'), ('q', MOSAIC_QUAD, (4,))])
+
+
+def _resize_table(dst, src):
+    """[4, dst] int32: source index 0 / 1 and 11-bit weights of cv2 INTER_LINEAR along one axis (data._linear_coeffs;
+    identity when no resize)"""
+    from .data import _linear_coeffs
+    if dst == src:
+        i = np.arange(dst)
+        return np.stack([i, i, np.full(dst, 2048), np.zeros(dst, np.int64)]).astype(np.int32)
+    return np.stack(_linear_coeffs(dst, src)).astype(np.int32)
+
+
+def compose_batch_gpu(specs, device, keep):
+    """compose every MosaicSpec of a batch on `device` with ONE dmy_mosaic_compose launch; -> device canvases
+    (uint8 [S2, S2, 3] tensors, kept alive through `keep` until the stream has used them)"""
+    import torch
+    from ._lib import call, ptr
+    from .functional import stream
+    assert call('dmy_mosaic_desc_bytes') == MOSAIC_DESC.itemsize, 'MosaicDesc layout mismatch'
+
+    def up(a):
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(device, non_blocking=True)
+        keep.append(t)
+        return t.data_ptr()
+
+    d = np.zeros(len(specs), dtype=MOSAIC_DESC)
+    outs = []
+    for n, sp in enumerate(specs):
+        out = torch.empty((sp.S2, sp.S2, 3), dtype=torch.uint8, device=device)
+        outs.append(out)
+        d[n]['dst'], d[n]['S2'] = out.data_ptr(), sp.S2
+        for k, (img, (h, w), (x1a, y1a, x2a, y2a, x1b, y1b)) in enumerate(sp.quads):
+            q = d[n]['q'][k]
+            q['src'], q['H0'], q['W0'], q['h'], q['w'] = up(img), img.shape[0], img.shape[1], h, w
+            q['xt'], q['yt'] = up(_resize_table(w, img.shape[1])), up(_resize_table(h, img.shape[0]))
+            q['x1a'], q['y1a'], q['x2a'], q['y2a'], q['x1b'], q['y1b'] = x1a, y1a, x2a, y2a, x1b, y1b
+    descs = torch.from_numpy(d.view(np.uint8)).to(device)
+    keep.append(descs)
+    call('dmy_mosaic_compose', ptr(descs), len(specs), max(sp.S2 for sp in specs), stream())
+    keep.extend(outs)
+    return outs
 
 
 def mosaic_warp(ds, index):
@@ -344,10 +425,10 @@ def _inverse9(M, persp):
 
 def render_cpu(rec):
     """the host tail of one record (datasets.py:552-622 after the draws): warp, mixup, HSV, flips -> HWC BGR"""
-    img = warp_image(rec['img'], rec['M'], rec['size'], rec['persp'], rec['changed'])
+    img = warp_image(_canvas(rec['img']), rec['M'], rec['size'], rec['persp'], rec['changed'])
     if rec['mix'] is not None:
         img2, M2, persp2, changed2, r = rec['mix']
-        img = (img * r + warp_image(img2, M2, rec['size'], persp2, changed2) * (1 - r)).astype(np.uint8)
+        img = (img * r + warp_image(_canvas(img2), M2, rec['size'], persp2, changed2) * (1 - r)).astype(np.uint8)
     if rec['luts'] is not None:
         img = np.ascontiguousarray(img)
         apply_hsv(img, rec['luts'])
@@ -368,8 +449,14 @@ def render_batch_gpu(recs, device):
     W, H = recs[0]['size']
     assert all(tuple(r['size']) == (W, H) for r in recs), 'one output size per batch'
     keep = []  # device canvases live until the kernel has run (stream-ordered frees)
+    specs = [r['img'] for r in recs if isinstance(r['img'], MosaicSpec)] + \
+        [r['mix'][0] for r in recs if r['mix'] is not None and isinstance(r['mix'][0], MosaicSpec)]
+    composed = dict(zip(map(id, specs), compose_batch_gpu(specs, device, keep))) if specs else {}
 
     def up(a):
+        if isinstance(a, MosaicSpec):
+            t = composed[id(a)]
+            return t.data_ptr()
         t = torch.from_numpy(np.ascontiguousarray(a)).to(device, non_blocking=True)
         keep.append(t)
         return t.data_ptr()

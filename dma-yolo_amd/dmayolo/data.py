@@ -247,6 +247,17 @@ class LoadImagesAndLabels(torch.utils.data.Dataset):
             im = resize_area(im, w, h) if (r < 1 and not self.augment) else resize_linear(im, w, h)
         return im, (h0, w0), im.shape[:2]
 
+    def load_image_raw(self, i):
+        """load_image without the pixel work: the decoded image, its size and the size load_image would resize it to
+        (augment.mosaic_canvas in gpu_compose mode; the resize then runs inside dmy_mosaic_compose)"""
+        im = _read_bgr(self.img_files[i])
+        h0, w0 = im.shape[:2]
+        r = self.img_size / max(h0, w0)
+        if r != 1:
+            assert r > 1 or self.augment, 'the GPU composition restates the INTER_LINEAR (augment) resize only'
+            return im, (h0, w0), (int(h0 * r), int(w0 * r))
+        return im, (h0, w0), (h0, w0)
+
     def record(self, index):
         """datasets.py:552-622 up to the pixel work: every random draw in the reference's order (mosaic?, the mosaic
         and its perspective draw, mixup? and its second mosaic and beta ratio, else letterbox + perspective draw,
@@ -340,12 +351,15 @@ class GpuAugmentLoader:
 
 
 def create_dataloader(path, imgsz, batch_size, stride, single_cls=False, hyp=None, augment=False, pad=0.0, rect=False,
-                      rank=-1, workers=8, shuffle=False, gpu_augment=None):
+                      rank=-1, workers=8, shuffle=False, gpu_augment=None, gpu_compose=True):
     """utils/datasets.py:95-121 (torch DataLoader; DistributedSampler under DDP so ranks shard the images).
-    gpu_augment=<device>: the augmentation tail runs on that GPU (GpuAugmentLoader)."""
+    gpu_augment=<device>: the augmentation tail runs on that GPU (GpuAugmentLoader); gpu_compose: the mosaic canvases
+    (resize + placement) as well."""
     dataset = LoadImagesAndLabels(path, imgsz, batch_size, augment=augment, hyp=hyp, rect=rect, stride=int(stride),
                                   pad=pad, single_cls=single_cls)
     dataset.gpu_augment = gpu_augment is not None
+    # mosaic canvases composed on the GPU too (dmy_mosaic_compose): the workers only decode and draw
+    dataset.gpu_compose = gpu_augment is not None and gpu_compose
     batch_size = min(batch_size, len(dataset))
     nw = min([os.cpu_count() or 1, batch_size if batch_size > 1 else 0, workers])
     sampler = None if rank == -1 else torch.utils.data.distributed.DistributedSampler(dataset, shuffle=shuffle)

@@ -324,6 +324,11 @@ int dmy_process_batch(const float* det, const int* det_off, const float* lab, co
  *      flips; layout in dmayolo/augment.py AUG_DESC) into uint8 out [n, 3, OH, OW]. */
 long dmy_aug_desc_bytes(void);
 int dmy_augment_batch(const void* descs, int n, void* out, int OH, int OW, void* stream);
+/* mosaic canvas composition (utils/datasets.py:680-724 with load_image :659-675's INTER_LINEAR resize): n MosaicDesc
+ * (4 decoded images, their host-built resize tables and canvas rectangles; layout in dmayolo/augment.py MOSAIC_DESC,
+ * sizeof = dmy_mosaic_desc_bytes) -> each desc's uint8 HWC BGR canvas of S2 x S2 (114 outside the four images). */
+long dmy_mosaic_desc_bytes(void);
+int dmy_mosaic_compose(const void* descs, int n, int S2, void* stream);
 
 #ifdef __cplusplus
 }

@@ -105,3 +105,31 @@ def test_dataset_and_collate(tmp_path, rect):
                 assert tuple(imgs[b, :, int(y), int(x)].tolist())[0] == 200, (name, row)
         seen += imgs.shape[0]
     assert seen == len(sizes)
+
+
+def test_deferred_mosaic_spec_composes_to_the_same_canvas(tmp_path):
+    """mosaic_canvas in gpu_compose mode (decoded images + rectangles, no pixel work) composed by compose_cpu equals
+    the canvas the direct path builds under the same random draws, and carries the same labels"""
+    import random
+    from PIL import Image
+    from dmayolo.data import LoadImagesAndLabels
+    from dmayolo.augment import mosaic_canvas, compose_cpu, MosaicSpec
+    from dmayolo.synthetic import HYP_VISDRONE
+    (tmp_path / 'images').mkdir()
+    (tmp_path / 'labels').mkdir()
+    rng = np.random.default_rng(5)
+    for i in range(6):
+        w, h = int(rng.integers(90, 230)), int(rng.integers(80, 200))
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(tmp_path / 'images' / f'{i}.png')
+        (tmp_path / 'labels' / f'{i}.txt').write_text('0 0.5 0.5 0.2 0.3')
+    ds = LoadImagesAndLabels(str(tmp_path / 'images'), img_size=128, batch_size=4, augment=True, hyp=dict(HYP_VISDRONE))
+    for idx in range(6):
+        random.seed(idx)
+        ds.gpu_compose = False
+        c1, l1 = mosaic_canvas(ds, idx)
+        random.seed(idx)
+        ds.gpu_compose = True
+        sp, l2 = mosaic_canvas(ds, idx)
+        assert isinstance(sp, MosaicSpec) and sp.shape == c1.shape
+        assert np.array_equal(compose_cpu(sp), c1) and np.array_equal(l1, l2)
+

@@ -128,3 +128,26 @@ def test_gpu_tail_throughput_at_1536():
     ms = e0.elapsed_time(e1)
     print(f'render 32 x 1536^2 (incl. 32 canvas uploads of 28 MB): {ms:.1f} ms')
     assert out.shape == (32, 3, 1536, 1536)
+
+
+@pytest.mark.parametrize('case', ['mosaic_warp_only', 'mosaic_mixup'])
+def test_gpu_mosaic_compose_equals_host(tmp_path, case):
+    """dmy_mosaic_compose (resize_linear + placement of the 4 decoded images on the GPU) == compose_cpu on the same
+    MosaicSpecs, and the whole deferred batch (compose + tail) == render_cpu"""
+    from dmayolo.data import LoadImagesAndLabels
+    from dmayolo.augment import MosaicSpec, compose_cpu, compose_batch_gpu, render_cpu, render_batch_gpu
+    ds = LoadImagesAndLabels(_dataset(tmp_path), img_size=160, batch_size=8, augment=True, hyp=_hyp(**CASES[case]))
+    ds.gpu_compose = True
+    random.seed(11)
+    np.random.seed(11)
+    recs = [ds.record(i) for i in range(8)]
+    specs = [r['img'] for r in recs if isinstance(r['img'], MosaicSpec)]
+    assert len(specs) == 8
+    keep = []
+    dev = [c.cpu().numpy() for c in compose_batch_gpu(specs, torch.device('cuda'), keep)]
+    for sp, d in zip(specs, dev):
+        h = compose_cpu(sp)
+        assert d.shape == h.shape and np.array_equal(d, h), f'{int((d != h).sum())} canvas bytes differ'
+    host = np.stack([np.ascontiguousarray(render_cpu(r).transpose(2, 0, 1)[::-1]) for r in recs])
+    out = render_batch_gpu(recs, torch.device('cuda')).cpu().numpy()
+    assert np.array_equal(out, host)

@@ -12,10 +12,13 @@ for cfg in ${CFGS:-dma-1536 v5s-640}; do
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r03/stats_$cfg -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py $ARGS > $GRAFT_REPO_ROOT/gpurun_out/r03/stats_$cfg.log 2>&1)
   rc=$?; echo "stats $cfg rc=$rc"; [ $rc -ne 0 ] && exit $rc
   [ -n "$NOPMC" ] && continue
+  # PMC passes on 1 + 1 steps: rocprofv3 --pmc segfaults inside the HIP runtime (dmy_bn_bwd_finalize's dispatch) a few
+  # seconds into the 3 + 2-step command (profiles/r03/pmc_crash.log), the short one completes
+  PARGS="--config $cfg --also none --steps 1 --warmup 1 --no-cpu-baseline --no-detect"
   for pass in fetch write; do
     ctr=$([ $pass = fetch ] && echo FETCH_SIZE || echo WRITE_SIZE)
     out=$GRAFT_REPO_ROOT/gpurun_out/r03/pmc_${cfg}_$pass
-    (cd /tmp && timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $ctr -d $out -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py $ARGS > $out.log 2>&1)
+    (cd /tmp && timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $ctr -d $out -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py $PARGS > $out.log 2>&1)
     rc=$?; echo "pmc $cfg $pass rc=$rc"; [ $rc -ne 0 ] && { tail -5 $out.log; exit $rc; }
   done
 done

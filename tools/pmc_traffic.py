@@ -44,6 +44,16 @@ def family(name):
         return 'conv_dgrad' if len(args) > 3 and args[3] == 'true' else 'conv_fwd'
     if 'conv_fwd_f8<' in name:
         return 'conv_fwd_f8'
+    if 'conv_p1p<' in name:  # <BM, BN, NS, WTR, DG>
+        args = _targs(name, 'conv_p1p<')
+        return 'conv_dgrad' if len(args) > 4 and args[4] == 'true' else 'conv_fwd'
+    if 'conv3_halo64<' in name:  # <DG>
+        return 'conv_dgrad' if _targs(name, 'conv3_halo64<')[0] == 'true' else 'conv_fwd'
+    if 'conv_p1s<' in name or 'conv_sk<' in name or 'conv_p1_persist<' in name:
+        if 'conv_p1_persist<' in name:
+            args = _targs(name, 'conv_p1_persist<')
+            return 'conv_dgrad' if len(args) > 2 and args[2] == 'true' else 'conv_fwd'
+        return 'conv_fwd'
     for fam, keys in FAMILIES.items():
         if any(k in name for k in keys):
             return fam
