@@ -167,7 +167,9 @@ struct MosaicQuad {
   const int* xt;             // [4][w]: x0, x1, a0, a1 of the resized columns
   const int* yt;             // [4][h]: y0, y1, b0, b1 of the resized rows
   int H0, W0, h, w;
-  int x1a, y1a, x2a, y2a, x1b, y1b, pad0, pad1;
+  int x1a, y1a, x2a, y2a, x1b, y1b;
+  int rgb;  // 1: the decoded image is RGB (load_image_raw), the canvas BGR
+  int pad1;
 };
 struct MosaicDesc {
   unsigned char* dst;  // canvas, HWC BGR uint8, S2 x S2
@@ -193,8 +195,9 @@ __global__ void __launch_bounds__(256) mosaic_compose_kernel(const MosaicDesc* _
     const unsigned char* r1 = q.src + (long long)y1 * q.W0 * 3;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const long long h0 = (long long)r0[x0 * 3 + c] * a0 + (long long)r0[x1 * 3 + c] * a1;
-      const long long h1 = (long long)r1[x0 * 3 + c] * a0 + (long long)r1[x1 * 3 + c] * a1;
+      const int cs = q.rgb ? 2 - c : c;  // source channel of canvas channel c (BGR)
+      const long long h0 = (long long)r0[x0 * 3 + cs] * a0 + (long long)r0[x1 * 3 + cs] * a1;
+      const long long h1 = (long long)r1[x0 * 3 + cs] * a0 + (long long)r1[x1 * 3 + cs] * a1;
       const long long v = (h0 * b0 + h1 * b1 + (1LL << 21)) >> 22;
       bgr[c] = v < 0 ? 0 : (v > 255 ? 255 : (int)v);
     }

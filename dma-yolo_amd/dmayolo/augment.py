@@ -317,9 +317,9 @@ def mosaic_canvas(ds, index):
 
 
 class MosaicSpec:
-    """a mosaic canvas not yet composed: its side S2 and per quadrant (decoded image, resized (h, w), canvas
+    """a mosaic canvas not yet composed: its side S2 and per quadrant (decoded RGB image tensor, resized (h, w), canvas
     rectangle (x1a, y1a, x2a, y2a) and source offset (x1b, y1b) in the resized image).  compose_cpu() / the GPU
-    (render_batch_gpu -> dmy_mosaic_compose) turn it into the uint8 canvas of datasets.py:680-724."""
+    (render_batch_gpu -> dmy_mosaic_compose) turn it into the uint8 BGR canvas of datasets.py:680-724."""
     __slots__ = ('S2', 'quads')
 
     def __init__(self, S2, quads):
@@ -335,6 +335,7 @@ def compose_cpu(spec):
     from .data import resize_linear
     img4 = np.full((spec.S2, spec.S2, 3), BORDER, dtype=np.uint8)
     for img, (h, w), (x1a, y1a, x2a, y2a, x1b, y1b) in spec.quads:
+        img = np.ascontiguousarray(np.asarray(img)[:, :, ::-1])  # RGB -> BGR, as _read_bgr
         im = resize_linear(img, w, h) if img.shape[:2] != (h, w) else img
         img4[y1a:y2a, x1a:x2a] = im[y1b:y1b + (y2a - y1a), x1b:x1b + (x2a - x1a)]
     return img4
@@ -346,7 +347,7 @@ def _canvas(img):
 
 MOSAIC_QUAD = np.dtype([('src', '<u8'), ('xt', '<u8'), ('yt', '<u8'), ('H0', '<i4'), ('W0', '<i4'), ('h', '<i4'),
                         ('w', '<i4'), ('x1a', '<i4'), ('y1a', '<i4'), ('x2a', '<i4'), ('y2a', '<i4'), ('x1b', '<i4'),
-                        ('y1b', '<i4'), ('pad0', '<i4'), ('pad1', '<i4')])
+                        ('y1b', '<i4'), ('rgb', '<i4'), ('pad1', '<i4')])
 MOSAIC_DESC = np.dtype([('dst', '<u8'), ('S2', '<i4'), ('pad', '<i4'), ('q', MOSAIC_QUAD, (4,))])
 
 
@@ -369,7 +370,7 @@ def compose_batch_gpu(specs, device, keep):
     assert call('dmy_mosaic_desc_bytes') == MOSAIC_DESC.itemsize, 'MosaicDesc layout mismatch'
 
     def up(a):
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(device, non_blocking=True)
+        t = (a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))).to(device, non_blocking=True)
         keep.append(t)
         return t.data_ptr()
 
@@ -383,6 +384,7 @@ def compose_batch_gpu(specs, device, keep):
             q = d[n]['q'][k]
             q['src'], q['H0'], q['W0'], q['h'], q['w'] = up(img), img.shape[0], img.shape[1], h, w
             q['xt'], q['yt'] = up(_resize_table(w, img.shape[1])), up(_resize_table(h, img.shape[0]))
+            q['rgb'] = 1  # load_image_raw's channel order: the kernel writes BGR
             q['x1a'], q['y1a'], q['x2a'], q['y2a'], q['x1b'], q['y1b'] = x1a, y1a, x2a, y2a, x1b, y1b
     descs = torch.from_numpy(d.view(np.uint8)).to(device)
     keep.append(descs)

@@ -165,12 +165,13 @@ def xyxy2xywhn(x, w=640, h=640, clip=False, eps=0.0):
     return y
 
 
-def _read_bgr(path):
-    """cv2.imread(path) (BGR uint8 HWC) through PIL, EXIF orientation applied as cv2 does"""
+def _read_bgr(path, rgb=False):
+    """cv2.imread(path) (BGR uint8 HWC) through PIL, EXIF orientation applied as cv2 does; rgb=True skips the channel
+    flip (the GPU composition reads RGB and writes BGR)"""
     from PIL import Image, ImageOps
     with Image.open(path) as im:
         im = ImageOps.exif_transpose(im).convert('RGB')
-        return np.ascontiguousarray(np.asarray(im)[:, :, ::-1])
+        return np.array(im) if rgb else np.ascontiguousarray(np.asarray(im)[:, :, ::-1])
 
 
 # ------------------------------------------------------------------ dataset / loader
@@ -248,9 +249,10 @@ class LoadImagesAndLabels(torch.utils.data.Dataset):
         return im, (h0, w0), im.shape[:2]
 
     def load_image_raw(self, i):
-        """load_image without the pixel work: the decoded image, its size and the size load_image would resize it to
-        (augment.mosaic_canvas in gpu_compose mode; the resize then runs inside dmy_mosaic_compose)"""
-        im = _read_bgr(self.img_files[i])
+        """load_image without the pixel work: the decoded image as an RGB uint8 HWC tensor (DataLoader workers hand
+        tensors over through shared memory, not the pipe), its size and the size load_image would resize it to
+        (augment.mosaic_canvas in gpu_compose mode; resize and RGB -> BGR then run inside dmy_mosaic_compose)"""
+        im = torch.from_numpy(_read_bgr(self.img_files[i], rgb=True))
         h0, w0 = im.shape[:2]
         r = self.img_size / max(h0, w0)
         if r != 1:
@@ -363,9 +365,10 @@ def create_dataloader(path, imgsz, batch_size, stride, single_cls=False, hyp=Non
     batch_size = min(batch_size, len(dataset))
     nw = min([os.cpu_count() or 1, batch_size if batch_size > 1 else 0, workers])
     sampler = None if rank == -1 else torch.utils.data.distributed.DistributedSampler(dataset, shuffle=shuffle)
+    # persistent workers: the reference's InfiniteDataLoader (datasets.py:124-141) reuses its workers across epochs
     loader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle and sampler is None,
                                          num_workers=nw, sampler=sampler, pin_memory=True,
-                                         collate_fn=LoadImagesAndLabels.collate_fn)
+                                         collate_fn=LoadImagesAndLabels.collate_fn, persistent_workers=nw > 0)
     if gpu_augment is not None:
         loader = GpuAugmentLoader(loader, gpu_augment)
     return loader, dataset

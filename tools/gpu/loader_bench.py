@@ -49,6 +49,7 @@ def main():
             for imgs, targets, _, _ in loader:
                 torch.cuda.synchronize()
                 done += 1
+                print(f'{"gpu" if compose else "host"} compose batch {done}', file=sys.stderr, flush=True)
                 if done == 2:  # the first two batches include the worker start-up
                     t0 = time.perf_counter()
                 elif done > 2:
