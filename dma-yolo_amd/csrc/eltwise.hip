@@ -198,6 +198,27 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const T* __restrict__ 
 // tile are staged in LDS and each input pixel gathers its contributions (deterministic, no atomics).
 constexpr int MP_TH = 16, MP_TW = 32;
 
+// Block -> (image, tile, 16-B channel vector) of the LDS max-pool kernels: one 1-D grid in an XCD-contiguous logical
+// order with the channel vector fastest, so the CV blocks that read the same pixel rows (one 16-B slice of each
+// 128..2048-B pixel row per block) run together on one XCD and share its L2 instead of each re-reading the rows from
+// HBM / the Infinity Cache (the 3-D grid it replaces put every image's tiles of one channel slice before the next).
+struct MpTile {
+  int b, c, h0, w0;
+};
+DEV MpTile mp_tile(int CV, int NV, int twn, int thn) {
+  const int nwg = (int)gridDim.x, id = (int)blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = id % 8, loc = id / 8;
+  int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  MpTile t;
+  t.c = (L % CV) * NV;
+  L /= CV;
+  t.w0 = (L % twn) * MP_TW;
+  L /= twn;
+  t.h0 = (L % thn) * MP_TH;
+  t.b = L / thn;
+  return t;
+}
+
 template <typename T, int K>
 __global__ void __launch_bounds__(256) maxpool_fwd_lds(const T* __restrict__ x, long xps, T* __restrict__ y, long yps,
                                                        uint8_t* __restrict__ arg, int H, int W, int C) {
@@ -205,9 +226,8 @@ __global__ void __launch_bounds__(256) maxpool_fwd_lds(const T* __restrict__ x, 
   __shared__ uint4 xin[IH * IW];
   __shared__ uint4 rm[IH * MP_TW];
   __shared__ uint2 ra[IH * MP_TW];
-  const int CV = C / NV;
-  const int b = blockIdx.z / CV, c = (blockIdx.z % CV) * NV;
-  const int h0 = blockIdx.y * MP_TH, w0 = blockIdx.x * MP_TW;
+  const MpTile tl = mp_tile(C / NV, NV, (W + MP_TW - 1) / MP_TW, (H + MP_TH - 1) / MP_TH);
+  const int b = tl.b, c = tl.c, h0 = tl.h0, w0 = tl.w0;
   const T* xb = x + (long)b * H * W * xps + c;
   for (int e = threadIdx.x; e < IH * IW; e += 256) {
     const int hh = h0 - P + e / IW, ww = w0 - P + e % IW;
@@ -280,16 +300,23 @@ __global__ void __launch_bounds__(256) maxpool_fwd_lds(const T* __restrict__ x, 
   }
 }
 
+// Backward, separable like the forward: an output q routes dy[q] to input (q_h + dh* - P, q_w + dw* - P) where dh* is
+// its column-pass winner and dw* the row-pass winner at (that row, q_w) -- the same dw* for every output that picks
+// that row position.  Stage A sums, for each (tile row, output column), the dy of the outputs whose column pass chose
+// that row (K checks) and keeps their dw*; stage B sums, for each input pixel, the stage-A sums whose dw* points at it
+// (K checks): 2K window checks per input instead of the K^2 of a direct gather (the k = 13 SPP pools of config 5 spent
+// 5 ms per call there).  Sums over dh then dw, in fixed order (deterministic, no atomics).
 template <typename T, int K>
 __global__ void __launch_bounds__(256) maxpool_bwd_lds(const T* __restrict__ dy, long dps, const uint8_t* __restrict__ arg,
                                                        T* __restrict__ dx, long dxps, int accumulate, int H, int W, int C) {
   constexpr int NV = Traits<T>::VW, P = K / 2, IH = MP_TH + K - 1, IW = MP_TW + K - 1;
   using AW = typename std::conditional<NV == 8, uint2, uint32_t>::type;
-  __shared__ uint4 gs[IH * IW];
-  __shared__ AW as_[IH * IW];
-  const int CV = C / NV;
-  const int b = blockIdx.z / CV, c = (blockIdx.z % CV) * NV;
-  const int h0 = blockIdx.y * MP_TH, w0 = blockIdx.x * MP_TW;
+  __shared__ uint4 gs[IH * IW];       // dy of every output that can route into the tile
+  __shared__ AW as_[IH * IW];         // their window offsets dh* K + dw* (0xFF: out of image)
+  __shared__ float dr[MP_TH * IW * NV];  // stage A: per (tile row, output column) the column-routed sums
+  __shared__ AW rs[MP_TH * IW];       // ... and their row-pass winner dw* (0xFF: nothing routed)
+  const MpTile tl = mp_tile(C / NV, NV, (W + MP_TW - 1) / MP_TW, (H + MP_TH - 1) / MP_TH);
+  const int b = tl.b, c = tl.c, h0 = tl.h0, w0 = tl.w0;
   // outputs q in [h0 - P, h0 + TH - 1 + P] x [w0 - P, w0 + TW - 1 + P]; out-of-image ones never route
   for (int e = threadIdx.x; e < IH * IW; e += 256) {
     const int qh = h0 - P + e / IW, qw = w0 - P + e % IW;
@@ -300,6 +327,37 @@ __global__ void __launch_bounds__(256) maxpool_bwd_lds(const T* __restrict__ dy,
     if constexpr (NV == 8) { if (!ok) as_[e] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu); }
   }
   __syncthreads();
+  // stage A: tile row h (input row h0 + h) x output column index ec; output row h0 + h + P - dh = gs row h + K - 1 - dh
+  for (int e = threadIdx.x; e < MP_TH * IW; e += 256) {
+    const int h = e / IW, ec = e % IW;
+    float s[NV];
+    uint8_t sel[sizeof(AW)];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) { s[j] = 0.f; sel[j] = 0xFF; }
+#pragma unroll
+    for (int dh = 0; dh < K; ++dh) {
+      const int slot = (h + K - 1 - dh) * IW + ec;
+      const AW a2 = as_[slot];
+      const uint8_t* a = reinterpret_cast<const uint8_t*>(&a2);
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) any |= a[j] != 0xFF && a[j] / K == dh;
+      if (!any) continue;
+      float d[NV];
+      unpack<T>(gs[slot], d);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const bool m = a[j] != 0xFF && a[j] / K == dh;
+        s[j] += m ? d[j] : 0.f;
+        sel[j] = m ? (uint8_t)(a[j] % K) : sel[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) dr[e * NV + j] = s[j];
+    rs[e] = *reinterpret_cast<const AW*>(sel);
+  }
+  __syncthreads();
+  // stage B: input (h0 + h, w0 + w) gathers the stage-A sums at output column index w + K - 1 - dw whose dw* == dw
   for (int e = threadIdx.x; e < MP_TH * MP_TW; e += 256) {
     const int h = e / MP_TW, w = e % MP_TW;
     const int ih = h0 + h, iw = w0 + w;
@@ -307,24 +365,14 @@ __global__ void __launch_bounds__(256) maxpool_bwd_lds(const T* __restrict__ dy,
     float s[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) s[j] = 0.f;
-    // output q = (ih + P - dh, iw + P - dw) routes to p iff its window offset == dh * K + dw
 #pragma unroll
-    for (int dh = 0; dh < K; ++dh)
+    for (int dw = 0; dw < K; ++dw) {
+      const int pos = h * IW + w + K - 1 - dw;
+      const AW a2 = rs[pos];
+      const uint8_t* a = reinterpret_cast<const uint8_t*>(&a2);
 #pragma unroll
-      for (int dw = 0; dw < K; ++dw) {
-        const int slot = (h + K - 1 - dh) * IW + (w + K - 1 - dw);
-        const AW a2 = as_[slot];
-        const uint8_t* a = reinterpret_cast<const uint8_t*>(&a2);
-        const uint8_t want = (uint8_t)(dh * K + dw);
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < NV; ++j) any |= a[j] == want;
-        if (!any) continue;
-        float d[NV];
-        unpack<T>(gs[slot], d);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) s[j] += a[j] == want ? d[j] : 0.f;
-      }
+      for (int j = 0; j < NV; ++j) s[j] += a[j] == dw ? dr[pos * NV + j] : 0.f;
+    }
     T* o = dx + (((long)b * H + ih) * W + iw) * dxps + c;
     if (accumulate) {
       float d[NV];
@@ -1106,7 +1154,7 @@ DMY_API int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yp
   const bool v = vec_ok(dtype, {C, xps, yps}, {x, y});
   if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;  // uint8 window offsets
   if (v && N * (C / (dtype ? 8 : 4)) < 65536 && k >= 3 && k <= 13) {
-    const dim3 gl(ceil_div(W, MP_TW), ceil_div(H, MP_TH), N * (C / (dtype ? 8 : 4)));
+    const unsigned gl = (unsigned)ceil_div(W, MP_TW) * ceil_div(H, MP_TH) * N * (C / (dtype ? 8 : 4));  // mp_tile order
 #define MP_LDS(KS) if (dtype) maxpool_fwd_lds<bf16, KS><<<gl, 256, 0, st>>>((const bf16*)x, xps, (bf16*)y, yps, arg, H, W, C); \
                    else maxpool_fwd_lds<float, KS><<<gl, 256, 0, st>>>((const float*)x, xps, (float*)y, yps, arg, H, W, C)
     switch (k) {
@@ -1140,7 +1188,7 @@ DMY_API int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned 
   const bool v = vec_ok(dtype, {C, dps, dxps}, {dy, dx});
   if (k < 1 || k > 15 || (k & 1) == 0) return (int)hipErrorInvalidValue;
   if (v && N * (C / (dtype ? 8 : 4)) < 65536 && k >= 3 && k <= 13) {
-    const dim3 gl(ceil_div(W, MP_TW), ceil_div(H, MP_TH), N * (C / (dtype ? 8 : 4)));
+    const unsigned gl = (unsigned)ceil_div(W, MP_TW) * ceil_div(H, MP_TH) * N * (C / (dtype ? 8 : 4));  // mp_tile order
 #define MP_LDS(KS) if (dtype) maxpool_bwd_lds<bf16, KS><<<gl, 256, 0, st>>>((const bf16*)dy, dps, arg, (bf16*)dx, dxps, accumulate, H, W, C); \
                    else maxpool_bwd_lds<float, KS><<<gl, 256, 0, st>>>((const float*)dy, dps, arg, (float*)dx, dxps, accumulate, H, W, C)
     switch (k) {
