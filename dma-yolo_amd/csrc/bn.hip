@@ -114,7 +114,7 @@ struct RowMap {
 template <typename T, int U = 1>
 __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, long zps, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, int act, const T* __restrict__ res,
-                                                      long rps, T* __restrict__ y, long yps, long M, int C) {
+                                                      long rps, T* __restrict__ y, long yps, long M, int C, int rev) {
   constexpr int VW = Traits<T>::VW;
   RowMap rm(C, VW);
   if (!rm.active()) return;
@@ -127,16 +127,16 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
     uint4 zv[U], rv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long mu = m + u * S;
-      if (mu < M) {
+      const long mu = rev ? M - 1 - (m + u * S) : m + u * S;
+      if (m + u * S < M) {
         zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
         if (res) rv[u] = *reinterpret_cast<const uint4*>(res + mu * rps + c0);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long mu = m + u * S;
-      if (mu >= M) break;
+      const long mu = rev ? M - 1 - (m + u * S) : m + u * S;
+      if (m + u * S >= M) break;
       float f[VW];
       unpack<T>(zv[u], f);
       if (res) {
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
                                                          long dps, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, const float* __restrict__ mean,
                                                          const float* __restrict__ invstd, int act, long M, int C,
-                                                         float* __restrict__ pdb, float* __restrict__ pdg) {
+                                                         float* __restrict__ pdb, float* __restrict__ pdg, int rev) {
   constexpr int VW = Traits<T>::VW;
   __shared__ float red[2][256 * VW];
   RowMap rm(C, VW);
@@ -256,8 +256,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
       uint4 zv[U], gv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long mu = m + u * S;
-        if (mu < M) {
+        const long mu = rev ? M - 1 - (m + u * S) : m + u * S;
+        if (m + u * S < M) {
           zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
           if (!STATS) gv[u] = *reinterpret_cast<const uint4*>(dy + mu * dps + c0);
         }
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z,
                                                         const float* __restrict__ invstd, int act,
                                                         const float* __restrict__ ca, const float* __restrict__ cb,
                                                         const float* __restrict__ cc, T* __restrict__ dz, long dzps,
-                                                        long M, int C) {
+                                                        long M, int C, int rev) {
   constexpr int VW = Traits<T>::VW;
   RowMap rm(C, VW);
   if (!rm.active()) return;
@@ -330,16 +330,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z,
     uint4 zv[U], gv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long mu = m + u * S;
-      if (mu < M) {
+      const long mu = rev ? M - 1 - (m + u * S) : m + u * S;
+      if (m + u * S < M) {
         zv[u] = *reinterpret_cast<const uint4*>(z + mu * zps + c0);
         gv[u] = *reinterpret_cast<const uint4*>(dy + mu * dps + c0);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long mu = m + u * S;
-      if (mu >= M) break;
+      const long mu = rev ? M - 1 - (m + u * S) : m + u * S;
+      if (m + u * S >= M) break;
       float zf[VW], gf[VW], o[VW];
       unpack<T>(zv[u], zf);
       unpack<T>(gv[u], gf);
@@ -481,6 +481,18 @@ inline int vec_grid(long M, int C, int VW) {
   const int RB = 256 / (C / VW);
   return grid_cap(ceil_div(M, (long)RB * 8), cap);
 }
+// row order of the streaming passes, as a bit mask (DMY_BN_ORDER): 1 = bn_act_fwd, 2 = bn_bwd_reduce, 4 = bn_bwd_apply
+// walk M from the END.  A pass that reads a tensor in the reverse of the order its producer (or the previous pass)
+// touched it starts on the lines still resident in the 256 MiB Infinity Cache instead of the ones evicted first:
+// conv writes z -> act reads z backwards (tail hot) and writes y backwards -> the next conv reads y forwards (head hot);
+// data-grad writes dy -> reduce reads dy, z forwards -> apply reads them backwards (tail hot) and writes dz backwards ->
+// the conv's data-grad reads dz forwards (head hot).  Default 5; same-box A/B on DMA-1536 (profiles/r03/ab_bnorder.log):
+// 0 -> 147.0 / 146.9, 3 -> 147.3 / 147.4, 5 -> 147.5 / 147.6 img/s (the tensors are 0.15-2.4 GB, so only their
+// Infinity-Cache-sized ends benefit)
+inline int bn_order() {
+  static const int o = env_knob("DMY_BN_ORDER", 5);
+  return o;
+}
 #define BN_UNROLL(KERNEL, ...)                                   \
   switch (bn_unroll()) {                                         \
     case 4: KERNEL(4, __VA_ARGS__); break;                       \
@@ -498,8 +510,8 @@ DMY_API int dmy_bn_stats(int dtype, const void* z, long zps, long M, int C, floa
   if (vec_ok(VW, C, zps, 0, 0, z, nullptr, nullptr) && C / VW <= 256) {
     const int g = vec_grid(M, C, VW);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype) bn_bwd_reduce_vec<bf16, true><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq);
-    else bn_bwd_reduce_vec<float, true><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq);
+    if (dtype) bn_bwd_reduce_vec<bf16, true><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq, 0);
+    else bn_bwd_reduce_vec<float, true><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq, 0);
     return (int)hipGetLastError();
   }
   const int P = dmy_bn_partial_rows(M);
@@ -532,10 +544,10 @@ DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scal
   const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res) && C / VW <= 256;
   if (vec) {
     const int g = vec_grid(M, C, VW);
-#define ACT_GO(U_, ...) bn_act_fwd_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C)
+#define ACT_GO(U_, ...) bn_act_fwd_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C, bn_order() & 1)
     if (dtype) { BN_UNROLL(ACT_GO, 0) }
 #undef ACT_GO
-    else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C);
+    else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C, bn_order() & 1);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);
     if (dtype) bn_act_fwd_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
@@ -571,10 +583,10 @@ DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, 0, z, dy, nullptr) && C / VW <= 256) {
     const int g = vec_grid(M, C, VW);
-#define RED_GO(U_, ...) bn_bwd_reduce_vec<bf16, false, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg)
+#define RED_GO(U_, ...) bn_bwd_reduce_vec<bf16, false, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, (bn_order() >> 1) & 1)
     if (dtype) { BN_UNROLL(RED_GO, 0) }
 #undef RED_GO
-    else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg);
+    else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, (bn_order() >> 1) & 1);
     return (int)hipGetLastError();
   }
   const int P = dmy_bn_partial_rows(M);
@@ -612,10 +624,10 @@ DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy,
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, dzps, z, dy, dz) && C / VW <= 256) {
     const int g = vec_grid(M, C, VW);
-#define APP_GO(U_, ...) bn_bwd_apply_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C)
+#define APP_GO(U_, ...) bn_bwd_apply_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C, (bn_order() >> 2) & 1)
     if (dtype) { BN_UNROLL(APP_GO, 0) }
 #undef APP_GO
-    else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C);
+    else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C, (bn_order() >> 2) & 1);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);
     if (dtype) bn_bwd_apply_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);

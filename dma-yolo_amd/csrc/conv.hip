@@ -755,22 +755,50 @@ struct WprepDesc {
   void* wt;
   int K, C, KH, KW;
 };
+// 32 (K) x 32 (C) x taps tiles through LDS: the OIHW rows are read contiguously (32 x 32 x taps floats) and both
+// copies are written 32 consecutive elements at a time (OHWI along C, IHWO along K).  The elementwise form it
+// replaces wrote the IHWO copy with a K-strided 2-byte scatter (1.59 ms per DMA-1536 step for 46 M weights).
+// Kernels with more than 9 taps (the 6 x 6 stem) take the elementwise loop.
+constexpr int kWpT = 9, kWpPitch = 32 * kWpT + 1;  // LDS row pitch (floats): odd, so the K-major reads are conflict-free
 template <typename T>
-__global__ void wprep_multi_kernel(const WprepDesc* __restrict__ d) {
+__global__ void __launch_bounds__(256) wprep_multi_kernel(const WprepDesc* __restrict__ d) {
   const WprepDesc L = d[blockIdx.y];
-  const long total = (long)L.K * L.C * L.KH * L.KW;
   T* wf = reinterpret_cast<T*>(L.wf);
   T* wt = reinterpret_cast<T*>(L.wt);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % L.C);
-    long t = i / L.C;
-    const int kw = (int)(t % L.KW);
-    t /= L.KW;
-    const int kh = (int)(t % L.KH);
-    const int k = (int)(t / L.KH);
-    const float v = L.w[(((long)k * L.C + c) * L.KH + kh) * L.KW + kw];
-    wf[i] = from_f<T>(v);
-    if (wt) wt[(((long)c * L.KH + kh) * L.KW + kw) * L.K + k] = from_f<T>(v);
+  const int taps = L.KH * L.KW;
+  if (taps > kWpT) {
+    const long total = (long)L.K * L.C * taps;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+      const int c = (int)(i % L.C);
+      const long t = i / L.C;
+      const int tap = (int)(t % taps), k = (int)(t / taps);
+      const float v = L.w[((long)k * L.C + c) * taps + tap];
+      wf[i] = from_f<T>(v);
+      if (wt) wt[((long)c * taps + tap) * L.K + k] = from_f<T>(v);
+    }
+    return;
+  }
+  __shared__ float s[32 * kWpPitch];  // [k][c * taps + tap]
+  const int tc = (L.C + 31) / 32, nt = ((L.K + 31) / 32) * tc, row = 32 * taps;
+  for (int tile = blockIdx.x; tile < nt; tile += gridDim.x) {
+    const int k0 = (tile / tc) * 32, c0 = (tile % tc) * 32;
+    const int nrow = min(32, L.C - c0) * taps;
+    for (int e = threadIdx.x; e < 32 * row; e += 256) {
+      const int kk = e / row, r = e - kk * row, k = k0 + kk;
+      s[kk * kWpPitch + r] = (k < L.K && r < nrow) ? L.w[((long)k * L.C + c0) * taps + r] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * row; e += 256) {  // OHWI: (k, tap, c), c fastest
+      const int cc = e & 31, t = e >> 5, tap = t % taps, kk = t / taps, k = k0 + kk, c = c0 + cc;
+      if (k < L.K && c < L.C) wf[((long)k * taps + tap) * L.C + c] = from_f<T>(s[kk * kWpPitch + cc * taps + tap]);
+    }
+    if (wt) {
+      for (int e = threadIdx.x; e < 32 * row; e += 256) {  // IHWO: (c, tap, k), k fastest
+        const int kk = e & 31, t = e >> 5, tap = t % taps, cc = t / taps, k = k0 + kk, c = c0 + cc;
+        if (k < L.K && c < L.C) wt[((long)c * taps + tap) * L.K + k] = from_f<T>(s[kk * kWpPitch + cc * taps + tap]);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -4360,7 +4388,7 @@ DMY_API int dmy_conv_wprep(int dtype, const float* w_oihw, void* w_ohwi, void* w
 DMY_API int dmy_conv_wprep_multi(int dtype, const void* descs, int n, void* stream) {
   if (n <= 0) return 0;
   static_assert(sizeof(WprepDesc) == 40, "WprepDesc layout is part of the C ABI");
-  const dim3 grid(64, n);
+  const dim3 grid(128, n);
   if (dtype) wprep_multi_kernel<bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const WprepDesc*)descs);
   else wprep_multi_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>((const WprepDesc*)descs);
   return (int)hipGetLastError();

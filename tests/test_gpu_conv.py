@@ -274,3 +274,20 @@ def test_halo_conv_strided_views(DG):
         assert float((ps.sum(0).double() - s1).abs().max()) < 1e-2 * (N * H * W) ** 0.5
         assert _rel(pq.sum(0), (ref.double() ** 2).sum((0, 2, 3))) < 1e-3
 
+
+
+def test_wprep_multi_matches_permutes():
+    """dmy_conv_wprep_multi (one launch for a model's weights; 32 x 32 x taps LDS tiles, elementwise for > 9 taps):
+    the OHWI and IHWO bf16 copies equal torch's permute + cast of the fp32 OIHW masters, ragged K / C included"""
+    from dmayolo.functional import WeightPrep
+    g = torch.Generator().manual_seed(5)
+    shapes = [(64, 32, 1, 1), (45, 70, 1, 1), (100, 36, 3, 3), (128, 256, 3, 3), (33, 17, 3, 3), (64, 3, 6, 6),
+              (1024, 512, 1, 1)]
+    ws = [torch.randn(s, generator=g).cuda() for s in shapes]
+    wp = WeightPrep(ws, torch.bfloat16, torch.device('cuda')).launch()
+    torch.cuda.synchronize()
+    for w in ws:
+        wf, wt = wp.get(w, torch.bfloat16)
+        K, C, KH, KW = w.shape
+        assert torch.equal(wf.view(K, KH, KW, C), w.permute(0, 2, 3, 1).bfloat16())
+        assert torch.equal(wt.view(C, KH, KW, K), w.permute(1, 2, 3, 0).bfloat16())
