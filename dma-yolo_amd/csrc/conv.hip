@@ -3007,12 +3007,12 @@ DEV u4 add_bf16x8(u4 a, u4 b) {
   return u4{o.x, o.y, o.z, o.w};
 }
 
-template <bool DG>
+template <bool DG, bool EP = false>
 __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                         bf16* __restrict__ y, float* __restrict__ psum,
                                                         float* __restrict__ psq, Geom g, int twn, int thn, int ntiles,
                                                         int per, unsigned xbytes, unsigned wbytes, unsigned ybytes,
-                                                        int accumulate) {
+                                                        int accumulate, Epi ep, unsigned rbytes) {
   __shared__ __attribute__((aligned(1024))) char smem[halo::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, px = lane & 31, hf = lane >> 5;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rw = make_rsrc(w, wbytes), ry = make_rsrc(y, ybytes);
@@ -3059,6 +3059,9 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
   issue_halo(u0, smem + halo::WBYTES);
   vm_wait<0>();
   const bool stats = psum != nullptr;
+  const bool resid = EP && ep.res != nullptr, pre = accumulate || resid;
+  const long pstride = resid ? ep.rps : g.yps;
+  const __amdgpu_buffer_rsrc_t rp = resid ? make_rsrc(ep.res, rbytes) : ry;
   f32x16 s1[2], s2[2];  // per channel block j: this lane's pixel column summed over both rows and every tile
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -3070,20 +3073,25 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
     if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
     int b, oh0, ow0;
     tile_pos(u, b, oh0, ow0);
-    unsigned mrow[2];
+    unsigned mrow[2], prow[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      mrow[i] = (unsigned)((((long)b * g.OH + oh0 + 2 * wid + i) * g.OW + ow0 + px) * g.yps);
-    u4 prev[2][2][2];  // accumulate: this lane's eight 16-B output vectors, loaded before the MFMAs
-    if (accumulate) {
+    for (int i = 0; i < 2; ++i) {
+      const long pix = ((long)b * g.OH + oh0 + 2 * wid + i) * g.OW + ow0 + px;
+      mrow[i] = (unsigned)(pix * g.yps);
+      prow[i] = (unsigned)(pix * pstride);
+    }
+    // accumulate (data-grad): this lane's eight 16-B output vectors; inference epilogue with a residual: the residual
+    // vectors at the same pixels / channels -- both loaded before the MFMAs
+    u4 prev[2][2][2];
+    if (pre) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int gq = 0; gq < 2; ++gq)
-            prev[i][j][gq] =
-                __builtin_amdgcn_raw_buffer_load_b128(ry, (mrow[i] + (unsigned)(32 * j + 16 * gq + 8 * hf)) * 2u, 0, 0);
+            prev[i][j][gq] = __builtin_amdgcn_raw_buffer_load_b128(
+                rp, (prow[i] + (unsigned)(32 * j + 16 * gq + 8 * hf)) * 2u, 0, 0);
     }
     f32x16 acc[2][2];
 #pragma unroll
@@ -3149,6 +3157,20 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
           const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
           u4 o = {r0[0], r1[0], r0[1], r1[1]};
           if (accumulate) o = add_bf16x8(o, prev[i][j][gp >> 1]);
+          if (EP) {  // eval BN scale / shift + act (+ residual) on the bf16-rounded conv output (epi_store)
+            const int n = 32 * j + 8 * gp + 8 * hf;
+            float f[8], r8[8];
+            unpack<bf16>(make_uint4(o[0], o[1], o[2], o[3]), f);
+            if (resid) unpack<bf16>(make_uint4(prev[i][j][gp >> 1][0], prev[i][j][gp >> 1][1], prev[i][j][gp >> 1][2],
+                                               prev[i][j][gp >> 1][3]), r8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float sc = ep.scale ? ep.scale[n + e] : 1.f, sh = ep.shift ? ep.shift[n + e] : 0.f;
+              f[e] = act_fwd(ep.act, f[e] * sc + sh) + (resid ? r8[e] : 0.f);
+            }
+            const uint4 q4 = pack<bf16>(f);
+            o = u4{q4.x, q4.y, q4.z, q4.w};
+          }
           const unsigned off = (mrow[i] + (unsigned)(32 * j + 8 * gp + 8 * hf)) * 2u;
           __builtin_amdgcn_raw_buffer_store_b128(o, ry, off, 0, 0);
         }
@@ -3503,14 +3525,19 @@ inline int halo_blocks(const Geom& g, int* per_out = nullptr) {
 inline int halo_rows(const Geom& g) { return v3::halo::NW * halo_blocks(g); }
 template <bool DG>
 int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, const Geom& g, hipStream_t st,
-                int acc = 0) {
+                int acc = 0, const Epi& ep = Epi{}) {
   const int thn = g.H / v3::halo::TH, twn = g.W / v3::halo::TW, nt = (int)halo_units(g);
   int per = 1;
   const int G = halo_blocks(g, &per);
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps));
   const unsigned yb = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
-  v3::conv3_halo64<DG><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb,
-                                                                  2u * 64 * 576, yb, acc);
+  const unsigned rb = ep.res != nullptr ? (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * ep.rps)) : 0u;
+  if (!DG && ep.on)  // inference epilogue: its own instantiation, so the training kernel's registers are untouched
+    v3::conv3_halo64<false, true><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per,
+                                                                           xb, 2u * 64 * 576, yb, acc, ep, rb);
+  else
+    v3::conv3_halo64<DG><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb,
+                                                                    2u * 64 * 576, yb, acc, ep, rb);
   return (int)hipGetLastError();
 }
 
@@ -3728,8 +3755,10 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
   if constexpr (sizeof(T) == 2) {
-    if (!ep.on && b == nullptr && halo_ok(g, x, w, y))
-      return launch_halo<false>((const bf16*)x, (const bf16*)w, (bf16*)y, ps, pq, g, st);
+    if (b == nullptr && halo_ok(g, x, w, y) &&
+        (!ep.on || ep.res == nullptr ||
+         (ep.rps % 8 == 0 && aligned16(ep.res) && 2.0 * ((double)g.N * g.OH * g.OW * ep.rps) < (double)v3::kBufOob)))
+      return launch_halo<false>((const bf16*)x, (const bf16*)w, (bf16*)y, ps, pq, g, st, 0, ep);
     if (conv_buf_mode() && sk_ok(g, x, w, y, ps, ep))
       return launch_sk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, st, ep);
     // small-M 1x1 layers (batch-1 inference: M < 65536): the register-epilogue GEMM on one-wave 64 x 64 tiles

@@ -275,6 +275,39 @@ def test_halo_conv_strided_views(DG):
         assert _rel(pq.sum(0), (ref.double() ** 2).sum((0, 2, 3))) < 1e-3
 
 
+@pytest.mark.parametrize('res', [False, True])
+def test_halo_conv_inference_epilogue(res):
+    """batch-1 eval forward of a 3x3 64 -> 64 layer on the halo kernel's epilogue instantiation (eval BN scale / shift
+    + SiLU (+ residual) on the bf16-rounded conv output), reading and writing channel slices of wider buffers"""
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    from dmayolo._lib import ACT_SILU
+    N, C, H, W, K = 1, 64, 384, 384, 64
+    g = torch.Generator().manual_seed(91 + res)
+    xb = torch.randn(N, 96, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    yb = torch.full((N, 80, H, W), 7.0, dtype=torch.bfloat16, device='cuda').contiguous(
+        memory_format=torch.channels_last)
+    x, y = xb[:, 16:80], yb[:, 8:72]
+    w = (torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5).cuda()
+    wf, _ = prep_weight(w, torch.bfloat16, False)
+    sc = (torch.rand(K, generator=g) + 0.5).cuda()
+    sh = (torch.randn(K, generator=g) * 0.2).cuda()
+    rb = torch.randn(N, 72, H, W, generator=g).bfloat16().cuda().contiguous(memory_format=torch.channels_last)
+    r = rb[:, 8:] if res else None
+    rc = call('dmy_conv_fwd_act', 1, ptr(x), ptr(wf), None, ptr(y), N, H, W, C, 96, K, 3, 3, 1, 1, H, W, 80, ptr(sc),
+              ptr(sh), ACT_SILU, ptr(r), 72 if res else 0, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float(), w.bfloat16().float(), padding=1)
+    z = F.silu(ref.bfloat16().float() * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1))
+    if res:
+        z = z + r.float()
+    assert _rel(y.float(), z) < 1e-2
+    bad = ((y.float() - z).abs() > 2 ** -6 * z.abs() + 1e-2).float().mean().item()
+    assert bad < 1e-3, bad
+    assert float((yb[:, :8].float() - 7).abs().max()) == 0 and float((yb[:, 72:].float() - 7).abs().max()) == 0, \
+        'slice overrun'
+
+
 
 def test_wprep_multi_matches_permutes():
     """dmy_conv_wprep_multi (one launch for a model's weights; 32 x 32 x taps LDS tiles, elementwise for > 9 taps):

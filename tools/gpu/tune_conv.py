@@ -146,7 +146,13 @@ def main():
             wsd = torch.empty(max(ne, 1), device='cuda')
             fns['wgrad_det'] = lambda: call('dmy_conv_wgrad_det', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s,
                                             p, OH, OW, K, 0, ptr(wsd), ne, stream())
+        if 'mm' in kinds and k == 1:  # vendor GEMM of the same 1x1 problem (torch.matmul -> hipBLASLt), a reference point only
+            a2, b2 = x.permute(0, 2, 3, 1).reshape(-1, C), wf.view(K, C).t()
+            y2 = torch.empty(a2.shape[0], K, dtype=torch.bfloat16, device='cuda')
+            fns['mm'] = lambda: torch.matmul(a2, b2, out=y2)
         for kind in kinds:
+            if kind == 'mm' and k != 1:
+                continue
             us = bench(fns[kind])
             print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s '
                   f'{by / us / 1e3:7.0f} GB/s', flush=True)
