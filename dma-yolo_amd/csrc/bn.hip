@@ -139,14 +139,14 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
       if (m + u * S >= M) break;
       float f[VW];
       unpack<T>(zv[u], f);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] = f[j] * sc[j] + sh[j];
+      act_fwd_n<VW>(act, f);
       if (res) {
         float r[VW];
         unpack<T>(rv[u], r);
 #pragma unroll
-        for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < VW; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+        for (int j = 0; j < VW; ++j) f[j] += r[j];
       }
       *reinterpret_cast<uint4*>(y + mu * yps + c0) = pack<T>(f);
     }
@@ -186,14 +186,14 @@ __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restri
     for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
       float f[8];
       unpack<bf16>(*reinterpret_cast<const uint4*>(z + m * zps + c0), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+      act_fwd_n<8>(act, f);
       if (res) {
         float r[8];
         unpack<bf16>(*reinterpret_cast<const uint4*>(res + m * rps + c0), r);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]) + r[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = act_fwd(act, f[j] * sc[j] + sh[j]);
+        for (int j = 0; j < 8; ++j) f[j] += r[j];
       }
       const uint4 v = pack<bf16>(f);
       *reinterpret_cast<uint4*>(y + m * yps + c0) = v;
@@ -268,13 +268,20 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
         float zf[VW], gf[VW];
         unpack<T>(zv[u], zf);
         if (!STATS) unpack<T>(gv[u], gf);
+        if (STATS) {  // plain column sums of z and z^2 (batch statistics / bias gradients)
 #pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          if (STATS) {  // plain column sums of z and z^2 (batch statistics / bias gradients)
+          for (int j = 0; j < VW; ++j) {
             a[j] += zf[j];
             b[j] += zf[j] * zf[j];
-          } else {
-            const float du = gf[j] * act_grad(act, zf[j] * sc[j] + sh[j]);
+          }
+        } else {
+          float ag[VW];
+#pragma unroll
+          for (int j = 0; j < VW; ++j) ag[j] = zf[j] * sc[j] + sh[j];
+          act_grad_n<VW>(act, ag);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const float du = gf[j] * ag[j];
             a[j] += du;
             b[j] += du * (zf[j] - mu[j]) * is[j];
           }
@@ -344,7 +351,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z,
       unpack<T>(zv[u], zf);
       unpack<T>(gv[u], gf);
 #pragma unroll
-      for (int j = 0; j < VW; ++j) o[j] = k1[j] * (gf[j] * act_grad(act, zf[j] * sc[j] + sh[j])) + k0[j] + k2[j] * zf[j];
+      for (int j = 0; j < VW; ++j) o[j] = zf[j] * sc[j] + sh[j];
+      act_grad_n<VW>(act, o);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) o[j] = k1[j] * (gf[j] * o[j]) + k0[j] + k2[j] * zf[j];
       *reinterpret_cast<uint4*>(dz + mu * dzps + c0) = pack<T>(o);
     }
   }

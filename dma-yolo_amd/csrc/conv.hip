@@ -196,8 +196,56 @@ struct Epi {
   int on;
 };
 
+// eval coefficients of the 8 consecutive channels n .. n + 7 (all < K): 16-B loads when the arrays are 16-B aligned
+// (n % 8 == 0 at every call), scale 1 / shift 0 when absent
+DEV void epi_coef8(const Epi& ep, int n, float (&sc)[8], float (&sh)[8]) {
+  const bool vs = (((uintptr_t)ep.scale | (uintptr_t)ep.shift) & 15) == 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float4 a = make_float4(1.f, 1.f, 1.f, 1.f), b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vs) {
+      if (ep.scale) a = *reinterpret_cast<const float4*>(ep.scale + n + 4 * h);
+      if (ep.shift) b = *reinterpret_cast<const float4*>(ep.shift + n + 4 * h);
+    } else {
+      if (ep.scale) a = make_float4(ep.scale[n + 4 * h], ep.scale[n + 4 * h + 1], ep.scale[n + 4 * h + 2], ep.scale[n + 4 * h + 3]);
+      if (ep.shift) b = make_float4(ep.shift[n + 4 * h], ep.shift[n + 4 * h + 1], ep.shift[n + 4 * h + 2], ep.shift[n + 4 * h + 3]);
+    }
+    sc[4 * h] = a.x; sc[4 * h + 1] = a.y; sc[4 * h + 2] = a.z; sc[4 * h + 3] = a.w;
+    sh[4 * h] = b.x; sh[4 * h + 1] = b.y; sh[4 * h + 2] = b.z; sh[4 * h + 3] = b.w;
+  }
+}
+// f = act(f * sc + sh) (+ r) over 8 values, the activation switch outside the element loop (act_fwd_n)
+DEV void epi_apply8(int act, float (&f)[8], const float (&sc)[8], const float (&sh)[8], const float* r) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
+  act_fwd_n<8>(act, f);
+  if (r != nullptr) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += r[e];
+  }
+}
+
 template <typename T, int VW>
 DEV void epi_store(const Epi& ep, const T* src, T* dst, int n, int K, long m, bool full) {
+  if constexpr (sizeof(T) == 2 && VW == 8) {
+    if (full) {  // 8 channels of a bf16 row: vector coefficient / residual loads, one hoisted activation switch
+      float f[8], sc[8], sh[8], r8[8];
+      unpack<T>(*reinterpret_cast<const uint4*>(src), f);
+      epi_coef8(ep, n, sc, sh);
+      const T* rp = ep.res != nullptr ? reinterpret_cast<const T*>(ep.res) + m * ep.rps + n : nullptr;
+      if (rp != nullptr) {
+        if ((((uintptr_t)rp) & 15) == 0) {
+          unpack<T>(*reinterpret_cast<const uint4*>(rp), r8);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r8[j] = to_f(rp[j]);
+        }
+      }
+      epi_apply8(ep.act, f, sc, sh, rp != nullptr ? r8 : nullptr);
+      *reinterpret_cast<uint4*>(dst) = pack<T>(f);
+      return;
+    }
+  }
   float f[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) {
@@ -1205,9 +1253,13 @@ DEV void store_dgrad_bn(bf16* ct, bf16* __restrict__ y, int accumulate, const Ge
         float f[8], zf[8];
         unpack<bf16>(v, f);
         unpack<bf16>(zv[q], zf);
+        float ag[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ag[j] = zf[j] * sc[j] + sh[j];
+        act_grad_n<8>(bb.act, ag);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float du = f[j] * act_grad(bb.act, zf[j] * sc[j] + sh[j]);
+          const float du = f[j] * ag[j];
           sa[j] += du;
           sb[j] += du * (zf[j] - mu[j]) * is[j];
         }
@@ -1629,15 +1681,11 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
           u4 rv = {0u, 0u, 0u, 0u};
           if (ep.res != nullptr)
             rv = __builtin_amdgcn_raw_buffer_load_b128(rr, (m < M && n < g.K) ? (unsigned)((m * ep.rps + n) * 2) : kBufOob, 0, 0);
-          float f[8], r8[8];
+          float f[8], r8[8], sc[8], sh[8];
           unpack<bf16>(make_uint4(v[0], v[1], v[2], v[3]), f);
           unpack<bf16>(make_uint4(rv[0], rv[1], rv[2], rv[3]), r8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int c = n + e < g.K ? n + e : 0;
-            const float sc = ep.scale ? ep.scale[c] : 1.f, sh = ep.shift ? ep.shift[c] : 0.f;
-            f[e] = act_fwd(ep.act, f[e] * sc + sh) + (ep.res != nullptr ? r8[e] : 0.f);
-          }
+          epi_coef8(ep, n < g.K ? n : 0, sc, sh);  // K % 8 == 0 here: a live vector has all 8 channels
+          epi_apply8(ep.act, f, sc, sh, ep.res != nullptr ? r8 : nullptr);
           const uint4 o = pack<bf16>(f);
           v = u4{o.x, o.y, o.z, o.w};
         }
@@ -3013,7 +3061,13 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
                                                         float* __restrict__ psq, Geom g, int twn, int thn, int ntiles,
                                                         int per, unsigned xbytes, unsigned wbytes, unsigned ybytes,
                                                         int accumulate, Epi ep, unsigned rbytes) {
-  __shared__ __attribute__((aligned(1024))) char smem[halo::LDS];
+  // the eval instantiation keeps the 64 channels' scale / shift after the ring (512 B, written before the first barrier)
+  __shared__ __attribute__((aligned(1024))) char smem[halo::LDS + (EP ? 512 : 0)];
+  if (EP && threadIdx.x < 128) {
+    const int c = threadIdx.x & 63;
+    const float* src = threadIdx.x < 64 ? ep.scale : ep.shift;
+    reinterpret_cast<float*>(smem + halo::LDS)[threadIdx.x] = src != nullptr ? src[c] : (threadIdx.x < 64 ? 1.f : 0.f);
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, px = lane & 31, hf = lane >> 5;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rw = make_rsrc(w, wbytes), ry = make_rsrc(y, ybytes);
   char* const wl = smem;
@@ -3159,15 +3213,18 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
           if (accumulate) o = add_bf16x8(o, prev[i][j][gp >> 1]);
           if (EP) {  // eval BN scale / shift + act (+ residual) on the bf16-rounded conv output (epi_store)
             const int n = 32 * j + 8 * gp + 8 * hf;
-            float f[8], r8[8];
+            float f[8], r8[8], sc[8], sh[8];
             unpack<bf16>(make_uint4(o[0], o[1], o[2], o[3]), f);
             if (resid) unpack<bf16>(make_uint4(prev[i][j][gp >> 1][0], prev[i][j][gp >> 1][1], prev[i][j][gp >> 1][2],
                                                prev[i][j][gp >> 1][3]), r8);
+            const float4* cf = reinterpret_cast<const float4*>(smem + halo::LDS) + n / 4;  // [scale 64 | shift 64]
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float sc = ep.scale ? ep.scale[n + e] : 1.f, sh = ep.shift ? ep.shift[n + e] : 0.f;
-              f[e] = act_fwd(ep.act, f[e] * sc + sh) + (resid ? r8[e] : 0.f);
+            for (int h = 0; h < 2; ++h) {
+              const float4 a = cf[h], b = cf[16 + h];
+              sc[4 * h] = a.x; sc[4 * h + 1] = a.y; sc[4 * h + 2] = a.z; sc[4 * h + 3] = a.w;
+              sh[4 * h] = b.x; sh[4 * h + 1] = b.y; sh[4 * h + 2] = b.z; sh[4 * h + 3] = b.w;
             }
+            epi_apply8(ep.act, f, sc, sh, resid ? r8 : nullptr);
             const uint4 q4 = pack<bf16>(f);
             o = u4{q4.x, q4.y, q4.z, q4.w};
           }
@@ -3456,6 +3513,11 @@ inline int p1p_small() {
   static const int t = env_int("DMY_P1P_SMALL", 0);
   return t;
 }
+// eval forwards (inference epilogue) on conv_p1p too: DMY_P1P_EP = 0 off, 1 on
+inline int p1p_eval() {
+  static const int t = env_int("DMY_P1P_EP", 0);
+  return t;
+}
 inline int p1p_maxn() {
   static const int t = env_int("DMY_P1P_MAXN", 256);
   return t;
@@ -3572,7 +3634,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       else V3_GO(BM, BN, NS, false, 0);                      \
     }                                                        \
   }
-  if (p1 && buf && p1p_mode() && tov < 0 && bb.z == nullptr && !ep.on) {  // persistent 1x1, register epilogue
+  if (p1 && buf && p1p_mode() && tov < 0 && bb.z == nullptr && (!ep.on || p1p_eval())) {  // persistent 1x1
     const int r = launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes, ep);
     if (r >= 0) return r;
   }
