@@ -120,8 +120,8 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
   if (!rm.active()) return;
   const int c0 = rm.cv * VW;
   float sc[VW], sh[VW];
-#pragma unroll
-  for (int j = 0; j < VW; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  ldf<VW>(scale + c0, sc);
+  ldf<VW>(shift + c0, sh);
   const long S = (long)gridDim.x * rm.RB;
   for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {
     uint4 zv[U], rv[U];
@@ -181,8 +181,8 @@ __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restri
   if (rm.active()) {
     const int c0 = rm.cv * 8;
     float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+    ldf<8>(scale + c0, sc);
+    ldf<8>(shift + c0, sh);
     for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += (long)gridDim.x * rm.RB) {
       float f[8];
       unpack<bf16>(*reinterpret_cast<const uint4*>(z + m * zps + c0), f);
@@ -244,12 +244,19 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec(const T* __restrict__ z
   for (int j = 0; j < VW; ++j) { a[j] = 0.f; b[j] = 0.f; }
   if (rm.active()) {
     float sc[VW], sh[VW], mu[VW], is[VW];
+    if (STATS) {
 #pragma unroll
-    for (int j = 0; j < VW; ++j) {
-      sc[j] = STATS ? 1.f : scale[c0 + j];
-      sh[j] = STATS ? 0.f : shift[c0 + j];
-      mu[j] = STATS ? 0.f : mean[c0 + j];
-      is[j] = STATS ? 1.f : invstd[c0 + j];
+      for (int j = 0; j < VW; ++j) {
+        sc[j] = 1.f;
+        sh[j] = 0.f;
+        mu[j] = 0.f;
+        is[j] = 1.f;
+      }
+    } else {
+      ldf<VW>(scale + c0, sc);
+      ldf<VW>(shift + c0, sh);
+      ldf<VW>(mean + c0, mu);
+      ldf<VW>(invstd + c0, is);
     }
     const long S = (long)gridDim.x * rm.RB;
     for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {
@@ -322,15 +329,19 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec(const T* __restrict__ z,
   RowMap rm(C, VW);
   if (!rm.active()) return;
   const int c0 = rm.cv * VW;
-  float sc[VW], sh[VW], k1[VW], k0[VW], k2[VW];
+  float sc[VW], sh[VW], k1[VW], k0[VW], k2[VW], t0[VW], t1[VW];
+  ldf<VW>(scale + c0, sc);
+  ldf<VW>(shift + c0, sh);
+  ldf<VW>(ca + c0, k1);
+  ldf<VW>(cc + c0, k2);
+  ldf<VW>(invstd + c0, t0);
+  ldf<VW>(cb + c0, k0);
+  ldf<VW>(mean + c0, t1);
 #pragma unroll
   for (int j = 0; j < VW; ++j) {
-    sc[j] = scale[c0 + j];
-    sh[j] = shift[c0 + j];
     // dz = ca*du + cb + cc*(z - mean)*invstd = ca*du + k0 + k2*z
-    k1[j] = ca[c0 + j];
-    k2[j] = cc[c0 + j] * invstd[c0 + j];
-    k0[j] = cb[c0 + j] - k2[j] * mean[c0 + j];
+    k2[j] = k2[j] * t0[j];
+    k0[j] = k0[j] - k2[j] * t1[j];
   }
   const long S = (long)gridDim.x * rm.RB;
   for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S * U) {

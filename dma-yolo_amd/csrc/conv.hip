@@ -1215,12 +1215,12 @@ DEV void store_dgrad_bn(bf16* ct, bf16* __restrict__ y, int accumulate, const Ge
   const bool colok = n < g.K;
   float sc[8], sh[8], mu[8], is[8], sa[8], sb[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = colok ? bb.scale[n + j] : 0.f;
-    sh[j] = colok ? bb.shift[n + j] : 0.f;
-    mu[j] = colok ? bb.mean[n + j] : 0.f;
-    is[j] = colok ? bb.invstd[n + j] : 0.f;
-    sa[j] = sb[j] = 0.f;
+  for (int j = 0; j < 8; ++j) sc[j] = sh[j] = mu[j] = is[j] = sa[j] = sb[j] = 0.f;
+  if (colok) {  // K % 8 == 0 on this path: a live column vector has all 8 channels
+    ldf<8>(bb.scale + n, sc);
+    ldf<8>(bb.shift + n, sh);
+    ldf<8>(bb.mean + n, mu);
+    ldf<8>(bb.invstd + n, is);
   }
   // rows in groups of HALF iterations: every z (and accumulate) load of a group is issued before any is consumed,
   // so a thread keeps HALF 16-B loads in flight instead of one dependent load per row

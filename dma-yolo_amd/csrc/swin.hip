@@ -126,11 +126,23 @@ __global__ void __launch_bounds__(256) ln_fwd_vec(const T* __restrict__ x, long 
   const int lane = threadIdx.x & 63, sub = lane % L, rw = lane / L;
   const int c0 = sub * VW;
   const bool on = c0 < C;
+  // gamma / beta of this lane's VW channels: 16-B loads (the scalar form was 2 x VW loads per wave, a wave's whole
+  // VMEM stream at batch-1 sizes where it handles one row: 19.4 us for 18.9 MB, 3.5 us for a copy of it)
   float wv[VW], bv[VW];
+  if (((((uintptr_t)w) | ((uintptr_t)b)) & 15) == 0) {
 #pragma unroll
-  for (int j = 0; j < VW; ++j) {
-    wv[j] = on ? w[c0 + j] : 0.f;
-    bv[j] = on ? b[c0 + j] : 0.f;
+    for (int j = 0; j < VW; j += 4) {
+      const float4 a = on ? *reinterpret_cast<const float4*>(w + c0 + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 e = on ? *reinterpret_cast<const float4*>(b + c0 + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = a.x; wv[j + 1] = a.y; wv[j + 2] = a.z; wv[j + 3] = a.w;
+      bv[j] = e.x; bv[j + 1] = e.y; bv[j + 2] = e.z; bv[j + 3] = e.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      wv[j] = on ? w[c0 + j] : 0.f;
+      bv[j] = on ? b[c0 + j] : 0.f;
+    }
   }
   const long rpb = (long)(blockDim.x >> 6) * RPW;
   for (long mb = (long)blockIdx.x * rpb; mb < M; mb += (long)gridDim.x * rpb) {
@@ -183,10 +195,11 @@ __global__ void __launch_bounds__(256) ln_bwd_vec(const T* __restrict__ x, long 
   float wv[VW], aw[VW], ab[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) {
-    wv[j] = on ? w[c0 + j] : 0.f;
+    wv[j] = 0.f;
     aw[j] = 0.f;
     ab[j] = 0.f;
   }
+  if (on) ldf<VW>(w + c0, wv);
   const long rpb = (long)(blockDim.x >> 6) * RPW;
   for (long mb = (long)blockIdx.x * rpb; mb < M; mb += (long)gridDim.x * rpb) {
     const long m = mb + (threadIdx.x >> 6) * RPW + rw;

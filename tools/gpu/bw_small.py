@@ -19,9 +19,10 @@ def graph_time(fn, n=50):
         best = min(best, e0.elapsed_time(e1) / n * 1e3)
     return best
 
-for mb in (1.2, 4.7, 9.4, 18.9, 37.7, 75.5, 302):
-    n = int(mb * 1e6 / 2)
-    a = torch.empty(n, dtype=torch.bfloat16, device='cuda').normal_()
-    b = torch.empty_like(a)
-    us = graph_time(lambda: b.copy_(a))
-    print(f'copy {mb:7.1f} MB: {us:8.1f} us  {2 * mb * 1e6 / us / 1e3:7.0f} GB/s (read + write)', flush=True)
+if __name__ == "__main__":
+  for mb in (1.2, 4.7, 9.4, 18.9, 37.7, 75.5, 302):
+      n = int(mb * 1e6 / 2)
+      a = torch.empty(n, dtype=torch.bfloat16, device='cuda').normal_()
+      b = torch.empty_like(a)
+      us = graph_time(lambda: b.copy_(a))
+      print(f'copy {mb:7.1f} MB: {us:8.1f} us  {2 * mb * 1e6 / us / 1e3:7.0f} GB/s (read + write)', flush=True)
