@@ -2106,10 +2106,23 @@ __global__ void __launch_bounds__(256) conv_sk(const bf16* __restrict__ x, const
 // writes its fp32 partial tile to a workspace slab, splitk_epi_kernel sums the slabs in split order and applies
 // bias + the inference epilogue (eval BN, act, residual) to the bf16-rounded sum -- the same value contract as
 // the one-launch path (deterministic; rounding order differs from the unsplit kernel).
+//
+// In-launch combine (fused = 1): the block that draws the last ticket of its tile sums the tile's slabs in split order and
+// applies the epilogue itself -- splitk_epi_kernel's arithmetic, so the same bits -- instead of a second launch reading
+// every slab back (MI355X_MICROARCH / cdna_hip_programming split-K recipe: plain slab stores, vmcnt drain, barrier, ONE
+// lane's agent-scope release + drain before a relaxed agent ticket; the reducer's one lane acquires at agent scope, drains,
+// and the barrier covers the workgroup; any XCD placement of a tile's splits is correct).  The tickets live in a device
+// array zeroed at load and re-zeroed by each tile's reducer, so launches that use it must not run concurrently on two
+// streams (the eval forward is one stream).
+constexpr int kSplitCnt = 8192;
+__device__ int g_split_cnt[kSplitCnt];
+
 template <int BM, int BN, int NS, bool P1>
 __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                                float* __restrict__ ws, Geom g, int gm, int gn, int per,
-                                                               unsigned xbytes, unsigned wbytes) {
+                                                               unsigned xbytes, unsigned wbytes, int fused,
+                                                               const float* __restrict__ bias, bf16* __restrict__ y,
+                                                               Epi ep) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2142,6 +2155,46 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __res
         const int n = n0 + wn * 64 + j * 16 + (lane & 15);
         if (m < M && n < g.K) slab[m * g.K + n] = acc[i][j][r];
       }
+  if (!fused) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores drained; the ring is idle, so smem carries the reducer flag
+  int* flag = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&g_split_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (int)gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&g_split_cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  // this tile's outputs: the slabs summed in split order, + bias, rounded to bf16, epilogue (splitk_epi_kernel's math)
+  constexpr int CPR = BN / 8, NTH = BM * BN / 64;
+  const int sp = (int)gridDim.y;
+  for (int e = threadIdx.x; e < BM * CPR; e += NTH) {
+    const int row = e / CPR, c = n0 + (e % CPR) * 8;
+    const long m = m0 + row;
+    if (m >= M || c >= g.K) continue;
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    for (int q = 0; q < sp; ++q) {
+      const float4* src = reinterpret_cast<const float4*>(ws + ((long)q * M + m) * g.K + c);
+      const float4 a = src[0], b = src[1];
+      f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
+      f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+    }
+    bf16 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = __float2bfloat16(f[j] + (bias != nullptr ? bias[c + j] : 0.f));
+    if (ep.on) epi_store<bf16, 8>(ep, t, y + m * g.yps + c, c, g.K, m, true);
+    else *reinterpret_cast<uint4*>(y + m * g.yps + c) = *reinterpret_cast<const uint4*>(t);
+  }
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
@@ -3746,14 +3799,19 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * g.KH * g.KW * g.C);
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
   const dim3 grid((unsigned)gm * gn, (unsigned)sp);
+  // DMY_SPLITK_FUSED = 1: the in-launch combine (conv_fwd_split's last-ticket reducer), 0 (default until measured on
+  // the box): splitk_epi_kernel
+  static const int fz = env_int("DMY_SPLITK_FUSED", 0);
+  const int fused = fz && gm * gn <= v3::kSplitCnt ? 1 : 0;
   if (g.K > 64) {
-    if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
-    else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
+    else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
   } else {
-    if (p1) v3::conv_fwd_split<128, 64, 2, true><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
-    else v3::conv_fwd_split<128, 64, 2, false><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    if (p1) v3::conv_fwd_split<128, 64, 2, true><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
+    else v3::conv_fwd_split<128, 64, 2, false><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
   }
-  splitk_epi_kernel<<<grid_cap(ceil_div(M * (g.K / 8), 256), 4096), 256, 0, st>>>(ws, sp, M, g.K, b, y, g.yps, ep);
+  if (!fused)
+    splitk_epi_kernel<<<grid_cap(ceil_div(M * (g.K / 8), 256), 4096), 256, 0, st>>>(ws, sp, M, g.K, b, y, g.yps, ep);
   return (int)hipGetLastError();
 }
 

@@ -656,7 +656,6 @@ __global__ void __launch_bounds__(64 * NW, 2) winattn_fwd_mfma(const bf16* __res
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int head = xhead(g.nh), grp = xgroup(g.nh);
   const int il = lane & 15, gq = lane >> 4;
-  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) tab[e] = table[e * g.nh + head];
   const int nwr = g.Rp / WS, nwc = g.Cp / WS;
   bf16* Vs = sm + w * (MATQ + MATP);
   bf16* Ps = Vs + MATQ;
@@ -674,8 +673,11 @@ __global__ void __launch_bounds__(64 * NW, 2) winattn_fwd_mfma(const bf16* __res
       for (int m = 0; m < 3; ++m) pre[m][i] = ppre[i] >= 0 ? src[m * (g.C / 8)] : make_uint4(0, 0, 0, 0);
     }
   };
-  __syncthreads();  // tab staged; the per-wave buffers below need no block barrier
+  // the first window's Q / K / V loads go out before the bias-table gather, so the two share one memory round trip
+  // (at batch 1 a block runs one or two windows and this prologue is most of its time)
   if (w0 + w < w1) fetch(w0 + w);
+  for (int e = threadIdx.x; e < NTAB; e += blockDim.x) tab[e] = table[e * g.nh + head];
+  __syncthreads();  // tab staged; the per-wave buffers below need no block barrier
   for (int wid = w0 + w; wid < w1; wid += NW) {
     const int wr = (wid / nwc) % nwr, wc = wid % nwc;
     bf16x8 qf[4], kf[4];

@@ -148,6 +148,14 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
         z = ref.bfloat16().float()  # the epilogue acts on the bf16-rounded conv output
         ref = F.silu(z * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1)) + res.float()
     assert _rel(y.float(), ref) < 1e-2
+    # the in-launch combine sums the slabs in split order whichever block draws the last ticket: 20 launches on a
+    # NaN-filled workspace give the same bits every time
+    first = y.clone()
+    for i in range(20):
+        ws.fill_(float('nan'))  # a reducer that read a slab before its producer's stores were visible would show NaN
+        call('dmy_conv_fwd_act_ws', 1, ptr(xd), ptr(wf), ptr(b.cuda()), ptr(y), *geo, ptr(sc), ptr(sh),
+             ACT_SILU if epi else 0, ptr(res), K if epi else 0, ptr(ws), ne, stream())
+        assert torch.equal(y, first), i
 
 
 def test_conv_fwd_1x1_small_m_unsplit():
