@@ -3799,8 +3799,9 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * g.KH * g.KW * g.C);
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
   const dim3 grid((unsigned)gm * gn, (unsigned)sp);
-  // DMY_SPLITK_FUSED = 1: the in-launch combine (conv_fwd_split's last-ticket reducer), 0 (default until measured on
-  // the box): splitk_epi_kernel
+  // DMY_SPLITK_FUSED = 1: the in-launch combine (conv_fwd_split's last-ticket reducer), 0 (default): splitk_epi_kernel.
+  // Measured SLOWER on the bs1 detect (profiles/r03/det_splitk_fused_ab.log: DMA-1536 4.52 -> 5.19 ms, yolov5s 0.79 ->
+  // 1.17 ms): 256 KB of slabs per tile read serially by one reducer block + a release per block
   static const int fz = env_int("DMY_SPLITK_FUSED", 0);
   const int fused = fz && gm * gn <= v3::kSplitCnt ? 1 : 0;
   if (g.K > 64) {
