@@ -29,6 +29,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'dma-yolo_amd'))
 sys.path.insert(0, ROOT)
 
+if os.environ.get('DMY_SEGV_REPORT'):  # diagnostic fault reporter (tools/segv/segv_report.c): PC / address / maps
+    import ctypes
+    ctypes.CDLL(os.path.join(ROOT, 'tools', 'segv', 'libsegv_report.so')).segv_report_install()
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -63,6 +67,12 @@ def parse():
                     'shape, algorithmic flops / bytes, measured us, roofline us): the table behind roofline.frac')
     ap.add_argument('--fp8', action='store_true',
                     help='config 5 (BASELINE configs[4]): e4m3 MFMA forward for every conv with C %% 128 == 0')
+    ap.add_argument('--ddp', default='arena', choices=['arena', 'torch'],
+                    help='N > 1 gradient exchange: the arena reducer (dmayolo.ddp.ArenaDDP: bucketed AVG all-reduce of '
+                         'slices of the weight-gradient arena, overlapped with backward) or torch DDP')
+    ap.add_argument('--bucket-mb', type=float, default=32.0, help='ArenaDDP bucket size (first bucket 4 MB)')
+    ap.add_argument('--grad-compress', default='none', choices=['none', 'bf16'],
+                    help='ArenaDDP: send the gradient buckets as bf16 (DDP bf16_compress_hook semantics)')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='process-group backend (nccl = RCCL; gloo only to rehearse several ranks on one GPU)')
     return ap.parse_args()
@@ -144,7 +154,26 @@ def cpu_baseline(cfg, seconds):
         if (el > seconds and n >= 2) or n >= 2000:
             break
     return dict(value=n / el, unit='images/s', cores=torch.get_num_threads(), kind='port',
-                sample=f'{n} bs1 train steps of {yml} @{img} (fp32 CPU oracle, {el:.1f} s)')
+                sample=f'{n} bs1 train steps of {yml} @{img} (fp32 CPU oracle, {el:.1f} s)', **host_cpu())
+
+
+def host_cpu():
+    """the host CPU the baseline ran on: model name (lscpu's 'Model name' = /proc/cpuinfo 'model name'), the logical
+    CPUs this process may run on, and the machine's total"""
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.lower().startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return dict(cpu_model=model, cpus_available=avail, cpus_machine=os.cpu_count())
 
 
 def write_launch_table(path, table, ks, cfg_name):
@@ -216,7 +245,10 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     torch.cuda.reset_peak_memory_stats(device)
     model = build(cfg, dtype, device, fp8=fp8)
     net = model
-    if world > 1:  # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
+    if world > 1 and a.ddp == 'arena':  # buckets = slices of the gradient arena (dmayolo/ddp.py)
+        from dmayolo.ddp import ArenaDDP
+        net = ArenaDDP(model, bucket_cap_mb=a.bucket_mb, compress=None if a.grad_compress == 'none' else a.grad_compress)
+    elif world > 1:  # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
         fu = any(isinstance(m, torch.nn.MultiheadAttention) for m in model.modules())
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev_idx], output_device=dev_idx,
                                                         find_unused_parameters=fu)
@@ -269,7 +301,10 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     assert torch.isfinite(loss).all(), 'non-finite loss'
     res = dict(value=round(world * bs * a.steps / el, 2), unit='images/s', ms_per_step=round(el / a.steps * 1e3, 3),
                config={'workload': f'{yml} train @{img} nc={nc}', 'model': yml, 'global_batch': total_bs, 'img': img,
-                       'parallelism': f'dp{world}'},
+                       'parallelism': f'dp{world}',
+                       **({'grad_exchange': (a.ddp + ('' if a.ddp == 'torch' else ' bucket %g MB' % a.bucket_mb) +
+                                             ('' if a.grad_compress == 'none' else ' ' + a.grad_compress))}
+                          if world > 1 else {})},
                roofline=roofline(ks, a.steps, el_events, dtype, name),
                loss_items=[round(float(v), 5) for v in items], lr=[round(float(g['lr']), 8) for g in tr.optimizer.param_groups],
                loss_scale=tr.scaler.get_scale())

@@ -223,6 +223,7 @@ class Model(nn.Module):
         prev = Fn.WgradArena.current, Fn.WeightPrep.current
         if arena:
             Fn.WgradArena.current = self._wgrad_arena()
+            self._last_arena = weakref.ref(Fn.WgradArena.current)  # ddp.ArenaDDP all-reduces slices of it
             Fn.WeightPrep.current = self._weight_prep(x.device).launch()
         fan = self._fanout() if _MODEL_SINKS and torch.is_grad_enabled() and self.training else {}
         sinks = {}

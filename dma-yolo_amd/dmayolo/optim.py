@@ -100,8 +100,31 @@ class FusedSGD(torch.optim.Optimizer):
 
 
 class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam semantics with the step count on the device.  The count is a per-parameter quantity in torch
+    (a parameter whose gradient first appears later starts at t = 0); here parameters that started together share one
+    device int32 counter (a cohort), and each cohort of a group is one kernel launch -- normally one per group.  The
+    counters live in the optimizer (not in param_groups / state), and state_dict() stores torch's format: a float32
+    CPU 'step' per parameter, from which load_state_dict + the next step() rebuild the counters on the parameters'
+    device (a checkpoint loaded with map_location='cpu' works)."""
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._ctr = {}  # id(param) -> its cohort's device int32 counter
+
+    def _counter(self, p, fresh):
+        """the device counter of parameter p; `fresh` (t0, device) -> counter shares new counters per start count"""
+        c = self._ctr.get(id(p))
+        if c is not None and c.device == p.device:
+            return c
+        st = self.state[p]
+        s = st.get('step')
+        t0 = int(float(c.item() if c is not None else s.item() if torch.is_tensor(s) else s)) \
+            if (c is not None or s is not None) else 0
+        key = (t0, p.device)
+        if key not in fresh:
+            fresh[key] = torch.full((1,), t0, dtype=torch.int32, device=p.device)
+        c = self._ctr[id(p)] = fresh[key]
+        return c
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -109,28 +132,46 @@ class FusedAdam(torch.optim.Optimizer):
             ps = [p for p in g['params'] if p.grad is not None]
             if not ps:
                 continue
-            ms, vs = [], []
-            step = g.get('_dstep')
-            if step is None:  # the group's step count lives on the device (one int32 shared by its params' state)
-                t0 = max((int(self.state[p]['step']) for p in ps if 'step' in self.state[p]), default=0)
-                step = g['_dstep'] = torch.full((1,), t0, dtype=torch.int32, device=ps[0].device)
+            fresh, cohorts = {}, {}
             for p in ps:
                 st = self.state[p]
                 if 'exp_avg' not in st:
                     st['exp_avg'] = torch.zeros_like(p)
                     st['exp_avg_sq'] = torch.zeros_like(p)
-                st['step'] = step  # torch keeps Adam's step as a tensor too; read it (host sync) only to log
-                ms.append(st['exp_avg'])
-                vs.append(st['exp_avg_sq'])
+                c = self._counter(p, fresh)
+                st['step'] = c  # torch keeps Adam's step as a tensor too; read it (host sync) only to log / save
+                cohorts.setdefault(id(c), (c, []))[1].append(p)
             b1, b2 = g['betas']
-            tb = _Table.get([ps, [p.grad for p in ps], ms, vs], ps[0].device)
             PARAM_GEN[0] += 1
-            # bias corrections from the device count (t = count + 1), which the kernel advances unless the GradScaler
-            # found a non-finite gradient: a skipped step leaves t alone, as torch (scaler.step skips optimizer.step)
-            _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
-                                float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
-                                0.0, 0.0, *_amp_ptrs(self), ctypes.c_void_p(step.data_ptr()), stream()), 'dmy_adam')
+            for c, cp in cohorts.values():
+                st = [self.state[p] for p in cp]
+                tb = _Table.get([cp, [p.grad for p in cp], [s['exp_avg'] for s in st], [s['exp_avg_sq'] for s in st]],
+                                cp[0].device)
+                # bias corrections from the device count (t = count + 1), which the kernel advances unless the
+                # GradScaler found a non-finite gradient: a skipped step leaves t alone, as torch (scaler.step skips
+                # optimizer.step)
+                _check(lib.dmy_adam(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.p(4), tb.p(5), tb.p(6), tb.nchunks,
+                                    float(g['lr']), float(b1), float(b2), float(g['eps']), float(g['weight_decay']),
+                                    0.0, 0.0, *_amp_ptrs(self), ctypes.c_void_p(c.data_ptr()), stream()), 'dmy_adam')
         return None
+
+    def state_dict(self):
+        sd = super().state_dict()
+        order = [p for g in self.param_groups for p in g['params']]
+        for i, p in enumerate(order):
+            ent = sd['state'].get(i)
+            if ent is not None and torch.is_tensor(ent.get('step')):
+                ent = sd['state'][i] = dict(ent)
+                ent['step'] = torch.tensor(float(ent['step'].item()), dtype=torch.float32)  # torch Adam's format
+        for g in sd['param_groups']:
+            g.pop('_dstep', None)
+        return sd
+
+    def load_state_dict(self, state_dict):
+        for g in state_dict.get('param_groups', []):
+            g.pop('_dstep', None)  # checkpoints of the earlier format kept the counter in the group
+        super().load_state_dict(state_dict)
+        self._ctr = {}  # rebuilt from state['step'] on the parameters' device at the next step()
 
 
 class GradScaler:

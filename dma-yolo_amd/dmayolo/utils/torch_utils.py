@@ -8,8 +8,10 @@ import torch.nn as nn
 
 
 def is_parallel(model):
-    """utils/torch_utils.py:146-148."""
-    return type(model) in (nn.parallel.DataParallel, nn.parallel.DistributedDataParallel)
+    """utils/torch_utils.py:146-148 (+ the arena reducer, dmayolo.ddp.ArenaDDP)."""
+    return type(model) in (nn.parallel.DataParallel, nn.parallel.DistributedDataParallel) or \
+        type(model).__name__ == 'ArenaDDP'
+
 
 
 def de_parallel(model):

@@ -8,6 +8,7 @@ import socket
 import sys
 import tempfile
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -101,3 +102,63 @@ def test_ddp_world2_applies_sum_of_rank_gradients():
             torch.testing.assert_close(v, exp[k].detach(), rtol=1e-4, atol=1e-6)
             n += 1
     assert n == len(exp)
+
+
+def _arena_worker(rank, world, port, out, compress):
+    _setup()
+    from dmayolo.ddp import ArenaDDP
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    model = _model()
+    if rank == 1:  # the wrapper broadcasts rank 0's initial state, as DDP does
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    net = ArenaDDP(model, bucket_cap_mb=0.25, first_bucket_mb=0.05, compress=compress)
+    assert len(net.buckets) > 3, net.bucket_sizes_mb()  # several buckets, so the in-order launch logic is exercised
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+    x, t = _batch(rank)
+    loss, _ = _loss_fn(model)(net(x), t)
+    loss.backward(torch.full((1,), float(world)))
+    # every gradient is a view of the wrapper's flat buffer afterwards, identical on both ranks
+    assert all(p.grad is not None for p in model.parameters())
+    flat = torch.cat([p.grad.flatten() for p in model.parameters()])
+    other = flat.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(flat, other)
+    opt.step()
+    if rank == 0:
+        torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('compress', [None, 'bf16'])
+def test_arena_reducer_world2_matches_ddp_sum(compress):
+    """dmayolo.ddp.ArenaDDP (bucketed AVG all-reduce of arena slices from post-accumulate hooks, in bucket order,
+    optional bf16 compression) on the CPU oracle model over gloo: the step equals the one that applies the sum of the
+    two ranks' gradients (rtol 1e-4; bf16 compression: the step delta within bf16 precision)"""
+    _setup()
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, 'rank0.pt')
+        mp.spawn(_arena_worker, args=(world, _free_port(), out, compress), nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    model = _model()
+    init = {k: v.detach().clone() for k, v in model.named_parameters()}
+    lf = _loss_fn(model)
+    for r in range(world):
+        x, t = _batch(r)
+        loss, _ = lf(model(x), t)
+        loss.backward()
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+    opt.step()
+    dmax = max(float((v.detach() - init[k]).norm()) for k, v in model.named_parameters())
+    for k, v in model.named_parameters():
+        if compress is None:
+            torch.testing.assert_close(got[k], v.detach(), rtol=1e-4, atol=1e-6)
+        else:
+            de, dg = v.detach() - init[k], got[k] - init[k]
+            # bf16 carries ~3 significant digits of each rank's half; floor for the near-cancelling BN sums
+            assert float((dg - de).norm()) <= 1e-2 * max(float(de.norm()), 1e-2 * dmax), k

@@ -197,3 +197,46 @@ def test_fused_adam_skipped_step_leaves_bias_correction():
             ref.step()
     assert int(opt.state[a]['step'].cpu()) == 2
     torch.testing.assert_close(a.detach().cpu(), ra.detach(), **TOL_ADAM)
+
+
+def test_fused_adam_checkpoint_resume_cpu_map_location(tmp_path):
+    """FusedAdam's state_dict is torch Adam's format (a float32 CPU 'step' per parameter, no device counter in
+    param_groups); a checkpoint saved with it and loaded with torch.load(map_location='cpu', weights_only=True) resumes
+    on the GPU with the right bias corrections (the counter is rebuilt on the parameters' device), and a parameter whose
+    gradient first appears later starts at t = 0, as in torch.  Compared with torch.optim.Adam doing the same."""
+    from dmayolo.optim import FusedAdam
+    g = torch.Generator().manual_seed(5)
+    a0, b0 = torch.randn(5000, generator=g), torch.randn(300, generator=g)
+    a, b = torch.nn.Parameter(a0.cuda()), torch.nn.Parameter(b0.cuda())
+    ra, rb = torch.nn.Parameter(a0.clone()), torch.nn.Parameter(b0.clone())
+    opt = FusedAdam([a, b], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    ref = torch.optim.Adam([ra, rb], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    grads = [(torch.randn(5000, generator=g), torch.randn(300, generator=g)) for _ in range(6)]
+    for i in range(3):  # b has no gradient for the first 2 steps
+        ga, gb = grads[i]
+        a.grad, ra.grad = ga.cuda(), ga.clone()
+        b.grad, rb.grad = (gb.cuda(), gb.clone()) if i >= 2 else (None, None)
+        opt.step()
+        ref.step()
+    sd = opt.state_dict()
+    assert all('_dstep' not in grp for grp in sd['param_groups'])
+    for st in sd['state'].values():
+        assert st['step'].device.type == 'cpu' and st['step'].dtype == torch.float32
+    assert [float(sd['state'][i]['step']) for i in (0, 1)] == [float(ref.state[ra]['step']), float(ref.state[rb]['step'])]
+    path = tmp_path / 'opt.pt'
+    torch.save({'optimizer': sd}, path)
+    loaded = torch.load(path, map_location='cpu', weights_only=True)['optimizer']
+    opt2 = FusedAdam([a, b], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    opt2.load_state_dict(loaded)
+    for st in opt2.state.values():  # torch moves the moments to the parameters' device on load
+        st['exp_avg'], st['exp_avg_sq'] = st['exp_avg'].cuda(), st['exp_avg_sq'].cuda()
+    for i in range(3, 6):
+        ga, gb = grads[i]
+        a.grad, ra.grad = ga.cuda(), ga.clone()
+        b.grad, rb.grad = gb.cuda(), gb.clone()
+        opt2.step()
+        ref.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.detach().cpu(), ra.detach(), **TOL_ADAM)
+    torch.testing.assert_close(b.detach().cpu(), rb.detach(), **TOL_ADAM)
+    assert int(opt2.state[a]['step'].cpu()) == 6 and int(opt2.state[b]['step'].cpu()) == 4

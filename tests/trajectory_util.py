@@ -1,0 +1,194 @@
+"""Multi-step training trajectories (test infrastructure, used by test_gpu_trajectory.py and tools/gpu/diag_trajectory.py).
+
+VERDICT r3 item 1: at random init the single-step gradient of these BN networks is dominated by storage-rounding noise,
+so a one-step comparison cannot tell a kernel bias from bf16 noise.  An overfit trajectory can: a few fixed synthetic
+batches, `steps` SGD steps (train.py's optimizer: nesterov SGD over the g0 / g1 / g2 groups of train.py:197-222, weight
+decay on g1 only, constant lr -- no warmup, so the loss actually falls within the run), run
+
+  * by the product (bf16 storage, HIP kernels, FusedSGD + the device GradScaler, as bench.py's step), and
+  * by the oracle (oracle/nn.py + oracle/loss.py) in fp32, and under tests/precision_emu.py's emulations: 'fp16' (the
+    reference's own CUDA-autocast training precision, train.py:432-445, with its 2^16 loss scale) and 'bf16' (the
+    product's storage model),
+
+all from the same state_dict on the same batches.  The oracle's plain-torch ops run on the GPU in fp32 for these
+trajectories (TF32 off); `pin_device_oracle` checks that device run against the CPU oracle on the first step.
+"""
+import os
+
+import torch
+import torch.nn as nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = os.path.join(ROOT, 'dma-yolo_amd', 'dmayolo', 'configs')
+LR, MOM, WD = 0.01, 0.937, 5e-4  # data/hyps/hyp.scratch.yaml lr0 / momentum / weight_decay (train.py:216-222)
+
+
+def groups(model):
+    """train.py:197-214 on any module tree: g0 BN weights (no decay), g1 weights + AdConcat.w (decay), g2 biases"""
+    g0, g1, g2 = [], [], []
+    for v in model.modules():
+        if isinstance(getattr(v, 'bias', None), nn.Parameter):
+            g2.append(v.bias)
+        if isinstance(v, nn.BatchNorm2d):
+            g0.append(v.weight)
+        elif isinstance(getattr(v, 'weight', None), nn.Parameter):
+            g1.append(v.weight)
+        elif isinstance(getattr(v, 'w', None), nn.Parameter):
+            g1.append(v.w)
+    return g0, g1, g2
+
+
+def _no_drop(model):
+    for mod in model.modules():
+        if hasattr(mod, 'drop_prob'):
+            mod.drop_prob = 0.0
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+        if type(mod).__name__ == 'SwinTransformerLayer' and hasattr(mod, 'drop_path'):
+            mod.drop_path = nn.Identity()
+    return model
+
+
+def load_cfg(yml, width=None, depth=None):
+    import yaml
+    with open(os.path.join(CFG, yml)) as f:
+        cfg = yaml.safe_load(f)
+    if width is not None:
+        cfg['width_multiple'], cfg['depth_multiple'] = width, depth
+    return cfg
+
+
+def make_batches(nb, bs, img, nc, per_image=20):
+    from dmayolo.synthetic import images, targets
+    return [(images(bs, img, seed=11 + i), targets(bs, nc, per_image=per_image, seed=11 + i)) for i in range(nb)]
+
+
+def product_model(cfg, nc, seed=0):
+    from dmayolo.models.yolo import Model
+    torch.manual_seed(seed)
+    m = Model(cfg, nc=nc, act_dtype=torch.bfloat16)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    return _no_drop(m), sd
+
+
+def product_trajectory(m, batches, hyp, steps, probe=0):
+    """bench.py's training step (forward, ComputeLoss, backward seeded by the GradScaler, FusedSGD) for `steps` steps
+    over the batches in turn; returns (losses [steps], train-mode outputs on batches[probe] after the last step)"""
+    from dmayolo.optim import build_optimizer, GradScaler
+    from dmayolo.utils.loss import ComputeLoss
+    m = m.cuda().train()
+    m.hyp = hyp
+    cl = ComputeLoss(m)
+    opt = build_optimizer(m, 'sgd', LR, MOM, WD)
+    scaler = GradScaler(torch.device('cuda'))
+    dev = [(x.cuda(), t.cuda()) for x, t in batches]
+    losses = []
+    for i in range(steps):
+        x, t = dev[i % len(dev)]
+        loss, _ = cl(m(x), t)
+        loss.backward(scaler.upstream)
+        scaler.step(opt)
+        scaler.update()
+        opt.zero_grad(set_to_none=True)
+        losses.append(loss.detach().reshape(1))
+        if i % 40 == 39:
+            print(f'  product step {i + 1}/{steps}', flush=True)
+    with torch.no_grad():
+        out = [o.float() for o in m(dev[probe][0])]
+    return torch.cat(losses).double().cpu(), [o.cpu() for o in out]
+
+
+class _TargetCache:
+    """oracle.loss.build_targets depends only on the level shapes, the targets and the anchors: the trajectories reuse
+    a few fixed batches, so the (python-loop) matching runs once per batch"""
+
+    def __init__(self):
+        from oracle import loss as ol
+        self.ol, self.orig, self.memo = ol, ol.build_targets, {}
+
+    def __enter__(self):
+        def cached(shapes, targets, anchors, anchor_t):
+            k = (tuple(tuple(s) for s in shapes), targets.data_ptr(), anchors.data_ptr(), float(anchor_t))
+            if k not in self.memo:
+                self.memo[k] = self.orig(shapes, targets, anchors, anchor_t)
+            return self.memo[k]
+        self.ol.build_targets = cached
+        return self
+
+    def __exit__(self, *a):
+        self.ol.build_targets = self.orig
+
+
+def oracle_model(cfg, nc, sd, mode, dev):
+    from oracle import nn as onn
+    from precision_emu import emulate
+    ref = onn.bn_defaults(onn.Model(cfg, nc=nc))
+    ref.load_state_dict(sd)
+    _no_drop(ref)
+    if mode is not None:
+        emulate(ref, mode)
+    return ref.to(dev).train()
+
+
+def oracle_trajectory(cfg, nc, sd, batches, hyp, steps, mode=None, dev='cuda', probe=0):
+    """the same trajectory on the oracle (fp32, or emulation `mode`); the loss (oracle/loss.py) runs on the CPU over
+    the level outputs copied back; returns (losses [steps], outputs on batches[probe] after the last step)"""
+    from oracle.loss import compute_loss
+    from precision_emu import input_round, LOSS_SCALE
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    ref = oracle_model(cfg, nc, sd, mode, dev)
+    anchors = sd['model.%d.anchors' % (len(ref.model) - 1)].float().cpu()
+    g0, g1, g2 = groups(ref)
+    opt = torch.optim.SGD(g0, lr=LR, momentum=MOM, nesterov=True)
+    opt.add_param_group({'params': g1, 'weight_decay': WD})
+    opt.add_param_group({'params': g2})
+    sc = LOSS_SCALE[mode] if mode else 1.0
+    xs = [(input_round(x.to(dev).float() / 255, mode), t) for x, t in batches]
+    losses = []
+    with _TargetCache():
+        for i in range(steps):
+            x, t = xs[i % len(xs)]
+            pr = ref(x)
+            lo, _ = compute_loss([p.cpu() for p in pr], t, anchors, hyp, nc)
+            opt.zero_grad(set_to_none=True)
+            (lo * sc).backward()
+            if sc != 1.0:
+                for p in ref.parameters():
+                    if p.grad is not None:
+                        p.grad.div_(sc)
+            opt.step()
+            losses.append(float(lo))
+            if i % 40 == 39:
+                print(f'  oracle ({mode or "fp32"}) step {i + 1}/{steps}', flush=True)
+    with torch.no_grad():
+        out = [o.float().cpu() for o in ref(xs[probe][0])]
+    return torch.tensor(losses, dtype=torch.float64), out
+
+
+def pin_device_oracle(cfg, nc, sd, batch, hyp):
+    """first-step loss and gradients of the device-run fp32 oracle vs the CPU oracle: (loss rel err, grad rel L2)"""
+    from oracle.loss import compute_loss
+    torch.backends.cudnn.allow_tf32 = False
+    res = []
+    for dev in ('cpu', 'cuda'):
+        ref = oracle_model(cfg, nc, sd, None, dev)
+        anchors = sd['model.%d.anchors' % (len(ref.model) - 1)].float().cpu()
+        x, t = batch
+        pr = ref(x.to(dev).float() / 255)
+        lo, _ = compute_loss([p.cpu() for p in pr], t, anchors, hyp, nc)
+        lo.backward()
+        res.append((float(lo), torch.cat([p.grad.double().cpu().flatten() for p in ref.parameters()
+                                          if p.grad is not None])))
+    (lc, gc), (lg, gg) = res
+    return abs(lg - lc) / abs(lc), float((gg - gc).norm() / gc.norm())
+
+
+def curve_err(a, b):
+    """loss-curve distance: mean over steps of |a - b| / b, and the same over the last quarter"""
+    r = (a - b).abs() / b.abs()
+    return float(r.mean()), float(r[-max(1, len(r) // 4):].mean())
+
+
+def out_err(po, ro):
+    return [float((a.double() - b.double()).norm() / b.double().norm()) for a, b in zip(po, ro)]
