@@ -214,7 +214,16 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
             tr = json.load(f).get(cfg_name, {}).get(dom)
         if tr:
             traffic, tsrc = round(tr['bytes_per_launch']), 'profiles/pmc_traffic.json: ' + tr['source']
+    mfma, msrc = {}, None  # MFMA-busy per family from the PMC pass of the same bench command (tools/pmc_mfma.py)
+    mpath = os.path.join(ROOT, 'profiles', 'pmc_mfma.json')
+    if os.path.exists(mpath):
+        with open(mpath) as f:
+            mj = json.load(f).get(cfg_name, {})
+        mfma = {k: v['mfma_busy'] for k, v in mj.items()}
+        msrc = next(iter(mj.values()))['source'] if mj else None
     return dict(bound='hbm' if hbm else 'mfma', kernel=f'dmy_{dom} (implicit-GEMM family, all launches of the roofline pass)',
+                mfma_busy=mfma or None, mfma_busy_unit='SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), '
+                'time-weighted per family; conv_3x3 = the k > 1 kernels', mfma_busy_source=msrc,
                 achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(troof / d['seconds'], 4),
                 achieved_over_peak=round(achieved / peak, 4),
                 traffic=traffic, traffic_unit='bytes/launch (HBM, PMC)', traffic_source=tsrc,
@@ -225,7 +234,8 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
                 kernels={k: dict(launches=v['launches'], ms=round(v['seconds'] * 1e3 / steps, 3),
                                  tflops=round(v['flops'] / v['seconds'] / 1e12, 2),
                                  gbps=round(v['bytes'] / v['seconds'] / 1e9, 1),
-                                 frac=round((v['troof_mfma'] + v['troof_hbm']) / v['seconds'], 4)) for k, v in ks.items()},
+                                 frac=round((v['troof_mfma'] + v['troof_hbm']) / v['seconds'], 4),
+                                 **({'mfma_busy': mfma[k]} if k in mfma else {})) for k, v in ks.items()},
                 conv_share_of_step=round(sum(v['seconds'] for v in ks.values()) / el_events, 3),
                 measured_in='separate pass of the same %d steps with per-launch HIP events (%.1f ms/step there)'
                             % (steps, el_events * 1e3 / steps))

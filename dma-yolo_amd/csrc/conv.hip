@@ -20,6 +20,7 @@
 // Block ids are remapped so consecutive tiles sharing an A panel land on one XCD (L2 reuse).
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 #include <cmath>
 
 // s_setprio(1) around the MFMA cluster of the LDS-DMA main loops (cdna_hip_programming.md §5.5 T5);
@@ -1510,7 +1511,13 @@ struct P1P {
   static constexpr int LDS = NS * C3_::STAGE + NW * 512;
 };
 
-template <int BM, int BN, int NS, int WTR, bool DG>
+// LANE (forward, one column tile): the BN partials are NOT written per 32/64-pixel group; each lane keeps running Σz /
+// Σz² of its 4 channels x its pixel lane over ALL tiles of the block (fp32, ~NI x tiles-per-wave terms), and each wave
+// row writes ONE partial row at the end (row blockIdx.x * WM + wave row, its WN waves writing their 64-channel slices;
+// dmy_conv_fwd_bn_rows reports G * WM rows).  For the
+// <= 64-column layers the per-32-pixel rows cost 12.5 % extra write bytes plus their per-tile DPP reductions
+// (64 -> 64 @384^2 bs32: 349 us with them vs 233 us without, round 4, gpurun_out r4/micro2_p1s.log).
+template <int BM, int BN, int NS, int WTR, bool DG, bool LANE = false>
 __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
     const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias, bf16* __restrict__ y,
     float* __restrict__ psum, float* __restrict__ psq, int /*accumulate: 0*/, Geom g, int gm, int gn, unsigned xbytes,
@@ -1531,7 +1538,12 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
   if ((int)blockIdx.x >= ntiles) return;
   const bool half = g.K <= 64;
   const int PR = half ? 32 : 64;                 // pixels per BN partial row (dmy_conv_fwd_partial_rows)
-  const int ngrp = psum != nullptr ? WTR / PR : 0;
+  const int ngrp = (psum != nullptr && !LANE) ? WTR / PR : 0;
+  float ls1[4][4], ls2[4][4];  // LANE: this lane's running sums over the block's tiles, [16-channel group][4 channels]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) ls1[j][rr] = ls2[j][rr] = 0.f;
   // this wave's epilogue VMEM ops per tile (no accumulate: the host routes it away; the inference epilogue's residual
   // adds one 16-B load per store)
   const int nepi = PP::NST * (ep.on && ep.res != nullptr ? 2 : 1) + 2 * ngrp;
@@ -1539,7 +1551,7 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, ybytes);
   const __amdgpu_buffer_rsrc_t rps = make_rsrc(psum, psum != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
   const __amdgpu_buffer_rsrc_t rpq = make_rsrc(psq, psq != nullptr ? (unsigned)((long)nprow * g.K * 4) : 0u);
-  if (psum != nullptr && BM < 2 * PR && blockIdx.x == 0) {
+  if (!LANE && psum != nullptr && BM < 2 * PR && blockIdx.x == 0) {
     // dmy_conv_fwd_partial_rows rounds the partial rows up to an even count; with 64-row tiles the last one can lie
     // past every tile: it holds no pixels and must still read as zero (plain stores, older than any stage load)
     for (long pr = (long)gm * BM / PR + threadIdx.x / 64; pr < nprow; pr += PP::NW)
@@ -1634,7 +1646,18 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
           for (int i = 0; i < NI; ++i) acc[i][j][rr] += bv;
         }
     }
-    if (psum != nullptr) {
+    if (LANE && psum != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const float v = mw + 16 * i + pl < M ? acc[i][j][rr] : 0.f;
+            ls1[j][rr] += v;
+            ls2[j][rr] += v * v;
+          }
+    } else if (psum != nullptr) {
       for (int gi = 0; gi < ngrp; ++gi) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1692,6 +1715,26 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         const unsigned off = (m < M && n < g.K) ? (unsigned)((m * g.yps + n) * 2) : kBufOob;
         __builtin_amdgcn_raw_buffer_store_b128(v, ry, off, 0, 0);
       }
+  }
+  if (LANE && psum != nullptr) {  // one partial row per wave row: reduce the 16 pixel lanes, transpose through LDS
+    const long prow = (long)blockIdx.x * C3_::WM + wm;  // the WN waves of wave row wm write its 64-channel slices
+    const int nw = wn * 64;  // one column tile (gn == 1): n0 = 0
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float s1 = row_sum16(ls1[j][rr]), s2 = row_sum16(ls2[j][rr]);
+        if (pl == 15) {
+          red[16 * j + 4 * q + rr] = s1;
+          red[64 + 16 * j + 4 * q + rr] = s2;
+        }
+      }
+    __builtin_amdgcn_wave_barrier();
+    const float v1 = red[lane], v2 = red[64 + lane];
+    const bool ok = prow < nprow && nw + lane < g.K;
+    const unsigned off = ok ? (unsigned)((prow * g.K + nw + lane) * 4) : kBufOob;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1), rps, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v2), rpq, off, 0, 0);
   }
 }
 
@@ -1847,13 +1890,14 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
 // yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
 // 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
 template <int KD, int NTH, bool G3 = false>
-__global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
+__global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                 long M, int NC, int ng, long xps, long yps, unsigned xbytes,
                                                 int ntiles, int kwrow, int H, int W) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
+  constexpr int NG2 = KD <= 128 ? 2 : 1, CP = 32 * NG2;  // 32-channel groups per column pass (registers: KD 160 / 256 keep 1)
   bf16* ws = reinterpret_cast<bf16*>(p1s_smem);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* red = reinterpret_cast<float*>(p1s_smem + ng * PITCH * 2) + wid * 64;  // this wave's [2][32] partials
@@ -1902,28 +1946,34 @@ __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1
         }
       }
     }
-    for (int ct = 0; ct < ncols; ct += 32) {
-      f32x4 acc[2][4];  // [16-channel block][16-pixel block]
+    // column passes of NG2 groups of 32 channels (CP = 32 * NG2 columns): the two 64-B halves of each 128-B output line
+    // (64 channels of one pixel) leave in back-to-back stores.  Stored 32 channels per pass instead, a line's second
+    // half followed a whole pass later and the write stream ran at 3.3-4.1 TB/s instead of 4.9-5.7 (round 4,
+    // tools/gpu/store_lab.hip: 'halves' vs 'pairs')
+    for (int ct = 0; ct < ncols; ct += CP) {
+      const int ngr = min(NG2, (ncols - ct) / 32);  // 32-channel groups in this pass (ncols is a multiple of 32)
+      f32x4 acc[2 * NG2][4];                       // [16-channel block][16-pixel block]
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < 2 * NG2; ++cb)
 #pragma unroll
         for (int pb = 0; pb < 4; ++pb) acc[cb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
+        for (int cb = 0; cb < 2 * NG2; ++cb) {
+          if (cb >= 2 * ngr) break;
           const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + (ct + cb * 16 + pl) * PITCH + kc * 32 + q * 8);
 #pragma unroll
           for (int pb = 0; pb < 4; ++pb)
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[pb][kc], acc[cb][pb], 0, 0, 0);
         }
-      const int nb = c0 + ct;  // first column of this 32-column pass
+      const int nb = c0 + ct;  // first column of this pass
       if (bias != nullptr) {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+        for (int cb = 0; cb < 2 * NG2; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float bv = bias[nb + cb * 16 + q * 4 + r];
+            const float bv = cb < 2 * ngr ? bias[nb + cb * 16 + q * 4 + r] : 0.f;
 #pragma unroll
             for (int pb = 0; pb < 4; ++pb) acc[cb][pb][r] += bv;
           }
@@ -1933,55 +1983,64 @@ __global__ void __launch_bounds__(NTH, KD == 64 ? 4 : KD == 128 ? 3 : 2) conv_p1
         for (int hh = 0; hh < 2; ++hh) {
           if (!half && hh == 1) break;
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
+          for (int gr = 0; gr < NG2; ++gr) {
+            if (gr >= ngr) break;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float s1 = 0.f, s2 = 0.f;
+            for (int c2 = 0; c2 < 2; ++c2)
 #pragma unroll
-              for (int pb = 0; pb < 4; ++pb) {
-                if (half && (pb >> 1) != hh) continue;
-                const float v = p0 + pb * 16 + pl < M ? acc[cb][pb][r] : 0.f;
-                s1 += v;
-                s2 += v * v;
+              for (int r = 0; r < 4; ++r) {
+                const int cb = 2 * gr + c2;
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int pb = 0; pb < 4; ++pb) {
+                  if (half && (pb >> 1) != hh) continue;
+                  const float v = p0 + pb * 16 + pl < M ? acc[cb][pb][r] : 0.f;
+                  s1 += v;
+                  s2 += v * v;
+                }
+                s1 = row_sum16(s1);
+                s2 = row_sum16(s2);
+                if (pl == 15) {  // channel c2 * 16 + q * 4 + r of 32-channel group gr
+                  red[c2 * 16 + q * 4 + r] = s1;
+                  red[32 + c2 * 16 + q * 4 + r] = s2;
+                }
               }
-              s1 = row_sum16(s1);
-              s2 = row_sum16(s2);
-              if (pl == 15) {  // channel cb * 16 + q * 4 + r of this pass
-                red[cb * 16 + q * 4 + r] = s1;
-                red[32 + cb * 16 + q * 4 + r] = s2;
-              }
-            }
-          // one 64-lane store: lanes 0..31 the 32 channel sums, lanes 32..63 the sums of squares (the wave's own
-          // LDS rows: the lane-15 writes above are ordered before this read by the wave's lgkmcnt)
-          __builtin_amdgcn_wave_barrier();
-          const float v = red[lane];
-          const long row = half ? 2L * t + hh : (long)t;
-          (lane < 32 ? psum : psq)[row * NC + nb + (lane & 31)] = v;
-          __builtin_amdgcn_wave_barrier();
+            // one 64-lane store per group: lanes 0..31 the 32 channel sums, lanes 32..63 the sums of squares (the
+            // wave's own LDS rows: the lane-15 writes above are ordered before this read by the wave's lgkmcnt)
+            __builtin_amdgcn_wave_barrier();
+            const float v = red[lane];
+            const long row = half ? 2L * t + hh : (long)t;
+            (lane < 32 ? psum : psq)[row * NC + nb + gr * 32 + (lane & 31)] = v;
+            __builtin_amdgcn_wave_barrier();
+          }
         }
       }
 #pragma unroll
       for (int pb = 0; pb < 4; ++pb) {
         const long m = p0 + pb * 16 + pl;
-        const f32x4 &a = acc[0][pb], &b = acc[1][pb];
-        const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
-        uint4 v;
-        v.x = s0[0];
-        v.y = s1[0];
-        v.z = s0[1];
-        v.w = s1[1];
-        if (m < M) {
-          uint4* dst = reinterpret_cast<uint4*>(y + m * yps + nb + chq);
-          if (accumulate) {
-            float f[8], o[8];
-            unpack<bf16>(v, f);
-            unpack<bf16>(*dst, o);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] += o[j];
-            v = pack<bf16>(f);
+        for (int gr = 0; gr < NG2; ++gr) {  // the groups of one pixel back to back: whole 128-B lines
+          if (gr >= ngr) break;
+          const f32x4 &a = acc[2 * gr][pb], &b = acc[2 * gr + 1][pb];
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
+          uint4 v;
+          v.x = s0[0];
+          v.y = s1[0];
+          v.z = s0[1];
+          v.w = s1[1];
+          if (m < M) {
+            uint4* dst = reinterpret_cast<uint4*>(y + m * yps + nb + gr * 32 + chq);
+            if (accumulate) {
+              float f[8], o[8];
+              unpack<bf16>(v, f);
+              unpack<bf16>(*dst, o);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] += o[j];
+              v = pack<bf16>(f);
+            }
+            *dst = v;
           }
-          *dst = v;
         }
       }
     }
@@ -3575,9 +3634,20 @@ inline int p1p_maxn() {
   static const int t = env_int("DMY_P1P_MAXN", 256);
   return t;
 }
-template <bool DG>
-int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-               hipStream_t st, unsigned xbytes, unsigned wbytes, const Epi& ep = Epi{}, bool small = false) {
+// per-lane BN partials in conv_p1p (LANE): DMY_P1P_LANE = 1 (default) for training forwards with one column tile
+inline int p1p_lane_mode() {
+  static const int t = env_int("DMY_P1P_LANE", 1);
+  return t;
+}
+// conv_p1p's persistent grid: blocks per CU from the LDS footprint, capped at the tile count, a multiple of 8 (XCDs)
+inline int p1p_grid(int ntiles, int lds) {
+  const int bpc = (160 * 1024) / lds;
+  int G = num_cus() * (bpc < 1 ? 1 : bpc);
+  return G > ntiles ? ntiles : G / 8 * 8;
+}
+// the tile configuration launch_p1p picks: f(BM, BN, NS, WTR) as integral constants; -1 when it declines
+template <bool DG, class F>
+int p1p_plan(const Geom& gv, int acc, const Epi& ep, bool small, F&& f) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const int nk = gv.C / v3::BK, mode = p1p_mode();
   const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
@@ -3585,32 +3655,55 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
   if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || rb >= (double)v3::kBufOob || nk < 1 ||
       (ep.res != nullptr && (ep.rps % 8 != 0 || !aligned16(ep.res))) || (mode == 1 && !small && gv.K > p1p_maxn()))
     return -1;
-  const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
-  const int NC = num_cus();
-#define P1P_GO(BM, BN, NS, WTR)                                                                                  \
-  {                                                                                                              \
-    using PP = v3::P1P<BM, BN, NS, WTR>;                                                                         \
-    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN), ntiles = gm * gn;                                   \
-    const int bpc = (160 * 1024) / PP::LDS;                                                                      \
-    int G = NC * (bpc < 1 ? 1 : bpc);                                                                            \
-    if (G > ntiles) G = ntiles;                                                                                  \
-    else G = G / 8 * 8;                                                                                          \
-    v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
-                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb); \
-    return (int)hipGetLastError();                                                                               \
-  }
+  using std::integral_constant;
+#define P1P_CFG(BM, BN, NS, WTR) \
+  return f(integral_constant<int, BM>{}, integral_constant<int, BN>{}, integral_constant<int, NS>{}, integral_constant<int, WTR>{})
   if (small) {  // small M (batch-1 inference): one-wave 64 x 64 tiles, several blocks per CU, the short K ring
-    if (nk >= 2) P1P_GO(64, 64, 3, 64)
-    P1P_GO(64, 64, 2, 64)
+    if (nk >= 2) P1P_CFG(64, 64, 3, 64);
+    P1P_CFG(64, 64, 2, 64);
   }
-  if (mode == 3 && gv.K > 64) P1P_GO(128, 128, 2, 64)
-  if (mode == 2 && gv.K >= 256) P1P_GO(256, 256, 2, 128)
+  if (mode == 3 && gv.K > 64) P1P_CFG(128, 128, 2, 64);
+  if (mode == 2 && gv.K >= 256) P1P_CFG(256, 256, 2, 128);
   if (gv.K > 64) {
-    if (nk >= 2) P1P_GO(256, 128, 3, 64)
-    P1P_GO(256, 128, 2, 64)
+    if (nk >= 2) P1P_CFG(256, 128, 3, 64);
+    P1P_CFG(256, 128, 2, 64);
   }
-  P1P_GO(256, 64, 2, 64)
-#undef P1P_GO
+  P1P_CFG(256, 64, 2, 64);
+#undef P1P_CFG
+}
+// BN partial rows of a LANE launch (one per wave row of the persistent grid), or 0 when launch_p1p would not use LANE
+inline int p1p_lane_rows(const Geom& gv) {
+  if (!p1p_lane_mode()) return 0;
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  return p1p_plan<false>(gv, 0, Epi{}, false, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
+    using PP = v3::P1P<decltype(bm)::value, decltype(bn)::value, decltype(ns)::value, decltype(wtr)::value>;
+    const int gm = ceil_div(M, decltype(bm)::value), gn = ceil_div(gv.K, decltype(bn)::value);
+    return gn == 1 ? p1p_grid(gm * gn, PP::LDS) * PP::C3_::WM : 0;
+  });
+}
+template <bool DG>
+int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
+               hipStream_t st, unsigned xbytes, unsigned wbytes, const Epi& ep = Epi{}, bool small = false) {
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
+  const double rb = ep.res != nullptr ? 2.0 * ((double)(M - 1) * ep.rps + gv.K) : 0.0;
+  return p1p_plan<DG>(gv, acc, ep, small, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
+    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, NS = decltype(ns)::value, WTR = decltype(wtr)::value;
+    using PP = v3::P1P<BM, BN, NS, WTR>;
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN), ntiles = gm * gn;
+    const int G = p1p_grid(ntiles, PP::LDS);
+    if constexpr (!DG) {
+      if (ps != nullptr && !small && gn == 1 && p1p_lane_mode()) {  // one BN partial row per wave (dmy_conv_fwd_bn_rows)
+        v3::conv_p1p<BM, BN, NS, WTR, false, true><<<(unsigned)G, PP::NTH, 0, st>>>(
+            x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb);
+        return (int)hipGetLastError();
+      }
+    }
+    const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
+    v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
+                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb);
+    return (int)hipGetLastError();
+  });
 }
 
 // 3x3 stride-1 64 -> 64-channel layers on the persistent halo kernel (v3::conv3_halo64): DMY_HALO = 0 off, 1 (default)
@@ -4350,6 +4443,20 @@ DMY_API int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w, const 
                                         int OH, int OW, long yps) {
   const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
   if (dtype && bias == nullptr && halo_ok(g, x, w, y)) return halo_rows(g);  // one row per wave (conv3_halo64)
+  if (dtype) {  // the training forward's route through conv_fwd_t / launch_v3 to a LANE conv_p1p: one row per wave
+    const long M = (long)N * OH * OW;
+    const bool p1 = KH == 1 && KW == 1 && S == 1 && P == 0;
+    const bool small = M < 65536 && M >= 64 && p1p_small() && p1 && C % 64 == 0 && xps % 8 == 0 && yps % 8 == 0 &&
+                       K % 8 == 0 && K >= 32 && aligned16(x) && aligned16(w) && aligned16(y) && conv_buf_mode() &&
+                       2.0 * ((double)N * H * W * xps) < (double)v3::kBufOob && 2.0 * K * C < (double)v3::kBufOob;
+    if (p1 && !small && v3_ok(C, xps, K, yps, x, w, y, M) &&
+        !(p1s_ok(g, x, w, y) && (p1s_mode() == 2 || K >= 2 * C)) && !stem_s_ok(g, x, w, y) && p1p_mode() &&
+        conv_buf_mode() && C % 64 == 0 && 2.0 * ((double)N * H * W * xps) < (double)v3::kBufOob &&
+        2.0 * K * C < (double)v3::kBufOob) {
+      const int r = p1p_lane_rows(g);
+      if (r > 0) return r;
+    }
+  }
   return dmy_conv_fwd_partial_rows((long)N * OH * OW, K);
 }
 

@@ -356,7 +356,7 @@ class SwinTransformerLayer(nn.Module):
         u = F.pad(u, (0, 0, 0, Cp - Cc, 0, Rp - R))
         if sh > 0:
             u = torch.roll(u, (-sh, -sh), (1, 2))
-            mask = swin_mask(Rp, Cp, ws, sh)
+            mask = swin_mask(Rp, Cp, ws, sh).to(u.device)
         else:
             mask = None
         win = u.view(B, Rp // ws, ws, Cp // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, C)

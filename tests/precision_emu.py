@@ -11,6 +11,11 @@ run again with the roundings a reduced-precision run performs, and the product i
                    gradient itself stays fp32) + the outputs of the composite modules whose result the product stores
                    in bf16 (Bottleneck / Swin residual sums, CoorAttention's x * a_w * a_h, the AdConcat weighted
                    copies, SCConv's gate product);
+  mode 'bf16_sink' 'bf16' + each leaf's INPUT gradient rounded to bf16 as it leaves the leaf: the product's data-grad
+                   kernels store every contribution to an input gradient in bf16 and accumulate the next one into that
+                   bf16 buffer (functional.GradSink; autograd's own sums of bf16 gradients), where 'bf16' sums the
+                   fp32 contributions first and rounds once at the producer's output.  A tensor with one consumer
+                   rounds the same value twice (no change); one with k consumers gets the k roundings the product has;
   mode 'fp16'     the reference's own training precision, CUDA autocast (train.py:434): the same roundings to fp16
                    (conv / linear / activation outputs and weights fp16, BatchNorm statistics and the loss fp32),
                    backward seeded with a 2^16 loss scale as GradScaler does, so that fp16 gradients do not underflow;
@@ -23,8 +28,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-DTYPES = {'bf16_act': torch.bfloat16, 'bf16': torch.bfloat16, 'fp16': torch.float16, 'fp8': torch.bfloat16}
-LOSS_SCALE = {'bf16_act': 1.0, 'bf16': 1.0, 'fp16': 2.0 ** 16, 'fp8': 1.0}
+DTYPES = {'bf16_act': torch.bfloat16, 'bf16': torch.bfloat16, 'bf16_sink': torch.bfloat16, 'fp16': torch.float16,
+          'fp8': torch.bfloat16}
+LOSS_SCALE = {'bf16_act': 1.0, 'bf16': 1.0, 'bf16_sink': 1.0, 'fp16': 2.0 ** 16, 'fp8': 1.0}
 
 LEAVES = (nn.Conv2d, nn.BatchNorm2d, nn.SiLU, nn.Upsample, nn.MaxPool2d, nn.Linear, nn.LayerNorm, nn.GELU, nn.Hardswish,
           nn.Sigmoid, nn.AvgPool2d, nn.AdaptiveAvgPool2d, nn.ReLU)
@@ -37,6 +43,19 @@ class RoundAct(torch.autograd.Function):
     def forward(ctx, x, dt):
         ctx.dt = dt
         return x.to(dt).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt).float(), None
+
+
+class RoundGrad(torch.autograd.Function):
+    """identity forward; the gradient flowing back through it rounded (a leaf's input-gradient contribution)"""
+
+    @staticmethod
+    def forward(ctx, x, dt):
+        ctx.dt = dt
+        return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
@@ -105,6 +124,12 @@ def emulate(model, mode):
             mod.register_forward_hook(hook)
     if mode == 'bf16_act':
         return model
+    if mode == 'bf16_sink':
+        pre = lambda m, i: tuple(RoundGrad.apply(a, dt) if torch.is_tensor(a) and a.requires_grad else a  # noqa: E731
+                                 for a in i)
+        for mod in model.modules():
+            if isinstance(mod, LEAVES):
+                mod.register_forward_pre_hook(pre)
     for mod in model.modules():
         if isinstance(mod, _stored_types()):
             mod.register_forward_hook(hook)
@@ -130,10 +155,12 @@ def input_round(x, mode):
     return x if mode is None else RoundAct.apply(x, DTYPES[mode])
 
 
-def oracle_run(cfg, nc, sd, x, t, anchors, hyp, mode):
+def oracle_run(cfg, nc, sd, x, t, anchors, hyp, mode, dev='cpu'):
     """the CPU oracle (fp32, or under emulation `mode`) on a product state_dict: train-mode forward of the uint8
     images x, ComputeLoss against targets t, backward.  Returns (model, outputs, loss, items); cfg is a yaml path or
-    dict.  DropPath is off (a random draw, not a rounding)."""
+    dict.  DropPath is off (a random draw, not a rounding).  dev='cuda' runs the same torch ops on the GPU (TF32 off):
+    another fp32 summation order, i.e. another realization of the emulation's rounding decisions; the loss (CPU
+    restatement) then runs over the outputs copied back."""
     import yaml
     from oracle import nn as onn
     from oracle.loss import compute_loss
@@ -149,15 +176,22 @@ def oracle_run(cfg, nc, sd, x, t, anchors, hyp, mode):
             mod.p = 0.0
     if mode is not None:
         emulate(ref, mode)
+    if dev != 'cpu':
+        torch.backends.cudnn.allow_tf32 = False
+        torch.backends.cuda.matmul.allow_tf32 = False
+        ref = ref.to(dev)
     ref.train()
-    pr = ref(input_round(x.float() / 255, mode))
-    lo, it = compute_loss(pr, t, anchors, hyp, nc)
+    pr = ref(input_round(x.to(dev).float() / 255, mode))
+    lo, it = compute_loss([p.cpu() for p in pr] if dev != 'cpu' else pr, t, anchors, hyp, nc)
     sc = LOSS_SCALE[mode] if mode else 1.0
     (lo * sc).backward()
     if sc != 1.0:
         for p in ref.parameters():
             if p.grad is not None:
                 p.grad.div_(sc)
+    if dev != 'cpu':
+        ref = ref.cpu()
+        pr = [p.detach().cpu() for p in pr]
     return ref, pr, lo, it
 
 

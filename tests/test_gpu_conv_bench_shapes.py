@@ -5,10 +5,14 @@ oracle than the bf16-storage emulation's; a kernel that dropped or double-counte
 partial tile at these M would show here as a NORM error (a bias), which bf16 rounding noise does not produce.
 
 Per (layer shape, kind) the test measures the relative L2 error and the norm ratio |y| / |y_ref| - 1:
-  forward / data-grad (bf16 output): rel L2 <= 6e-3 (one bf16 rounding of each output is ~2.2e-3 rms) and
-                                     |norm ratio - 1| <= 1e-3 (unbiased rounding moves the norm by ~1e-6)
-  weight-grad (fp32 accumulation):   rel L2 <= 1e-3, |norm ratio - 1| <= 1e-4 (fp32 sums over up to 9.4 M pixels)
-  forward BN partials:               sum / sum of squares per channel within 1e-3 relative (sum: or 1e-2 sqrt(M) absolute)
+  forward / data-grad (bf16 output): rel L2 <= 2.5e-3 -- one round-to-nearest of each output to bf16 is 2^-8 / sqrt(12)
+                                     = 1.13e-3 of ulp-relative, 1.66e-3 of rms for these Gaussian outputs, which is what
+                                     every shape measures (round 4, gpurun_out r4/diag_tests.log) -- and
+                                     |norm ratio - 1| <= 5e-5 (measured <= 3.8e-6: unbiased rounding)
+  weight-grad (fp32 accumulation):   rel L2 <= 5e-5 (measured <= 5.6e-6), |norm ratio - 1| <= 1e-6 (measured 7e-8)
+  forward BN partials:               sum / sum of squares per channel within 1e-6 relative (measured 1.8e-8; sum: or
+                                     1e-2 sqrt(M) absolute)
+A split-K chunk, a parity class or a tile dropped or counted twice moves these by orders of magnitude.
 The shape lists are the unique (N, C, H, W, K, k, s) of profiles/r03/*_launches.csv (yolov5s @640 bs64, DMA-YOLO-l @1536
 bs32) minus the 6x6 image stems, which the model runs as the space-to-depth k3 view (test_gpu_model.py covers it).
 1x1 weight-grads go through dmy_conv_wgrad_ex with the OIHW | ZEROED flags the training step uses (arena slices)."""
@@ -126,7 +130,7 @@ def _check_shape(N, C, H, W, K, k, s, seed):
     return out
 
 
-BOUNDS = {'fwd': (6e-3, 1e-3), 'dgrad': (6e-3, 1e-3), 'wgrad': (1e-3, 1e-4), 'bn': (1e-3, 0.0)}
+BOUNDS = {'fwd': (2.5e-3, 5e-5), 'dgrad': (2.5e-3, 5e-5), 'wgrad': (5e-5, 1e-6), 'bn': (1e-6, 0.0)}
 
 
 @pytest.mark.parametrize('cfg,shape', [('v5s', sh) for sh in V5S] + [('dma', sh) for sh in DMA])

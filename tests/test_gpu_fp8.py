@@ -230,8 +230,8 @@ def test_config5_fp8_step_vs_fp32_oracle():
     emulation (tests/precision_emu.py 'fp8': bf16 storage + e4m3 forward operands with the product's per-tensor /
     per-channel scales, bf16 backward).  Bounds on what the e4m3 kernel computes, the forward: Detect outputs relative
     L2 per level <= 1.1 * emu + 2e-3 and loss <= 1.1 * emu + 5e-3 (round 3, measured: product 2.43/3.39/1.48/6.54e-2 vs
-    emu 2.28/3.36/1.50/6.48e-2).  The gradient metrics are printed, not bounded: at random init this config's gradient
-    is chaotic under ANY rounding (its CBAM channel maxima, SPP / SPPF argmaxes and global attention route on
+    emu 2.28/3.36/1.50/6.48e-2).  The gradient metrics are bounded against the envelope of the emulation realizations
+    (below), loosely: at random init this config's gradient is chaotic under ANY rounding (its CBAM channel maxima, SPP / SPPF argmaxes and global attention route on
     near-ties) -- the bf16 emulation alone has whole-gradient cosine -0.11 against fp32, the fp8 one 0.007 -- so no
     gradient bound separates a correct kernel from a wrong one here; the fp8 kernels' backward is bf16 and is pinned
     by the bf16 tests.  The bf16 emulation's numbers are printed beside them (the e4m3 forward's cost on top of bf16)."""
@@ -262,6 +262,7 @@ def test_config5_fp8_step_vs_fp32_oracle():
     loss, items = ComputeLoss(m)(p, t.cuda())
     loss.backward()
     runs = {mode: oracle_run(cfg, nc, sd, x, t, anchors, hyp, mode) for mode in (None, 'fp8', 'bf16')}
+    runs['fp8_gpu'] = oracle_run(cfg, nc, sd, x, t, anchors, hyp, 'fp8', 'cuda')  # a second rounding realization
     ref, pr, lr_, _ = runs[None]
     rg = dict(ref.named_parameters())
     names = [k for k in rg if rg[k].grad is not None]
@@ -273,9 +274,18 @@ def test_config5_fp8_step_vs_fp32_oracle():
     got = errs(p, loss, dict(m.named_parameters()))
     e8 = errs(runs['fp8'][1], runs['fp8'][2], dict(runs['fp8'][0].named_parameters()))
     e16 = errs(runs['bf16'][1], runs['bf16'][2], dict(runs['bf16'][0].named_parameters()))
+    e8g = errs(runs['fp8_gpu'][1], runs['fp8_gpu'][2], dict(runs['fp8_gpu'][0].named_parameters()))
     f = lambda r: 'outputs %s loss %.2e grad-norm vector %.2e cos %.4f' % (['%.2e' % v for v in r[0]], r[1], r[2], r[3])  # noqa: E731
-    print(f'config 5 fp8 product: {f(got)}\n  fp8 emulation: {f(e8)}\n  bf16 emulation: {f(e16)}')
+    print(f'config 5 fp8 product: {f(got)}\n  fp8 emulation: {f(e8)}\n  fp8 emulation, GPU fp32 order: {f(e8g)}\n'
+          f'  bf16 emulation: {f(e16)}')
     for a, e in zip(got[0], e8[0]):
         assert a <= 1.1 * e + 2e-3, (got[0], e8[0])
     assert got[1] <= 1.1 * e8[1] + 5e-3, (got[1], e8[1])
     assert max(e8[0]) > 0 and all(a < 0.15 for a in got[0])  # the e4m3 forward really ran and stayed close
+    # gradient bounds against the envelope of the emulation realizations (fp8 on CPU / GPU order, and bf16 -- the
+    # backward IS bf16): round 3 measured the grad-norm vector at 0.327 (product) vs 0.082 (fp8 emu) vs 0.336 (bf16
+    # emu), i.e. realization noise at random init; the training-run check of this leg is test_gpu_trajectory.py's
+    # 'c5-fp8@256' case
+    env_gn = max(e8[2], e8g[2], e16[2])
+    assert got[2] <= 1.5 * env_gn + 2e-2, (got[2], e8[2], e8g[2], e16[2])
+    assert got[3] >= min(e8[3], e8g[3], e16[3]) - 0.1, (got[3], e8[3], e8g[3], e16[3])

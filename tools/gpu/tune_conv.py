@@ -130,6 +130,8 @@ def main():
         fns = {
             'fwd': lambda: call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k,
                                 k, s, p, OH, OW, K, stream()),
+            'fwdnb': lambda: call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), None, None, N, H, W, C, C, K, k,
+                                  k, s, p, OH, OW, K, stream()),
             'dgrad': lambda: call('dmy_conv_dgrad', 1, ptr(dy), ptr(wt), ptr(dx), 0, N, H, W, C, C, K, k, k, s, p, OH,
                                   OW, K, stream()),
             'wgrad': lambda: call('dmy_conv_wgrad', 1, ptr(x), ptr(dy), ptr(dwo), N, H, W, C, C, K, k, k, s, p, OH, OW,
@@ -150,8 +152,20 @@ def main():
             a2, b2 = x.permute(0, 2, 3, 1).reshape(-1, C), wf.view(K, C).t()
             y2 = torch.empty(a2.shape[0], K, dtype=torch.bfloat16, device='cuda')
             fns['mm'] = lambda: torch.matmul(a2, b2, out=y2)
+        if 'copy' in kinds:  # calibration: a torch copy moving the same bytes as the 1x1 forward (read x, write y)
+            xf_ = x.permute(0, 2, 3, 1).reshape(-1)
+            yf_ = torch.empty(N * OH * OW * K, dtype=torch.bfloat16, device='cuda')
+            n_ = min(xf_.numel(), yf_.numel())
+            fns['copy'] = lambda: yf_[:n_].copy_(xf_[:n_])
+        if 'fill' in kinds:  # calibration: write-only stream of the output's bytes
+            yfl_ = torch.empty(N * OH * OW * K, dtype=torch.bfloat16, device='cuda')
+            fns['fill'] = lambda: yfl_.fill_(1.0)
+        if 'bcast' in kinds and k == 1 and K % C == 0:  # calibration: the 1x1 byte pattern (read x once, write y once)
+            xb_ = x.permute(0, 2, 3, 1).reshape(-1, 1, C)
+            yb_ = torch.empty(N * OH * OW, K // C, C, dtype=torch.bfloat16, device='cuda')
+            fns['bcast'] = lambda: yb_.copy_(xb_.expand(-1, K // C, C))
         for kind in kinds:
-            if kind == 'mm' and k != 1:
+            if (kind == 'mm' and k != 1) or kind not in fns:
                 continue
             us = bench(fns[kind])
             print(f'{kind:6s} N{N} C{C} {H}x{W} K{K} k{k} s{s}: {us:9.1f} us {fl / us / 1e6:8.1f} TFLOP/s '
