@@ -678,3 +678,150 @@ DMY_API int dmy_reduce_rows(const float* part, int P, int C, float* out, int acc
   reduce_rows_kernel<<<C, 256, 0, (hipStream_t)stream>>>(part, P, C, out, accumulate);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- SCConv gate with k3's BatchNorm folded in
+// SCConv (models/common.py:1279-1316): out = k3(x) * sigmoid(x + up(k2(x))), k3 = conv + BN (no activation).  Unfused,
+// k3's BN costs a bn_act_fwd pass (read z3, write u3) in the forward and a bn_bwd_reduce pass (read du3, z3) in the
+// backward, over the layer's largest tensors (64 channels @768^2 bs32: 2.4 GB each).  Here the gate reads z3 and applies
+// k3's BN scale / shift itself (u3 = bf16(z3 * scale + shift): the value bn_act_fwd would have stored), and the gate's
+// backward writes du3 AND k3's backward-reduce partials (sum du3, sum du3 * xhat3 over its rows; du3 as stored in
+// bf16), one row per block, so k3's ConvBNActFn backward skips bn_bwd_reduce (functional.BnLink).  Thread layout of the
+// BN streaming kernels (RowMap: a thread owns one 8-channel vector and walks rows), rows in order: deterministic.
+namespace {
+DEV int nearest_src_bn(int d, int in, int out) {  // ATen nearest index rule (= eltwise.hip nearest_src)
+  if (out == in) return d;
+  if (out == 2 * in) return d >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf(__fmul_rn((float)d, scale));
+  return s < in - 1 ? s : in - 1;
+}
+
+__global__ void __launch_bounds__(256) scgate_bn_fwd_kernel(const bf16* __restrict__ x, long xps,
+                                                            const bf16* __restrict__ z, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, const bf16* __restrict__ g,
+                                                            bf16* __restrict__ out, int N, int H, int W, int C, int GH,
+                                                            int GW) {
+  constexpr int VW = 8;
+  RowMap rm(C, VW);
+  if (!rm.active()) return;
+  const int c0 = rm.cv * VW;
+  float sc[VW], sh[VW];
+  ldf<VW>(scale + c0, sc);
+  ldf<VW>(shift + c0, sh);
+  const long M = (long)N * H * W, S = (long)gridDim.x * rm.RB;
+  for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S) {
+    const int w = (int)(m % W), h = (int)((m / W) % H), b = (int)(m / ((long)W * H));
+    const long gp = ((long)b * GH + nearest_src_bn(h, GH, H)) * GW + nearest_src_bn(w, GW, W);
+    const uint4 xv = *reinterpret_cast<const uint4*>(x + m * xps + c0);
+    const uint4 zv = *reinterpret_cast<const uint4*>(z + m * C + c0);
+    const uint4 gv = *reinterpret_cast<const uint4*>(g + gp * C + c0);
+    float xf[VW], zf[VW], gf[VW], o[VW];
+    unpack<bf16>(xv, xf);
+    unpack<bf16>(zv, zf);
+    unpack<bf16>(gv, gf);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const float u = to_f(from_f<bf16>(zf[j] * sc[j] + sh[j]));  // k3's BN output as bn_act_fwd stores it
+      const float sg = sigmoidf_(to_f(from_f<bf16>(xf[j] + gf[j])));
+      o[j] = u * to_f(from_f<bf16>(sg));
+    }
+    *reinterpret_cast<uint4*>(out + m * C + c0) = pack<bf16>(o);
+  }
+}
+
+__global__ void __launch_bounds__(256) scgate_bn_bwd_kernel(
+    const bf16* __restrict__ x, long xps, const bf16* __restrict__ z, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const bf16* __restrict__ g, const bf16* __restrict__ dout, bf16* __restrict__ du3, bf16* __restrict__ dpre, int N,
+    int H, int W, int C, int GH, int GW, float* __restrict__ pdb, float* __restrict__ pdg) {
+  constexpr int VW = 8;
+  __shared__ float red[2][256 * VW];
+  RowMap rm(C, VW);
+  const int c0 = rm.cv * VW;
+  float a[VW], bsum[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) a[j] = bsum[j] = 0.f;
+  if (rm.active()) {
+    float sc[VW], sh[VW], mu[VW], is[VW];
+    ldf<VW>(scale + c0, sc);
+    ldf<VW>(shift + c0, sh);
+    ldf<VW>(mean + c0, mu);
+    ldf<VW>(invstd + c0, is);
+    const long M = (long)N * H * W, S = (long)gridDim.x * rm.RB;
+    for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S) {
+      const int w = (int)(m % W), h = (int)((m / W) % H), b = (int)(m / ((long)W * H));
+      const long gp = ((long)b * GH + nearest_src_bn(h, GH, H)) * GW + nearest_src_bn(w, GW, W);
+      const uint4 xv = *reinterpret_cast<const uint4*>(x + m * xps + c0);
+      const uint4 zv = *reinterpret_cast<const uint4*>(z + m * C + c0);
+      const uint4 gv = *reinterpret_cast<const uint4*>(g + gp * C + c0);
+      const uint4 dv = *reinterpret_cast<const uint4*>(dout + m * C + c0);
+      float xf[VW], zf[VW], gf[VW], df[VW], du[VW], dp[VW];
+      unpack<bf16>(xv, xf);
+      unpack<bf16>(zv, zf);
+      unpack<bf16>(gv, gf);
+      unpack<bf16>(dv, df);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const float u = to_f(from_f<bf16>(zf[j] * sc[j] + sh[j]));
+        const float sg = sigmoidf_(to_f(from_f<bf16>(xf[j] + gf[j])));
+        dp[j] = df[j] * u * sg * (1.f - sg);
+        du[j] = df[j] * sg;
+      }
+      const uint4 duv = pack<bf16>(du);
+      *reinterpret_cast<uint4*>(du3 + m * C + c0) = duv;
+      *reinterpret_cast<uint4*>(dpre + m * C + c0) = pack<bf16>(dp);
+      float dr[VW];
+      unpack<bf16>(duv, dr);  // the reduce sees du3 as stored, as bn_bwd_reduce would read it
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        a[j] += dr[j];
+        bsum[j] += dr[j] * (zf[j] - mu[j]) * is[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    red[0][threadIdx.x * VW + j] = a[j];
+    red[1][threadIdx.x * VW + j] = bsum[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int cv = c / VW, j = c % VW;
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = 0; r < rm.RB; ++r) {
+      const int t = r * rm.CV + cv;
+      s1 += red[0][t * VW + j];
+      s2 += red[1][t * VW + j];
+    }
+    pdb[(long)blockIdx.x * C + c] = s1;
+    pdg[(long)blockIdx.x * C + c] = s2;
+  }
+}
+}  // namespace
+
+static bool scgate_bn_ok(int C, long xps, const void* x, const void* z, const void* g, const void* o) {
+  return C % 8 == 0 && C / 8 <= 256 && xps % 8 == 0 && vec_ok(8, C, xps, 0, 0, x, z, g) && vec_ok(8, C, 0, 0, 0, o, nullptr, nullptr);
+}
+
+DMY_API int dmy_scgate_bn_rows(int N, int H, int W, int C) { return vec_grid((long)N * H * W, C, 8); }
+
+DMY_API int dmy_scgate_bn_fwd(const void* x, long xps, const void* z, const float* scale, const float* shift,
+                              const void* g, void* out, int N, int H, int W, int C, int GH, int GW, void* stream) {
+  if (!scgate_bn_ok(C, xps, x, z, g, out)) return (int)hipErrorInvalidValue;
+  const int grid = dmy_scgate_bn_rows(N, H, W, C);
+  scgate_bn_fwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)x, xps, (const bf16*)z, scale, shift,
+                                                              (const bf16*)g, (bf16*)out, N, H, W, C, GH, GW);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_scgate_bn_bwd(const void* x, long xps, const void* z, const float* scale, const float* shift,
+                              const float* mean, const float* invstd, const void* g, const void* dout, void* du3,
+                              void* dpre, int N, int H, int W, int C, int GH, int GW, float* pdb, float* pdg,
+                              void* stream) {
+  if (!scgate_bn_ok(C, xps, x, z, g, du3) || !vec_ok(8, C, 0, 0, 0, dout, dpre, nullptr)) return (int)hipErrorInvalidValue;
+  const int grid = dmy_scgate_bn_rows(N, H, W, C);
+  scgate_bn_bwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const bf16*)x, xps, (const bf16*)z, scale, shift, mean,
+                                                              invstd, (const bf16*)g, (const bf16*)dout, (bf16*)du3,
+                                                              (bf16*)dpre, N, H, W, C, GH, GW, pdb, pdg);
+  return (int)hipGetLastError();
+}

@@ -76,6 +76,9 @@ SIGNATURES = {
     'dmy_bifpn_wgrad': [P, I, I, P, F, P, P],
     'dmy_scgate_fwd': [I, P, L, P, P, P, I, I, I, I, I, I, P],
     'dmy_scgate_bwd': [I, P, L, P, P, P, P, P, L, I, I, I, I, I, I, I, P],
+    'dmy_scgate_bn_rows': [I, I, I, I],
+    'dmy_scgate_bn_fwd': [P, L, P, P, P, P, P, I, I, I, I, I, I, P],
+    'dmy_scgate_bn_bwd': [P, L, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P],
     'dmy_ca_pool_fwd': [I, P, L, P, I, I, I, I, P],
     'dmy_ca_pool_bwd': [I, P, P, L, I, I, I, I, I, P],
     'dmy_ca_apply_fwd': [I, P, L, P, P, P, L, I, I, I, I, P],

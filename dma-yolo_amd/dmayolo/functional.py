@@ -235,12 +235,13 @@ class WeightPrep:
 class ConvSpec:
     """Static description of one conv(+BN)(+act) layer; `bn` is the live nn.BatchNorm2d (or None).
     wcache / ecache: inference-only caches of the prepped weight and the eval BN coefficients."""
-    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', 'fp8', 'f8cache', 'f8_emit', '__weakref__')
+    __slots__ = ('stride', 'pad', 'act', 'bn', 'wcache', 'ecache', 'fp8', 'f8cache', 'f8_emit', 'defer', '__weakref__')
 
     def __init__(self, stride, pad, act, bn=None):
         self.stride, self.pad, self.act, self.bn = int(stride), int(pad), int(act), bn
         self.wcache = self.ecache = self.f8cache = self.f8_emit = None
         self.fp8 = False
+        self.defer = False  # deferred_affine(): the consumer applies this layer's BN (see SCGateFn)
 
 
 _SPECS = weakref.WeakKeyDictionary()
@@ -508,6 +509,11 @@ class BnLink:
 # 3421 -> 3325 (profiles/r02/ab_bnfuse.log): the epilogue's extra z stream and reduction lengthen the data-grad by
 # more than the separate streaming bn_bwd_reduce pass it saves.
 FUSE_BN_REDUCE = [os.environ.get('DMY_FUSE_BN_REDUCE', '0') == '1']
+# SCConv's k3 BatchNorm applied by its gate (SCGateFn, dmy_scgate_bn_*): DMY_DEFER_AFFINE=0 restores the separate
+# bn_act_fwd / bn_bwd_reduce passes
+DEFER_AFFINE = [os.environ.get('DMY_DEFER_AFFINE', '1') == '1']
+# backward BN partials (> 256 rows) folded by the two-stage column sum before the finalize (DMY_BWD_COLSUM=0: off)
+BWD_COLSUM = [os.environ.get('DMY_BWD_COLSUM', '1') == '1']
 
 
 class ConvBNActFn(torch.autograd.Function):
@@ -621,6 +627,26 @@ class ConvBNActFn(torch.autograd.Function):
                 _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
                 call('dmy_bn_eval_coef', ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
                      float(bn.eps), K, ptr(scale), ptr(shift), stream())
+            defer = (spec.defer and DEFER_AFFINE[0] and train_bn and need_grad and dt == torch.bfloat16 and
+                     spec.act == ACT_NONE and res is None and out is None and K % 8 == 0 and f8 is None)
+            if defer:
+                # the consumer (SCGateFn) reads z and applies scale / shift itself, and hands this layer's backward the
+                # reduce partials (BnLink): the tensor returned is z, valid only for that consumer
+                ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
+                ctx.bnlink = BnLink(z, scale, shift, mean, invstd, spec.act, K)
+                z._dmy_affine, z._dmy_bnlink = (scale, shift, mean, invstd), ctx.bnlink
+                ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, False
+                ctx.link_in = link_in if (link_in is not None and not s2d and Cp == C and link_in.K == C and
+                                          link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
+                ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
+                ctx.ggeom = (Hg, Wg, kg, sg, pg)
+                ctx.cp = Cp
+                ctx.has_bias = bias is not None
+                ctx.xsink, ctx.rsink = xsink, rsink
+                ctx.arena = WgradArena.current
+                ctx.wkey = weight.data_ptr()
+                ctx.pkeys = tuple(t.data_ptr() if t is not None else None for t in (bias, gamma, beta))
+                return z
             y = out if out is not None else new_act(N, K, OH, OW, x)
             emit = spec.f8_emit if (F8_DELAYED[0] and dt == torch.bfloat16 and K % 8 == 0 and yps % 8 == 0 and
                                     (res is None or rps % 8 == 0)) else None
@@ -689,17 +715,19 @@ class ConvBNActFn(torch.autograd.Function):
                     link.ready = None
                 if rd is not None and rd[0].data_ptr() == dy.data_ptr() and rd[1] == dps and \
                         rd[0]._version == rd[5]:
-                    _, _, pdb, pdg, P, _ = rd  # written by the consumer's data-grad epilogue (a row per tile)
-                    if P > 256:  # two-stage column reduction, as for the forward epilogue partials
-                        S = call('dmy_colsum2_rows', P)
-                        pd2, pg2 = f32(S * K, dev), f32(S * K, dev)
-                        call('dmy_colsum2', ptr(pdb), ptr(pdg), P, K, ptr(pd2), ptr(pg2), stream())
-                        pdb, pdg, P = pd2, pg2, S
+                    _, _, pdb, pdg, P, _ = rd  # written by the consumer (data-grad epilogue / SCConv gate)
                 else:
                     P = call('dmy_bn_reduce_rows', dt, ptr(z), K, ptr(dy), dps, M, K)
                     pdb, pdg = f32(P * K, dev), f32(P * K, dev)
                     call('dmy_bn_bwd_reduce', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean),
                          ptr(invstd), spec.act, M, K, ptr(pdb), ptr(pdg), stream())
+                if P > 256 and BWD_COLSUM[0]:
+                    # up to 4096 block rows: the one-block-per-channel finalize read them with a stride of K floats in
+                    # 20 us per layer (97 layers per DMA-1536 step); the two-stage column sum reads them coalesced
+                    S = call('dmy_colsum2_rows', P)
+                    pd2, pg2 = f32(S * K, dev), f32(S * K, dev)
+                    call('dmy_colsum2', ptr(pdb), ptr(pdg), P, K, ptr(pd2), ptr(pg2), stream())
+                    pdb, pdg, P = pd2, pg2, S
                 dgamma, dbeta = pgrad(ctx.pkeys[1]), pgrad(ctx.pkeys[2])
                 call('dmy_bn_bwd_finalize', ptr(pdb), ptr(pdg), P, K, float(M), ptr(gamma), ptr(invstd), ptr(dgamma),
                      ptr(dbeta), ptr(ca), ptr(cb), ptr(cc), stream())
@@ -785,13 +813,15 @@ class ConvBNActFn(torch.autograd.Function):
         return dx, dw, dbias, dgamma, dbeta, dres, None, None, None, None
 
 
-def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None, out=None):
+def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsink=None, rsink=None, out=None,
+                defer=False):
     """xsink / rsink: GradSinks collecting the gradient of x / of the residual (see GradSink).  out: an NHWC view
     (a concat_buffer channel slice) the activation is written into instead of a fresh tensor, when the layer has a
     separate activation pass (BN and / or act / residual); the returned tensor is then that view."""
     if spec is None:  # a persistent spec per weight PARAMETER (views made per call share their base), so the
         # inference caches (prepped weight, eval BN coefficients) hold across calls for the Detect / Swin / CBAM convs
         spec = _param_spec(weight._base if weight._base is not None else weight, stride, pad, act, bn)
+    spec.defer = bool(defer)
     gamma = bn.weight if bn is not None else None
     beta = bn.bias if bn is not None else None
     _OUT[0] = out
@@ -952,18 +982,29 @@ def ctypes_off(t, c0):
 # ------------------------------------------------------------------ SCConv gate / CoorAttention
 
 class SCGateFn(torch.autograd.Function):
-    """out = u3 * sigmoid(x + nearest(g))  (models/common.py:1311-1314)."""
+    """out = u3 * sigmoid(x + nearest(g))  (models/common.py:1311-1314).  When u3 is k3's deferred BN output (z with
+    `_dmy_affine`, conv_bn_act(defer=True)), the gate applies k3's BN scale / shift to z itself and its backward writes
+    k3's BN backward-reduce partials into k3's BnLink (dmy_scgate_bn_fwd / _bwd), so k3's bn_act_fwd and
+    bn_bwd_reduce passes disappear."""
 
     @staticmethod
     def forward(ctx, x, u3, g, sink=None):
         ctx.sink = sink
+        aff, link = getattr(u3, '_dmy_affine', None), getattr(u3, '_dmy_bnlink', None)
         x, xps = pixel_stride(x)
-        u3 = u3.contiguous(memory_format=CL)
         g = g.contiguous(memory_format=CL)
         N, C, H, W = x.shape
         GH, GW = g.shape[2:]
         out = new_act(N, C, H, W, x)
-        call('dmy_scgate_fwd', dcode(x), ptr(x), xps, ptr(u3), ptr(g), ptr(out), N, H, W, C, GH, GW, stream())
+        ctx.aff = ctx.link = None
+        if aff is not None:
+            assert pixel_stride(u3)[0] is u3 and u3.stride(1) == 1 and u3.stride(3) == C, 'deferred z must be dense NHWC'
+            call('dmy_scgate_bn_fwd', ptr(x), xps, ptr(u3), ptr(aff[0]), ptr(aff[1]), ptr(g), ptr(out), N, H, W, C, GH,
+                 GW, stream())
+            ctx.aff, ctx.link = aff, link
+        else:
+            u3 = u3.contiguous(memory_format=CL)
+            call('dmy_scgate_fwd', dcode(x), ptr(x), xps, ptr(u3), ptr(g), ptr(out), N, H, W, C, GH, GW, stream())
         ctx.save_for_backward(x, u3, g)
         ctx.xps = xps
         return out
@@ -977,8 +1018,17 @@ class SCGateFn(torch.autograd.Function):
         du3 = new_act(N, C, H, W, x)
         # d(x + up(g)) -> x's gradient sink; the resize backward of g needs it on its own
         dpre = new_act(N, C, H, W, x)
-        call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), C, 0, N, H,
-             W, C, GH, GW, stream())
+        if ctx.aff is not None:
+            sc, sh, mean, invstd = ctx.aff
+            P = call('dmy_scgate_bn_rows', N, H, W, C)
+            pdb, pdg = f32(P * C, x.device), f32(P * C, x.device)
+            call('dmy_scgate_bn_bwd', ptr(x), ctx.xps, ptr(u3), ptr(sc), ptr(sh), ptr(mean), ptr(invstd), ptr(g),
+                 ptr(dout), ptr(du3), ptr(dpre), N, H, W, C, GH, GW, ptr(pdb), ptr(pdg), stream())
+            # k3's ConvBNActFn backward takes these partials iff the gradient it receives IS du3, unmodified
+            ctx.link.ready = (du3, C, pdb, pdg, P, du3._version)
+        else:
+            call('dmy_scgate_bwd', dcode(x), ptr(x), ctx.xps, ptr(u3), ptr(g), ptr(dout), ptr(du3), ptr(dpre), C, 0,
+                 N, H, W, C, GH, GW, stream())
         dg = new_act(N, C, GH, GW, x)
         call('dmy_resize_bwd', dcode(x), ptr(dpre), C, ptr(dg), C, N, GH, GW, H, W, C, stream())
         dx = dpre if ctx.sink is None else ctx.sink.passthrough(dpre)

@@ -49,14 +49,15 @@ def _pad_int(p):
     return p if isinstance(p, int) else p[0]
 
 
-def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None, out=None):
+def conv_forward(conv, bn, act, x, res=None, xsink=None, rsink=None, out=None, defer=False):
     """conv (nn.Conv2d, groups=1, dilation=1) -> optional BN -> act (+ residual) on the HIP path.
-    xsink / rsink: Fn.GradSink for the gradients of x / res when they have other consumers."""
+    xsink / rsink: Fn.GradSink for the gradients of x / res when they have other consumers.  defer: a train-mode BN
+    layer without activation returns its pre-BN output for a consumer that applies the BN itself (SCConv's gate)"""
     assert conv.groups == 1 and conv.dilation in (1, (1, 1)), 'grouped/dilated conv not on the DMA-YOLO path'
     s = conv.stride if isinstance(conv.stride, int) else conv.stride[0]
     pad, a = _pad_int(conv.padding), act_code(act)
     return Fn.conv_bn_act(x, conv.weight, conv.bias, bn, s, pad, a, res=res, spec=Fn.spec_for(conv, s, pad, a, bn),
-                          xsink=xsink, rsink=rsink, out=out)
+                          xsink=xsink, rsink=rsink, out=out, defer=defer)
 
 
 class Conv(nn.Module):
@@ -196,7 +197,7 @@ class SCConv(nn.Module):
         r = r if isinstance(r, int) else r[0]
         sk = Fn.GradSink(3) if xsink is None else xsink.expect(3)  # x -> avg-pool (k2), k3, the gate
         g = conv_forward(self.k2[1], self.k2[2], None, Fn.AvgPoolFn.apply(x, r, sk))
-        u3 = conv_forward(self.k3[0], self.k3[1], None, x, xsink=sk)
+        u3 = conv_forward(self.k3[0], self.k3[1], None, x, xsink=sk, defer=True)  # BN applied by the gate
         return conv_forward(self.k4[0], self.k4[1], None, Fn.SCGateFn.apply(x, u3, g, sk))
 
 

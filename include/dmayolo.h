@@ -160,6 +160,15 @@ int dmy_scgate_fwd(int dtype, const void* x, long xps, const void* u3, const voi
                    int C, int GH, int GW, void* stream);
 int dmy_scgate_bwd(int dtype, const void* x, long xps, const void* u3, const void* g, const void* dout, void* du3,
                    void* dpre, long dpps, int accumulate, int N, int H, int W, int C, int GH, int GW, void* stream);
+/* the same gate with k3's BatchNorm (common.py:1296-1300) folded in (bf16): the forward reads k3's pre-BN conv output z
+   and applies scale / shift; the backward also writes k3's BN backward-reduce partials, one row per block
+   (dmy_scgate_bn_rows rows of C floats each) */
+int dmy_scgate_bn_rows(int N, int H, int W, int C);
+int dmy_scgate_bn_fwd(const void* x, long xps, const void* z, const float* scale, const float* shift, const void* g,
+                      void* out, int N, int H, int W, int C, int GH, int GW, void* stream);
+int dmy_scgate_bn_bwd(const void* x, long xps, const void* z, const float* scale, const float* shift,
+                      const float* mean, const float* invstd, const void* g, const void* dout, void* du3, void* dpre,
+                      int N, int H, int W, int C, int GH, int GW, float* pdb, float* pdg, void* stream);
 /* CoorAttention pooling + re-weighting: common.py:1183-1207 */
 int dmy_ca_pool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, void* stream);
 int dmy_ca_pool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C,
