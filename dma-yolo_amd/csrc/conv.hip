@@ -1889,12 +1889,12 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
 // G3: the same streaming GEMM over a 3x3 stride-1 pad-1 gather of a 16-channel input (the space-to-depth stem of every
 // yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
 // 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
-template <int KD, int NTH, bool G3 = false>
+template <int KD, int NTH, bool G3 = false, bool EPI = false>
 __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                 long M, int NC, int ng, long xps, long yps, unsigned xbytes,
-                                                int ntiles, int kwrow, int H, int W) {
+                                                int ntiles, int kwrow, int H, int W, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
   constexpr int NG2 = KD <= 128 ? 2 : 1, CP = 32 * NG2;  // 32-channel groups per column pass (registers: KD 160 / 256 keep 1)
@@ -2031,7 +2031,16 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
           v.w = s1[1];
           if (m < M) {
             uint4* dst = reinterpret_cast<uint4*>(y + m * yps + nb + gr * 32 + chq);
-            if (accumulate) {
+            if (EPI && ep.on) {  // eval BN scale / shift + act (+ residual) on the bf16-rounded conv output (epi_store)
+              const int n = nb + gr * 32 + chq;
+              float f[8], r8[8], sc[8], sh[8];
+              unpack<bf16>(v, f);
+              if (ep.res != nullptr)
+                unpack<bf16>(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(ep.res) + m * ep.rps + n), r8);
+              epi_coef8(ep, n, sc, sh);
+              epi_apply8(ep.act, f, sc, sh, ep.res != nullptr ? r8 : nullptr);
+              v = pack<bf16>(f);
+            } else if (accumulate) {
               float f[8], o[8];
               unpack<bf16>(v, f);
               unpack<bf16>(*dst, o);
@@ -3547,6 +3556,11 @@ inline int p1s_mode() {
   static int t = env_int("DMY_P1S", 1);
   return t;
 }
+// eval forwards (inference epilogue: eval BN + act + residual in the store loop) on conv_p1s too: DMY_P1S_EP = 1 (default)
+inline int p1s_eval() {
+  static int t = env_int("DMY_P1S_EP", 1);
+  return t;
+}
 inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
   if (!p1s_mode() || gv.KH != 1 || gv.KW != 1 || gv.S != 1 || gv.P != 0) return false;
   if (gv.C != 64 && gv.C != 128 && gv.C != 256) return false;
@@ -3562,9 +3576,9 @@ inline bool stem_s_ok(const Geom& gv, const void* x, const void* w, const void* 
     return false;
   return 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps) < (double)v3::kBufOob && (long)gv.N * gv.H * gv.W < (1L << 31);
 }
-template <int KD, int NTH, bool G3 = false>
+template <int KD, int NTH, bool G3 = false, bool EPI = false>
 int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
-                  const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
+                  const Geom& gv, hipStream_t st, int lds_kib, int bpc, const Epi& ep = Epi{}) {
   constexpr int pitch_b = (KD + 8) * 2, scratch = NTH / 64 * 256;
   const long M = (long)gv.N * gv.OH * gv.OW;
   int ng = ((lds_kib * 1024 - scratch) / pitch_b) / 32 * 32;
@@ -3574,7 +3588,7 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   const int lds = ng * pitch_b + scratch;
   static bool raised = false;
   if (!raised) {
-    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     raised = true;
   }
@@ -3584,14 +3598,16 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   if (nbx > maxb) nbx = maxb;
   const dim3 grid((unsigned)nbx, (unsigned)G);
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps);
-  v3::conv_p1s<KD, NTH, G3><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
-                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W);
+  v3::conv_p1s<KD, NTH, G3, EPI><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
+                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W, ep);
   return (int)hipGetLastError();
 }
 inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
-                      const Geom& gv, hipStream_t st) {
+                      const Geom& gv, hipStream_t st, const Epi& ep = Epi{}) {
   static const int nth = env_int("DMY_P1S_NTH", 512), lds = env_int("DMY_P1S_LDS", 160), bpc = env_int("DMY_P1S_BPC", 1);
-#define P1S_GO(KD_, NTH_) return launch_p1s_kd<KD_, NTH_>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc)
+#define P1S_GO(KD_, NTH_)                                                                      \
+  return ep.on ? launch_p1s_kd<KD_, 512, false, true>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc, ep) \
+               : launch_p1s_kd<KD_, NTH_>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc, ep)
   if (gv.C == 64) {
     if (nth == 1024) P1S_GO(64, 1024);
     if (nth == 512) P1S_GO(64, 512);
@@ -3754,10 +3770,13 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
               hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}, int tov = -1) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
-  if (!ep.on && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
-    return launch_p1s(x, w, b, y, ps, pq, acc, gv, st);
-  if (!DG && !ep.on && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
-    return launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  // eval epilogue on the streaming kernels (forward, no accumulate): the residual read as 16-B vectors
+  const bool ep_ok = !ep.on || (!DG && !acc && p1s_eval() && (ep.res == nullptr || (ep.rps % 8 == 0 && aligned16(ep.res))));
+  if (ep_ok && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
+    return launch_p1s(x, w, b, y, ps, pq, acc, gv, st, ep);
+  if (!DG && ep_ok && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
+    return ep.on ? launch_p1s_kd<160, 768, true, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
+                 : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep);
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
   const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;

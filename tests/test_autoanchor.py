@@ -68,3 +68,19 @@ def test_kmean_anchors_reproducible_and_fits():
     wh = torch.tensor(label_wh(shapes, labels, 640), dtype=torch.float32)
     best = _ratio_metric(torch.tensor(outs[0], dtype=torch.float32), wh)[1]
     assert float((best > 0.25).float().mean()) > 0.98
+
+
+def test_anchor_metric_known_answers():
+    """utils/autoanchor.py:35-37 / 86-90 on hand-made boxes (a known-answer check of the restated metric, since the
+    reference's own run is unavailable): a label equal to an anchor scores 1; w and h off by 2x and 4x score min(1/2,
+    1/4) = 0.25; the best anchor is the closer one; BPR counts best > 1/thr"""
+    from dmayolo.utils.autoanchor import _ratio_metric
+    k = torch.tensor([[10.0, 20.0], [40.0, 40.0]])
+    wh = torch.tensor([[10.0, 20.0], [20.0, 80.0], [40.0, 40.0], [5.0, 10.0], [160.0, 10.0]])
+    x, best = _ratio_metric(k, wh)
+    exp_x = torch.tensor([[1.0, 0.25], [0.25, 0.5], [0.25, 1.0], [0.5, 0.125], [1 / 16, 0.25]])
+    torch.testing.assert_close(x, exp_x)
+    torch.testing.assert_close(best, torch.tensor([1.0, 0.5, 1.0, 0.5, 0.25]))
+    thr = 4.0
+    assert abs(float((best > 1 / thr).float().mean()) - 0.8) < 1e-7  # BPR: 4 of 5 labels have an anchor inside 4x
+    assert abs(float((x > 1 / thr).float().sum(1).mean()) - 0.8) < 1e-7  # AAT: anchors above threshold per label
