@@ -157,15 +157,18 @@ __global__ void __launch_bounds__(256) bn_act_fwd_vec(const T* __restrict__ z, l
 // y = act(z * scale + shift) (+ res) as bn_act_fwd_vec (bf16), plus y8[m][c] = e4m3(y * 448 / amax) dense, where amax
 // is the PREVIOUS step's max |y| (the G block maxima `pmax` it left, reduced here by every block; block 0 records it
 // in used[0] for the conv's dequantisation), and this step's block maxima go to nmax[blockIdx.x] for the next step.
-// Values above the previous amax saturate at +-448 (delayed scaling).  A NaN anywhere makes the next amax NaN.
+// Values above the previous amax x headroom saturate at +-448 (delayed scaling); nsat (optional, G floats) receives
+// each block's count of saturated elements, so the clipping a growing activation range causes is visible.
+// A NaN anywhere makes the next amax NaN.
 __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restrict__ z, long zps,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift, int act,
                                                             const bf16* __restrict__ res, long rps, bf16* __restrict__ y,
                                                             long yps, long M, int C, unsigned char* __restrict__ y8,
                                                             const float* __restrict__ pmax, int G,
-                                                            float* __restrict__ nmax, float* __restrict__ used) {
-  __shared__ float red[4];
+                                                            float* __restrict__ nmax, float* __restrict__ used,
+                                                            float headroom, float* __restrict__ nsat) {
+  __shared__ float red[4], rsat[4];
   float a = 0.f;
   for (int i = threadIdx.x; i < G; i += 256) a = nanmax(a, pmax[i]);
 #pragma unroll
@@ -174,10 +177,11 @@ __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restri
   __syncthreads();
   a = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
   __syncthreads();
+  a *= headroom;
   if (blockIdx.x == 0 && threadIdx.x == 0) used[0] = a;
-  const float inv = a > 0.f ? 448.f / a : 1.f;
+  const float inv = a > 0.f ? 448.f / a : 1.f, thr = a > 0.f ? a : 448.f;  // |v| > thr saturates
   RowMap rm(C, 8);
-  float mx = 0.f;
+  float mx = 0.f, sat = 0.f;
   if (rm.active()) {
     const int c0 = rm.cv * 8;
     float sc[8], sh[8];
@@ -199,7 +203,10 @@ __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restri
       *reinterpret_cast<uint4*>(y + m * yps + c0) = v;
       unpack<bf16>(v, f);  // quantise the stored (bf16-rounded) value, as a separate pass over y would
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mx = nanmax(mx, fabsf(f[j]));
+      for (int j = 0; j < 8; ++j) {
+        mx = nanmax(mx, fabsf(f[j]));
+        sat += fabsf(f[j]) > thr ? 1.f : 0.f;
+      }
       uint2 o;
       o.x = pack4_e4m3(f[0] * inv, f[1] * inv, f[2] * inv, f[3] * inv);
       o.y = pack4_e4m3(f[4] * inv, f[5] * inv, f[6] * inv, f[7] * inv);
@@ -208,9 +215,17 @@ __global__ void __launch_bounds__(256) bn_act_fwd_f8_kernel(const bf16* __restri
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = nanmax(mx, __shfl_xor(mx, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sat += __shfl_xor(sat, o, 64);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = mx;
+    rsat[threadIdx.x >> 6] = sat;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) nmax[blockIdx.x] = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    nmax[blockIdx.x] = nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3]));
+    if (nsat) nsat[blockIdx.x] = (rsat[0] + rsat[1]) + (rsat[2] + rsat[3]);
+  }
 }
 
 template <typename T>
@@ -581,12 +596,14 @@ DMY_API int dmy_bn_act_f8_blocks(void) { return 1024; }
 
 DMY_API int dmy_bn_act_fwd_f8(const void* z, long zps, const float* scale, const float* shift, int act, const void* res,
                               long rps, void* y, long yps, long M, int C, void* y8, const float* pmax, float* nmax,
-                              float* used, void* stream) {
-  if (C % 8 != 0 || C / 8 > 256 || !vec_ok(8, C, zps, yps, res ? rps : 0, z, y, res) || ((uintptr_t)y8 & 7))
+                              float* used, float headroom, float* nsat, void* stream) {
+  if (C % 8 != 0 || C / 8 > 256 || !vec_ok(8, C, zps, yps, res ? rps : 0, z, y, res) || ((uintptr_t)y8 & 7) ||
+      !(headroom >= 1.f))
     return (int)hipErrorInvalidValue;
   const int G = dmy_bn_act_f8_blocks();
   bn_act_fwd_f8_kernel<<<G, 256, 0, (hipStream_t)stream>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps,
-                                                          (bf16*)y, yps, M, C, (unsigned char*)y8, pmax, G, nmax, used);
+                                                          (bf16*)y, yps, M, C, (unsigned char*)y8, pmax, G, nmax, used,
+                                                          headroom, nsat);
   return (int)hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 #include "common.h"
 #include <cstdlib>
 #include <type_traits>
+#include <atomic>
 #include <cmath>
 
 // s_setprio(1) around the MFMA cluster of the LDS-DMA main loops (cdna_hip_programming.md §5.5 T5);
@@ -2181,7 +2182,7 @@ __global__ void __launch_bounds__(256) conv_sk(const bf16* __restrict__ x, const
 // lane's agent-scope release + drain before a relaxed agent ticket; the reducer's one lane acquires at agent scope, drains,
 // and the barrier covers the workgroup; any XCD placement of a tile's splits is correct).  The tickets live in a device
 // array zeroed at load and re-zeroed by each tile's reducer, so launches that use it must not run concurrently on two
-// streams (the eval forward is one stream).
+// streams: launch_splitk gives the in-launch combine to the first stream that uses it only.
 constexpr int kSplitCnt = 8192;
 __device__ int g_split_cnt[kSplitCnt];
 
@@ -2946,6 +2947,90 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
   for (int e = threadIdx.x; e < BM * BN; e += 512) {
     const int row = e / BN, m = m0 + row;
     if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
+  }
+}
+
+// Weight-grad, wide tile (round 4): BM x BN = 256 x 256 (256 output channels x 256 GEMM columns), 8 waves of 128 x 64
+// (WM = 2 x WN = 4, 128 accumulators per lane), a 2-stage LDS-DMA ring of 64 KiB stages (the next stage streams in
+// under the current one's MFMAs, as the forward wide tile).  Against the 256 x 128 tile of conv_wgrad_v4: a wave reads
+// (128 + 64) x 64 bf16 of LDS per K step for 64 MFMAs instead of (64 + 64) x 64 for 32, and a split's dy rows are read
+// once per 256 columns instead of once per 128 -- the 1x1 weight-grads with >= 256 input and output channels run at
+// 750-865 TF/s (30-35 % of the MFMA peak) on the 256 x 128 tile.  The fp32 tile leaves through LDS in two 128-row
+// halves (the whole 256 x 260 fp32 tile would not fit).
+template <int BM, int BN>
+__global__ void __launch_bounds__(512) conv_wgrad_w(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                    float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn,
+                                                    unsigned xbytes, unsigned dybytes) {
+  constexpr int WM = BM / 128, NS = 2;
+  static_assert(WM * (BN / 64) == 8, "8 waves of 128 x 64");
+  using LD = WgradLdsNB<BM, BN, 8>;
+  constexpr int STAGE = WgradLdsN<BM, BN>::STAGE;
+  constexpr int RS = BN + 4;
+  constexpr int CT = 128 * RS * 4;  // one 128-row half of the fp32 tile
+  constexpr int LDSB = NS * STAGE > CT ? NS * STAGE : CT;
+  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = lin % (gm * gn), split = lin / (gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long NP = (long)g.N * g.OH * g.OW;
+  const int nk_all = (int)((NP + 63) / 64);
+  const int kt0 = split * kt_per_split;
+  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    LD ld(x, dy, g, m0, n0, kt0, wid, lane, xbytes, dybytes);
+    ld.issue(smem, wid);
+    for (int kt = 0; kt < nk; ++kt) {
+      vm_wait<0>();  // stage kt landed (the only stage in flight)
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < nk) ld.issue(smem + ((kt + 1) % NS) * STAGE, wid);  // under this step's MFMAs
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[8], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag_k<BN>(Bs, wn * 64 + j * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = frag_k<BM>(As, wm * 128 + i * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  vm_wait<0>();
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+  const int Ntot = g.KH * g.KW * g.C;
+  static_assert(512 % BN == 0, "epilogue column must be fixed per thread");
+  const int c = threadIdx.x % BN, n = n0 + c;
+  const long coff = wgrad_col(g, n);
+#pragma unroll
+  for (int hh = 0; hh < WM; ++hh) {  // 128-row halves: the waves of wave row hh stage theirs, every thread stores
+    if (wm == hh) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 128 * BN; e += 512) {
+      const int row = e / BN, m = m0 + hh * 128 + row;
+      if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
+    }
+    __syncthreads();
   }
 }
 
@@ -3915,7 +4000,12 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   // Measured SLOWER on the bs1 detect (profiles/r03/det_splitk_fused_ab.log: DMA-1536 4.52 -> 5.19 ms, yolov5s 0.79 ->
   // 1.17 ms): 256 KB of slabs per tile read serially by one reducer block + a release per block
   static const int fz = env_int("DMY_SPLITK_FUSED", 0);
-  const int fused = fz && gm * gn <= v3::kSplitCnt ? 1 : 0;
+  // the tickets are one device array: the stream of the first fused launch owns them, any other stream takes the
+  // two-launch path (two streams' fused launches would share counters)
+  static std::atomic<hipStream_t> owner{nullptr};
+  hipStream_t none = nullptr;
+  const bool mine = fz && (owner.compare_exchange_strong(none, st) || none == st);
+  const int fused = mine && gm * gn <= v3::kSplitCnt ? 1 : 0;
   if (g.K > 64) {
     if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
     else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
@@ -4196,12 +4286,13 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_
     splits = (wgrad_target() + tiles / 2) / tiles;
     if (splits < 1) splits = 1;
   } else {
-    // launch_wgrad_v3's model with one resident block per CU, twice the tile per K step and atomics
-    const double R = num_cus();
+    // launch_wgrad_v3's model with one resident block per CU, twice the tile per K step and atomics (the wide
+    // 256 x 256 tile: twice that again, per K step and per epilogue)
+    const double R = num_cus(), sc = (double)BM * BN / (256.0 * 128.0);
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
       const double blocks = (double)tiles * sp;
-      const double t = ceil(blocks / R) * ceil_div(nk, sp) * 1.9 * 2 * 0.5 + blocks * 0.0504 * 2;
+      const double t = ceil(blocks / R) * ceil_div(nk, sp) * 1.9 * 2 * 0.5 * sc + blocks * 0.0504 * 2 * sc;
       if (t < best) { best = t; splits = sp; }
     }
   }
@@ -4212,9 +4303,18 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_
   if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
-  v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  if constexpr (BM == 256 && BN == 256)
+    v3::conv_wgrad_w<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  else
+    v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
+}
+// the wide 256 x 256 weight-grad tile (v3::conv_wgrad_w) for K_out >= 256 and >= 256 GEMM columns: DMY_WGRAD_W = 1 on
+// (default), 0 off
+inline int wgrad_w_mode() {
+  static int t = env_int("DMY_WGRAD_W", 1);
+  return t;
 }
 
 // tap-fused 3x3 s1 weight-grad (v3::conv_wgrad_tap): 0 = off, 1 = on (default) where it applies
@@ -4345,6 +4445,8 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
                        : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
         db4 < (double)v3::kBufOob) {
+      if (wgrad_w_mode() && g.K >= 256 && Ntot >= 256)
+        return launch_wgrad_v4<256, 256>((const bf16*)x, (const bf16*)dy, dw, g, st);
       if (v4 == 2 || (v4 == 3 && g.K >= 256)) return launch_wgrad_v4<256, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
       if (v4 == 1) return launch_wgrad_v4<128, 256>((const bf16*)x, (const bf16*)dy, dw, g, st);
     }

@@ -55,7 +55,7 @@ SIGNATURES = {
     'dmy_bn_eval_coef': [P, P, P, P, F, I, P, P, P],
     'dmy_bn_act_fwd': [I, P, L, P, P, I, P, L, P, L, L, I, P],
     'dmy_bn_act_f8_blocks': [],
-    'dmy_bn_act_fwd_f8': [P, L, P, P, I, P, L, P, L, L, I, P, P, P, P, P],
+    'dmy_bn_act_fwd_f8': [P, L, P, P, I, P, L, P, L, L, I, P, P, P, P, F, P, P],
     'dmy_bn_bwd_reduce': [I, P, L, P, L, P, P, P, P, I, L, I, P, P, P],
     'dmy_bn_bwd_finalize': [P, P, I, I, D, P, P, P, P, P, P, P, P],
     'dmy_bn_bwd_apply': [I, P, L, P, L, P, P, P, P, I, P, P, P, P, L, L, I, P],

@@ -309,26 +309,52 @@ def _f8_ws():
 F8_DELAYED = [os.environ.get('DMY_F8_DELAYED', '1') == '1']
 
 
+# headroom on the delayed amax (DMY_F8_HEADROOM, >= 1; 1 = none): a margin against an activation range that grows
+# between steps, at the cost of log2(headroom) bits of e4m3 resolution
+F8_HEADROOM = [float(os.environ.get('DMY_F8_HEADROOM', '1'))]
+
+
 class F8Emit:
     """Per producer layer: two ping-pong arrays of block maxima (this step's |y| maxima become the next step's
-    quantisation amax).  The first step only records maxima (its consumer quantises just in time)."""
-    __slots__ = ('buf', 'p', 'valid')
+    quantisation amax) and the last call's per-block saturation counts.  The first step only records maxima (its
+    consumer quantises just in time)."""
+    __slots__ = ('buf', 'p', 'valid', 'numel')
 
     def __init__(self, dev):
         nb = call('dmy_bn_act_f8_blocks')
-        self.buf = torch.zeros(2, nb, dtype=torch.float32, device=dev)
-        self.p, self.valid = 0, False
+        self.buf = torch.zeros(3, nb, dtype=torch.float32, device=dev)
+        self.p, self.valid, self.numel = 0, False, 0
 
     def run(self, z, scale, shift, act, res, rps, y, yps, M, K):
         """BN-act of the producer with the e4m3 side output; returns (y8, used amax) or None on the first step"""
         y8 = torch.empty(M * K, dtype=torch.uint8, device=z.device)
         used = f32(1, z.device)
         call('dmy_bn_act_fwd_f8', ptr(z), K, ptr(scale), ptr(shift), act, ptr(res), rps, ptr(y), yps, M, K, ptr(y8),
-             ptr(self.buf[self.p]), ptr(self.buf[1 - self.p]), ptr(used), stream())
+             ptr(self.buf[self.p]), ptr(self.buf[1 - self.p]), ptr(used), F8_HEADROOM[0], ptr(self.buf[2]), stream())
         self.p ^= 1
         out = (y8, used) if self.valid else None
-        self.valid = True
+        self.valid, self.numel = True, M * K
         return out
+
+    def saturated(self):
+        """(count, fraction) of the last call's e4m3 elements clipped at +-448 (a device sync)"""
+        n = float(self.buf[2].sum()) if self.valid else 0.0
+        return n, n / max(1, self.numel)
+
+
+def f8_saturation(model):
+    """{module name: (saturated count, fraction)} of every delayed-scaling producer's last step"""
+    out = {}
+    for name, mod in model.named_modules():
+        if not isinstance(mod, torch.nn.Conv2d):
+            continue
+        ent = _PSPECS.get(id(mod.weight))
+        if ent is None or ent[0]() is not mod.weight:
+            continue
+        for sp in ent[1].values():
+            if isinstance(sp.f8_emit, F8Emit):
+                out[name] = sp.f8_emit.saturated()
+    return out
 
 
 def _fp8_weight(weight, spec, wkey, dev):

@@ -114,11 +114,13 @@ int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scale, const
 /* config-5 fp8 with delayed scaling: dmy_bn_act_fwd (bf16) that also writes the e4m3 copy y8 [M][C] (dense) of its
  * output for an e4m3 conv consumer (dmy_conv_fwd_fp8), quantised with the PREVIOUS step's amax -- the max over the
  * dmy_bn_act_f8_blocks() floats pmax that the previous call left in its nmax; used[0] receives that amax (the conv's
- * xamax) -- and leaves this step's block maxima in nmax (same size).  Replaces dmy_fp8_quant's two passes. */
+ * xamax) -- and leaves this step's block maxima in nmax (same size).  Replaces dmy_fp8_quant's two passes.
+ * headroom (>= 1) multiplies that amax (Transformer-Engine-style margin against a growing range); nsat (nullable, same
+ * size as nmax) receives per block the count of elements that saturated at +-448. */
 int dmy_bn_act_f8_blocks(void);
 int dmy_bn_act_fwd_f8(const void* z, long zps, const float* scale, const float* shift, int act, const void* res,
                       long rps, void* y, long yps, long M, int C, void* y8, const float* pmax, float* nmax, float* used,
-                      void* stream);
+                      float headroom, float* nsat, void* stream);
 int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy, long dps, const float* scale,
                       const float* shift, const float* mean, const float* invstd, int act, long M, int C, float* pdb,
                       float* pdg, void* stream);

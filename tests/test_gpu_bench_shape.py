@@ -135,6 +135,15 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     ratios = sorted(gn_err[2][i] / max(e_gn[2][i], 1e-12) for i in gn_err[2])
     med = ratios[len(ratios) // 2]
     print(f'  per-layer gradient error product / emulation: median {med:.3f}, range {ratios[0]:.3f}..{ratios[-1]:.3f}')
+    worst = sorted(gn_err[2], key=lambda i: -gn_err[2][i] / max(e_gn[2][i], 1e-12))[:4]
+    print('  worst layers (id: product err / emulation err): ' +
+          ', '.join(f'{i}: {gn_err[2][i]:.2e}/{e_gn[2][i]:.2e}' for i in worst))
+    # the parameters that carry the grad-norm-vector error: |norm(product grad) - norm(fp32 grad)|, largest first
+    pm = dict(m.named_parameters())
+    dn = sorted(((abs(float(pm[k].grad.norm()) - float(gn_b[j])), k, float(gn_b[j])) for j, k in enumerate(names)
+                 if pm[k].grad is not None), reverse=True)[:5]
+    print('  largest grad-norm differences (|product - fp32|, fp32 norm): ' +
+          ', '.join(f'{k} {d:.2e} ({b:.2e})' for d, k, b in dn))
     assert gn_err[1] <= 1.1 * max(e_gn[1], r_gn[1]) + 1e-2, (gn_err[:2], e_gn[:2], r_gn[:2])
     assert med <= 1.1, ratios
     assert gn_err[0] <= 1.5 * max(e_gn[0], r_gn[0]) + 2e-3, (gn_err[:2], e_gn[:2], r_gn[:2])

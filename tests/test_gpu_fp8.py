@@ -56,6 +56,46 @@ def test_fp8_quant_matches_torch_cast(slice_):
     assert torch.equal(x8, ref)
 
 
+@pytest.mark.parametrize('headroom', [1.0, 2.0])
+def test_bn_act_f8_delayed_amax_headroom_and_saturation(headroom):
+    """dmy_bn_act_fwd_f8 (delayed scaling): y = z * scale + shift in bf16, its e4m3 copy quantised with the PREVIOUS
+    amax (max of the pmax block maxima) x headroom -- torch's cast of the same scaled values, every byte --, this
+    call's block maxima in nmax, and per block the count of elements above that amax in nsat (the clipping
+    of a range that grew since the last step is counted, not silent)."""
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(8)
+    M, C = 5000, 64
+    z = (torch.randn(M, C, generator=g) * 2).bfloat16().cuda()
+    scale = (torch.rand(C, generator=g) + 0.5).cuda()
+    shift = (torch.randn(C, generator=g) * 0.1).cuda()
+    G = call('dmy_bn_act_f8_blocks')
+    prev = 3.0  # last step's amax: smaller than this step's range, so some elements clip
+    pmax = torch.zeros(G, device='cuda')
+    pmax[7] = prev
+    nmax, nsat = torch.full((G,), -1.0, device='cuda'), torch.full((G,), -1.0, device='cuda')
+    used = torch.empty(1, device='cuda')
+    y = torch.empty(M, C, dtype=torch.bfloat16, device='cuda')
+    y8 = torch.empty(M * C, dtype=torch.uint8, device='cuda')
+    call('dmy_bn_act_fwd_f8', ptr(z), C, ptr(scale), ptr(shift), 0, None, 0, ptr(y), C, M, C, ptr(y8),
+         ptr(pmax), ptr(nmax), ptr(used), headroom, ptr(nsat), stream())
+    torch.cuda.synchronize()
+    yr = (z.float() * scale + shift).bfloat16()
+    assert torch.equal(y, yr)
+    a = prev * headroom
+    assert float(used) == a
+    yf = yr.float()
+    ref = _e4m3(yf * (torch.tensor(448.0, device='cuda') / torch.tensor(a, device='cuda'))).reshape(-1)
+    assert torch.equal(y8, ref)
+    assert float(nmax.max()) == float(yf.abs().max()) and float(nmax.min()) >= 0
+    nclip = int((yf.abs() > a).sum())
+    assert nclip > 0 if headroom == 1.0 else True
+    assert float(nsat.sum()) == nclip and float(nsat.min()) >= 0
+    # a sub-1 headroom is refused
+    with pytest.raises(RuntimeError):
+        call('dmy_bn_act_fwd_f8', ptr(z), C, ptr(scale), ptr(shift), 0, None, 0, ptr(y), C, M, C, ptr(y8),
+             ptr(pmax), ptr(nmax), ptr(used), 0.5, None, stream())
+
+
 def test_fp8_wprep_matches_torch_cast():
     from dmayolo.functional import call, ptr, stream
     g = torch.Generator().manual_seed(4)
@@ -209,13 +249,16 @@ def test_fp8_delayed_scaling_equals_jit_on_repeated_batch():
                     out = m(x)
                 finally:
                     Fn.call = orig
-        return [o.float() for o in out], counts
+        return [o.float() for o in out], counts, Fn.f8_saturation(m)
 
     try:
-        jit, cj = run(False)
-        dly, cd = run(True)
+        jit, cj, _ = run(False)
+        dly, cd, sat = run(True)
     finally:
         Fn.F8_DELAYED[0] = True
+    # the same batch again: no element exceeds the previous step's amax, so nothing saturated
+    print('saturation', sat)
+    assert len(sat) >= 8 and all(n == 0 for n, _ in sat.values())
     print('jit', {k: v for k, v in cj.items() if 'f8' in k or 'fp8' in k}, 'delayed',
           {k: v for k, v in cd.items() if 'f8' in k or 'fp8' in k})
     assert cd.get('dmy_bn_act_fwd_f8', 0) >= 8

@@ -20,6 +20,11 @@ fi
 if [ -n "$MICRO" ]; then
   TUNE_COLD=1 timeout -k 10 300 python -u tools/gpu/tune_conv.py $MICRO ${MICROKINDS:-fwd,fwdnb,dgrad} > gpurun_out/r4/micro_${TAG}.log 2>&1
   echo "micro rc=$?"
+  if [ -n "$MICROAB" ]; then  # the same launches with one library knob changed, e.g. MICROAB=DMY_WGRAD_W=0
+    env $MICROAB TUNE_COLD=1 timeout -k 10 300 python -u tools/gpu/tune_conv.py $MICRO ${MICROKINDS:-fwd,fwdnb,dgrad} \
+        > gpurun_out/r4/micro_${TAG}_ab.log 2>&1
+    echo "micro ab rc=$?"
+  fi
 fi
 if [ -n "$BENCH" ]; then
   timeout -k 10 600 python bench.py $BENCH > gpurun_out/r4/bench_$TAG.json 2> gpurun_out/r4/bench_$TAG.err
