@@ -11,6 +11,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libdmayolo_hip.so')
+if os.environ.get('DMY_LIB_AB'):  # kernel A/B tooling only: another in-tree build of the same C ABI, by file name
+    LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ['DMY_LIB_AB']))
 
 P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_double
 

@@ -348,10 +348,11 @@ def f8_saturation(model):
     for name, mod in model.named_modules():
         if not isinstance(mod, torch.nn.Conv2d):
             continue
+        sps = [_SPECS[mod]] if mod in _SPECS else []  # module-held specs (common.conv_forward)
         ent = _PSPECS.get(id(mod.weight))
-        if ent is None or ent[0]() is not mod.weight:
-            continue
-        for sp in ent[1].values():
+        if ent is not None and ent[0]() is mod.weight:
+            sps += list(ent[1].values())
+        for sp in sps:
             if isinstance(sp.f8_emit, F8Emit):
                 out[name] = sp.f8_emit.saturated()
     return out

@@ -141,3 +141,47 @@ def test_conv_kernels_at_bench_shapes(cfg, shape):
     bad = [(kd, e, n) for kd, (e, n) in r.items() if e > BOUNDS[kd][0] or abs(n) > BOUNDS[kd][1]]
     torch.cuda.empty_cache()
     assert not bad, bad
+
+
+def test_halo_bn_statistics_large_mean_at_bench_shape():
+    """the persistent halo kernel (3x3 s1 64 -> 64, DMA-YOLO-l's 768^2 bs32 layer: ~288 tiles per block)
+    sums each lane's BN sum / sum of squares over every tile of its block; with mean >> std, var = E[z^2] - E[z]^2
+    amplifies a running-sum error by (mean / std)^2.  Inputs 1 + 0.05 n and positive weights give mean / std ~ 470
+    (amplification ~2e5); the batch mean and variance from the kernel's partial rows (summed in float64, as
+    dmy_bn_finalize does) against float64 statistics of an fp32 reference convolution: mean within 1e-6, variance
+    within 2e-3 relative."""
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    torch.backends.cuda.matmul.allow_tf32 = False
+    N, C, H, W, K = 32, 64, 768, 768, 64
+    dev = 'cuda'
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = (1 + 0.05 * torch.randn(N, C, H, W, generator=g, device=dev)).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    w = (1 + 0.2 * torch.randn(K, C, 3, 3, generator=g, device=dev)) / (C * 9)
+    wf, _ = prep_weight(w, torch.bfloat16, False)
+    y = torch.empty(N, K, H, W, dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    P = call('dmy_conv_fwd_bn_rows', 1, ptr(x), ptr(wf), None, ptr(y), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K)
+    ps = torch.full((P, K), float('nan'), device=dev)
+    pq = torch.full((P, K), float('nan'), device=dev)
+    call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K,
+         stream())
+    M = N * H * W
+    mean_p = ps.double().sum(0) / M
+    var_p = pq.double().sum(0) / M - mean_p ** 2
+    del ps, pq, y
+    wb = w.bfloat16().float().reshape(K, C * 9)
+    s1 = torch.zeros(K, device=dev, dtype=torch.float64)
+    s2 = torch.zeros(K, device=dev, dtype=torch.float64)
+    for b in range(N):
+        z = torch.matmul(wb, F.unfold(x[b:b + 1].float(), 3, padding=1)[0]).double()  # [K, H W]
+        s1 += z.sum(1)
+        s2 += (z * z).sum(1)
+        del z
+    mean_r = s1 / M
+    var_r = s2 / M - mean_r ** 2
+    em = float(((mean_p - mean_r).abs() / mean_r.abs()).max())
+    ev = float(((var_p - var_r).abs() / var_r).max())
+    ratio = float((mean_r / var_r.sqrt()).mean())
+    print(f'halo BN statistics at {N}x{C}x{H}x{W}: P {P} rows, mean / std {ratio:.0f}, max rel err mean {em:.2e} '
+          f'var {ev:.2e}')
+    assert P >= 64 and em < 1e-6 and ev < 2e-3, (em, ev)

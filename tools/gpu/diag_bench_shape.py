@@ -44,3 +44,13 @@ for r in rows[:25]:
 print('worst cos among params with >0.1% of the squared norm:')
 for r in sorted([r for r in rows if r[0] ** 2 / tot > 1e-3], key=lambda r: r[2])[:15]:
     print('%.4f %-40s cos %.4f rel %.3e ratio %.4f' % (r[0] ** 2 / tot, r[1], r[2], r[3], r[4] / (r[0] + 1e-300)))
+lids = sorted({int(k.split('.')[1]) for k in pq if pq[k].grad is not None})
+
+
+def lnorm(pg, lid):
+    return float(torch.cat([pg[k].grad.double().flatten().cpu() for k in pq
+                            if pq[k].grad is not None and int(k.split('.')[1]) == lid]).norm())
+
+
+print('per-layer gradient norm product / fp32 oracle: ' + ' '.join(f'{lid}:{lnorm(pp, lid) / lnorm(pq, lid):.3f}'
+                                                                for lid in lids))
