@@ -19,7 +19,9 @@ if [ -z "$NOGLOO" ]; then
       > $OUT/bench_gloo2_$TAG.json 2> $OUT/bench_gloo2_$TAG.err
   rc=$?; echo "gloo2 rc=$rc"; tail -c 400 $OUT/bench_gloo2_$TAG.json; [ $rc -ne 0 ] && { tail -5 $OUT/bench_gloo2_$TAG.err; exit $rc; }
 fi
-if [ -n "$C5" ]; then
+if [ -n "$C5" ]; then  # config 5 @1920 bs8, bf16 then the fp8 forward (delayed scaling)
+  timeout -k 10 600 python bench.py --config c5-1920 --also none --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_c5_bf16_$TAG.json 2> $OUT/bench_c5_bf16_$TAG.err
+  rc=$?; echo "c5 bf16 rc=$rc"; tail -c 400 $OUT/bench_c5_bf16_$TAG.json; [ $rc -ne 0 ] && exit $rc
   timeout -k 10 600 python bench.py --config c5-1920 --also none --fp8 --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_c5_fp8_$TAG.json 2> $OUT/bench_c5_fp8_$TAG.err
   rc=$?; echo "c5 fp8 rc=$rc"; tail -c 400 $OUT/bench_c5_fp8_$TAG.json
 fi
