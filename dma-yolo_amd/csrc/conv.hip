@@ -1895,7 +1895,7 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                 long M, int NC, int ng, long xps, long yps, unsigned xbytes,
-                                                int ntiles, int kwrow, int H, int W, Epi ep) {
+                                                int ntiles, int kwrow, int H, int W, Epi ep, int pf) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
   constexpr int NG2 = KD <= 128 ? 2 : 1, CP = 32 * NG2;  // 32-channel groups per column pass (registers: KD 160 / 256 keep 1)
@@ -1921,9 +1921,13 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
   const int q = lane >> 4, pl = lane & 15;
   // this lane's 16-B output chunk of a 32-channel pair of 16-channel tiles (after the permlane16 swap)
   const int chq = (q & 1) * 16 + (q >> 1) * 8;
-  for (int t = blockIdx.x * NW + wid; t < ntiles; t += gridDim.x * NW) {
-    const long p0 = (long)t * 64;
-    bf16x8 xf[4][KC];
+  // PF: the next tile's X fragments are loaded while this tile's column passes run (training variants, KD <= 128: 64
+  // more VGPRs; DMY_P1S_PF = 0 turns it off at run time)
+  constexpr bool PF = !G3 && !EPI && KD <= 128;
+  const int tstride = gridDim.x * NW;
+  bf16x8 xf[4][KC];
+  auto load_x = [&](bf16x8 (&dst)[4][KC], int tt) {
+    const long p0 = (long)tt * 64;
 #pragma unroll
     for (int pb = 0; pb < 4; ++pb) {
       const long m = p0 + pb * 16 + pl;
@@ -1935,7 +1939,7 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
           const bool ok = m < M && tap < 9 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
           const unsigned off = ok ? (unsigned)(((bi * H + ih) * W + iw) * (int)xps + 8 * (q & 1)) * 2u : kBufOob;
           const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-          xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+          dst[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
         }
       } else {
         const unsigned base = m < M ? (unsigned)(m * xps + q * 8) * 2u : kBufOob;
@@ -1943,9 +1947,20 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
         for (int kc = 0; kc < KC; ++kc) {
           const unsigned off = base == kBufOob ? kBufOob : base + kc * 64u;
           const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-          xf[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
+          dst[pb][kc] = *reinterpret_cast<const bf16x8*>(&v);
         }
       }
+    }
+  };
+  const int t0 = blockIdx.x * NW + wid;
+  if (PF && pf && t0 < ntiles) load_x(xf, t0);
+  for (int t = t0; t < ntiles; t += tstride) {
+    const long p0 = (long)t * 64;
+    bf16x8 xn[4][KC];
+    if (PF && pf) {
+      if (t + tstride < ntiles) load_x(xn, t + tstride);
+    } else {
+      load_x(xf, t);
     }
     // column passes of NG2 groups of 32 channels (CP = 32 * NG2 columns): the two 64-B halves of each 128-B output line
     // (64 channels of one pixel) leave in back-to-back stores.  Stored 32 channels per pass instead, a line's second
@@ -2053,6 +2068,12 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
           }
         }
       }
+    }
+    if (PF && pf) {
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) xf[pb][kc] = xn[pb][kc];
     }
   }
 }
@@ -3642,6 +3663,8 @@ inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+// DMY_P1S = 0 off, 1 (default) the output-heavy forwards (K >= 2 C), 3 those and the output-heavy data-grads, 2 every
+// eligible GEMM view (A/B)
 inline int p1s_mode() {
   static int t = env_int("DMY_P1S", 1);
   return t;
@@ -3688,8 +3711,9 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   if (nbx > maxb) nbx = maxb;
   const dim3 grid((unsigned)nbx, (unsigned)G);
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps);
+  static const int pf = env_int("DMY_P1S_PF", 1);
   v3::conv_p1s<KD, NTH, G3, EPI><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
-                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W, ep);
+                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W, ep, pf);
   return (int)hipGetLastError();
 }
 inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
@@ -3862,7 +3886,8 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   // eval epilogue on the streaming kernels (forward, no accumulate): the residual read as 16-B vectors
   const bool ep_ok = !ep.on || (!DG && !acc && p1s_eval() && (ep.res == nullptr || (ep.rps % 8 == 0 && aligned16(ep.res))));
-  if (ep_ok && bb.z == nullptr && p1s_ok(gv, x, w, y) && (p1s_mode() == 2 || (!DG && gv.K >= 2 * gv.C)))
+  if (ep_ok && bb.z == nullptr && p1s_ok(gv, x, w, y) &&
+      (p1s_mode() == 2 || ((!DG || p1s_mode() == 3) && gv.K >= 2 * gv.C)))
     return launch_p1s(x, w, b, y, ps, pq, acc, gv, st, ep);
   if (!DG && ep_ok && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
     return ep.on ? launch_p1s_kd<160, 768, true, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
@@ -4174,7 +4199,8 @@ inline long dgrad_bn_rows(const Geom& g, const void* dy, const void* wt, const v
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   const bool buf = conv_buf_mode() && g.K % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
   if (p1 && buf && p1_persist_mode()) return 0;
-  if (p1 && p1s_mode() == 2 && p1s_ok(make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, 1, 1, 1, 0, g.H, g.W, g.xps), dy, wt, dx))
+  if (p1 && (p1s_mode() == 2 || (p1s_mode() == 3 && g.C >= 2 * g.K)) &&
+      p1s_ok(make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, 1, 1, 1, 0, g.H, g.W, g.xps), dy, wt, dx))
     return 0;
   if (p1 && p1_tile_mode() != 0) return 0;  // 128-row / 64-column tiles
   if (buf && tall_mode() && !p1 && g.C <= 128 && (long)ceil_div(M, 512) * ceil_div(g.C, 128) >= 4L * num_cus())
