@@ -222,16 +222,20 @@ def test_bench_shape_fp32_product_vs_oracle():
     assert all(abs(v - 1) < 1e-3 for v in lr.values()), lr
 
 
-def test_bench_shape_layers_bf16_vs_emulation():
-    """Every top-level layer of DMA-YOLO-l alone at the bench shape (1536, bs 2) on the inputs the fp32 oracle sees
-    there (tests/module_parity.py): the bf16 product module and the bf16-storage emulation of the oracle module against
-    the fp32 oracle module, for one seeded upstream gradient.  Bounds per layer (round 4 measured: product / emulation
-    input-gradient error 1.0-1.6x, parameter-gradient error 0.97-1.26x, norms within 2e-4 of fp32 for both):
-    input and parameter gradient relative L2 <= 1.75 x the emulation's + 5e-4, norm ratios within 1e-3 of 1."""
+@pytest.mark.parametrize('yml,img,bs', [('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 1536, 2),
+                                        ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2)])
+def test_bench_shape_layers_bf16_vs_emulation(yml, img, bs):
+    """Every top-level layer of a bench model alone at its bench resolution on the inputs the fp32 oracle sees there
+    (tests/module_parity.py): the bf16 product module and the bf16-storage emulation of the oracle module against the
+    fp32 oracle module, for one seeded upstream gradient.  DMA-YOLO-l @1536 (config 3) and config 5 @1920 -- there
+    C3TR's global attention runs over 60 x 60 = 3,600 tokens per image, as in the bench.  Bounds per layer (round 4
+    measured on DMA-YOLO-l: product / emulation input-gradient error 1.0-1.6x, parameter-gradient error 0.97-1.26x,
+    norms within 2e-4 of fp32 for both): input and parameter gradient relative L2 <= 1.75 x the emulation's + 5e-4,
+    norm ratios within 1e-3 of 1."""
     from module_parity import layer_parity, fmt
     bad = []
     n = 0
-    for i, name, row in layer_parity('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 1536, 2):
+    for i, name, row in layer_parity(yml, img, bs):
         print(fmt(i, name, row), flush=True)
         n += 1
         if isinstance(row, Exception):
@@ -245,4 +249,4 @@ def test_bench_shape_layers_bf16_vs_emulation():
         for kd in ('dxn', 'wn'):
             if kd in row and abs(row[kd][0] - 1) > 1e-3:
                 bad.append((i, name, kd, row[kd]))
-    assert n >= 20 and not bad, bad
+    assert n >= 15 and not bad, bad
