@@ -41,7 +41,10 @@ def run_layer(res, xs, xin, g, pm, om, em):
             C = y.shape[1]
             res['gup'] = torch.randn(y.shape, generator=g, device='cuda') + \
                 torch.linspace(-0.5, 0.5, C, device='cuda').view(1, -1, 1, 1)
-        (y.float() * res['gup']).sum().backward()
+        # the product's output is bf16, so autograd hands it the upstream gradient rounded to bf16: the emulation gets
+        # the same rounded gradient, the fp32 oracle the exact one
+        gup = res['gup'].bfloat16().float() if kind == 'emu' else res['gup']
+        (y.float() * gup).sum().backward()
         res[kind] = (torch.cat([x.grad.float().flatten() for x in xi]),
                      {k: p.grad.detach().float().flatten() for k, p in mod.named_parameters() if p.grad is not None})
 

@@ -10,7 +10,7 @@ run again with the roundings a reduced-precision run performs, and the product i
                    and data-gradient (the kernels read bf16 OHWI / IHWO copies of the fp32 master weights; the weight
                    gradient itself stays fp32) + the outputs of the composite modules whose result the product stores
                    in bf16 (Bottleneck / Swin residual sums, CoorAttention's x * a_w * a_h, the AdConcat weighted
-                   copies, SCConv's gate product);
+                   copies, SCConv's gate product, CBAM's ca, ca * x, pooled map, spatial gate and output);
   mode 'bf16_sink' 'bf16' + each leaf's INPUT gradient rounded to bf16 as it leaves the leaf: the product's data-grad
                    kernels store every contribution to an input gradient in bf16 and accumulate the next one into that
                    bf16 buffer (functional.GradSink; autograd's own sums of bf16 gradients), where 'bf16' sums the
@@ -33,7 +33,7 @@ DTYPES = {'bf16_act': torch.bfloat16, 'bf16': torch.bfloat16, 'bf16_sink': torch
 LOSS_SCALE = {'bf16_act': 1.0, 'bf16': 1.0, 'bf16_sink': 1.0, 'fp16': 2.0 ** 16, 'fp8': 1.0}
 
 LEAVES = (nn.Conv2d, nn.BatchNorm2d, nn.SiLU, nn.Upsample, nn.MaxPool2d, nn.Linear, nn.LayerNorm, nn.GELU, nn.Hardswish,
-          nn.Sigmoid, nn.AvgPool2d, nn.AdaptiveAvgPool2d, nn.ReLU)
+          nn.Sigmoid, nn.AvgPool2d, nn.AdaptiveAvgPool2d, nn.AdaptiveMaxPool2d, nn.ReLU)
 
 
 class RoundAct(torch.autograd.Function):
@@ -141,6 +141,17 @@ def emulate(model, mode):
         elif type(mod) is nn.Linear:
             mod.forward = (lambda m: lambda x: F.linear(x, RoundWeight.apply(m.weight, dt), m.bias))(mod)
     from oracle import nn as onn
+    if hasattr(onn, 'CBAM'):
+        for mod in model.modules():
+            if isinstance(mod, onn.ChannelAttentionModule):
+                mod.register_forward_hook(hook)  # ca, the sigmoid of the summed MLP branches, is stored
+            if isinstance(mod, onn.CBAM):
+                def cbam_fwd(x, m=mod):  # the product stores out1 = ca * x, the pooled map, sa and the output
+                    out1 = RoundAct.apply(m.channel_attention(x) * x, dt)
+                    s2 = RoundAct.apply(torch.cat([out1.mean(1, keepdim=True), out1.max(1, keepdim=True)[0]], 1), dt)
+                    sa = RoundAct.apply(torch.sigmoid(m.spatial_attention.conv2d(s2)), dt)
+                    return RoundAct.apply(sa * out1, dt)
+                mod.forward = cbam_fwd
     if hasattr(onn, 'SCConv'):
         for mod in model.modules():
             if isinstance(mod, onn.SCConv):
