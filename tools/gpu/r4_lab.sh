@@ -12,7 +12,7 @@ if [ -n "$LAB" ]; then
   rc=$?; echo "lab rc=$rc"; cat gpurun_out/r4/${LAB}_$TAG.log; [ $rc -ne 0 ] && exit $rc
 fi
 if [ -n "$T" ]; then
-  timeout -k 10 1000 python -u -m pytest $T -v -s -p no:cacheprovider --timeout 600 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest $T ${TK:+-k "$TK"} -v -s -p no:cacheprovider --timeout 600 --timeout-method thread \
       > gpurun_out/r4/tests_$TAG.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r4/tests_$TAG.log | tail -2; grep -E "^FAILED|^ERROR" gpurun_out/r4/tests_$TAG.log | head -20
   [ $rc -ge 2 ] && exit $rc
