@@ -1898,7 +1898,10 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
                                                 int ntiles, int kwrow, int H, int W, Epi ep, int pf) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
-  constexpr int NG2 = KD <= 128 ? 2 : 1, CP = 32 * NG2;  // 32-channel groups per column pass (registers: KD 160 / 256 keep 1)
+  // 32-channel groups per column pass: 2 (64-column passes, whole 128-B output lines per pixel) up to 512 threads, 1 at
+  // 768 / 1024 threads (3-4 waves per SIMD: no room for the second group's accumulators) and in the KD 256 eval variant
+  // (its epilogue registers)
+  constexpr int NG2 = NTH <= 512 && !(EPI && KD > 128) ? 2 : 1, CP = 32 * NG2;
   bf16* ws = reinterpret_cast<bf16*>(p1s_smem);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* red = reinterpret_cast<float*>(p1s_smem + ng * PITCH * 2) + wid * 64;  // this wave's [2][32] partials
@@ -3681,6 +3684,14 @@ inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) 
     return false;
   return 2.0 * ((double)gv.N * gv.OH * gv.OW * gv.xps) < (double)v3::kBufOob;
 }
+// threads per block of the training stem (DMY_P1S_STEM_NTH): 512 = 64-column passes that write whole 128-B output lines
+// per pixel, 768 = round 2's 32-column passes; 0 (default) = 512 for >= 64 output channels, else 768.  Cold-cache
+// (profiles/r04/stem_ab.log): DMA-1536 stem (64 ch @768^2 bs32) 1483 -> 1185 us, config 5 (64 @960^2 bs8) 585 -> 434 us,
+// but yolov5s (32 ch @320^2 bs64: one 32-column pass either way) 213 -> 242 us with 512, so it keeps 768
+inline int stem_nth(int K) {
+  static const int t = env_int("DMY_P1S_STEM_NTH", 0);
+  return t ? t : (K >= 64 ? 512 : 768);
+}
 // the k3 s1 p1 view of the space-to-depth stem (16 input channels): DMY_P1S_STEM = 0 keeps the LDS-DMA tile
 inline bool stem_s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
   static const int on = env_int("DMY_P1S_STEM", 1);
@@ -3891,7 +3902,8 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
     return launch_p1s(x, w, b, y, ps, pq, acc, gv, st, ep);
   if (!DG && ep_ok && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
     return ep.on ? launch_p1s_kd<160, 768, true, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
-                 : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep);
+           : stem_nth(gv.K) == 512 ? launch_p1s_kd<160, 512, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
+                               : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep);
   // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
   const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
