@@ -4499,7 +4499,10 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     if (vec && (g.K > 64 || nm == 2) && Ntot >= 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && nm == 1) {
-      const bool wide = Ntot >= 512 || Ntot % 256 == 0;
+      // one 256-column tile also for 128 < Ntot < 256 (the 144-column space-to-depth stem view: on 128-column tiles
+      // the second tile re-read every dy row for 16 columns of work): DMY_WGRAD_ONE_TILE = 0 keeps two tiles
+      static const int one = env_int("DMY_WGRAD_ONE_TILE", 1);
+      const bool wide = Ntot >= 512 || Ntot % 256 == 0 || (one && Ntot > 128 && Ntot < 256);
       if (g.K <= 32) return wide ? launch_wgrad_v3n<32, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
                                  : launch_wgrad_v3n<32, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
       return wide ? launch_wgrad_v3n<64, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
