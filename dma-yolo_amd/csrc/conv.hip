@@ -3672,9 +3672,12 @@ inline int p1s_mode() {
   static int t = env_int("DMY_P1S", 1);
   return t;
 }
-// eval forwards (inference epilogue: eval BN + act + residual in the store loop) on conv_p1s too: DMY_P1S_EP = 1 (default)
+// eval forwards (inference epilogue: eval BN + act + residual in the store loop) on conv_p1s too: DMY_P1S_EP = 1 on,
+// 0 (default) off.  Measured SLOWER on the graph-replayed batch-1 detect (profiles/r04/det_p1s_ep_ab.log, two passes on
+// one box: DMA-1536 p50 4.662 / 4.653 ms on vs 4.524 / 4.515 off; yolov5s@640 0.777 / 0.776 vs 0.768 / 0.785): at
+// batch 1 a 64-pixel wave tile per 8-wave block leaves most CUs idle, where the v2 / LDS-DMA tiles spread the layer
 inline int p1s_eval() {
-  static int t = env_int("DMY_P1S_EP", 1);
+  static int t = env_int("DMY_P1S_EP", 0);
   return t;
 }
 inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) {

@@ -172,8 +172,8 @@ def test_conv_fwd_1x1_small_m_unsplit():
 FILL_SHAPES = [(1, 256, 96, 96, 256, 1, 1), (1, 128, 192, 192, 128, 1, 1), (1, 128, 190, 186, 128, 3, 1),
                (1, 512, 48, 48, 512, 1, 1), (1, 1024, 37, 41, 200, 1, 1), (2, 64, 45, 47, 136, 1, 1),
                (1, 256, 96, 96, 1024, 1, 1), (3, 128, 65, 67, 512, 3, 2),
-               # output-heavy 1x1 eval forwards on the streaming GEMM's epilogue (conv_p1s<.., EPI>, M >= 16384,
-               # K >= 2C): 64-column passes, a 32-column tail pass, the residual read as 16-B vectors
+               # output-heavy 1x1 eval forwards (M >= 16384, K >= 2C; on the streaming GEMM's epilogue,
+               # conv_p1s<.., EPI>, under DMY_P1S_EP=1): 64-column passes, a 32-column tail pass, a 16-B residual
                (1, 128, 192, 192, 512, 1, 1), (2, 64, 130, 126, 128, 1, 1), (1, 256, 128, 130, 544, 1, 1)]
 
 
