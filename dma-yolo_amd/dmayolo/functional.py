@@ -45,6 +45,22 @@ def f32(n, dev):
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
+_CONST = {}
+
+
+def const_vec(n, value, dev):
+    """a cached fp32 vector of n copies of value on dev, for kernel arguments that are only read (the unit scale /
+    zero shift of the activation-only passes): one fill per (n, value, device) instead of two per layer and step"""
+    key = (int(n), float(value), str(dev))
+    t = _CONST.get(key)
+    if t is None:
+        t = torch.full((int(n),), float(value), dtype=torch.float32, device=dev)
+        # a fill recorded into a HIP graph only runs at replay: cache only what an eager fill has written
+        if not torch.cuda.is_current_stream_capturing():
+            _CONST[key] = t
+    return t
+
+
 # Output-into-slice side channel of conv_bn_act (see concat_buffer): the view is consumed by the ConvBNActFn.apply
 # that conv_bn_act issues right after setting it, and only when its shape / dtype / device match the output.
 _OUT = [None]
@@ -694,7 +710,7 @@ class ConvBNActFn(torch.autograd.Function):
             _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             if spec.act != ACT_NONE or res is not None:
                 y = out if out is not None else new_act(N, K, OH, OW, x)
-                one, zero = torch.ones(K, device=dev), torch.zeros(K, device=dev)
+                one, zero = const_vec(K, 1.0, dev), const_vec(K, 0.0, dev)
                 call('dmy_bn_act_fwd', dcode(x), ptr(z), K, ptr(one), ptr(zero), spec.act, ptr(res), rps, ptr(y), yps,
                      M, K, stream())
             else:
@@ -769,8 +785,7 @@ class ConvBNActFn(torch.autograd.Function):
             x, wt, z = ctx.saved_tensors
             if spec.act != ACT_NONE:
                 dz = new_act(N, K, OH, OW, z)
-                zero = torch.zeros(K, device=dev)
-                one = torch.ones(K, device=dev)
+                zero, one = const_vec(K, 0.0, dev), const_vec(K, 1.0, dev)
                 call('dmy_bn_bwd_apply', dt, ptr(z), K, ptr(dy), dps, ptr(one), ptr(zero), ptr(zero), ptr(one),
                      spec.act, ptr(one), ptr(zero), ptr(zero), ptr(dz), K, M, K, stream())
                 dzps = K
