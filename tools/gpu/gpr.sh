@@ -4,6 +4,8 @@
 OUT=$1; shift; TO=$1; shift
 for i in $(seq 1 12); do
   timeout 2700 /usr/local/graft/bin/gpurun --timeout $TO -- "$@" > $OUT 2>&1
-  if grep -q "status=transient" $OUT && grep -q "nothing was charged\|no free box\|backing off" $OUT; then sleep 150; continue; fi
+  if grep -q "backing off" $OUT || { grep -q "status=transient" $OUT && grep -q "nothing was charged\|no free box" $OUT; }; then
+    sleep 150; continue
+  fi
   break
 done
