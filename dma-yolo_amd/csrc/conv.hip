@@ -1522,7 +1522,7 @@ template <int BM, int BN, int NS, int WTR, bool DG, bool LANE = false>
 __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
     const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias, bf16* __restrict__ y,
     float* __restrict__ psum, float* __restrict__ psq, int /*accumulate: 0*/, Geom g, int gm, int gn, unsigned xbytes,
-    unsigned wbytes, unsigned ybytes, int nprow, Epi ep, unsigned rbytes) {
+    unsigned wbytes, unsigned ybytes, int nprow, Epi ep, unsigned rbytes, int ff) {
   using PP = P1P<BM, BN, NS, WTR>;
   using C3_ = typename PP::C3_;
   constexpr int PER = PP::PER, NI = PP::NI;
@@ -1617,7 +1617,7 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         vm_wait<0>();  // other epilogue shapes (accumulate, 32-pixel partial rows): wait for everything
       }
       __builtin_amdgcn_s_barrier();
-      if (s + NS - 1 < total) issue(s + NS - 1);
+      if (!ff && s + NS - 1 < total) issue(s + NS - 1);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
       const bf16* Bs = As + BM * BK;
 #pragma unroll
@@ -1627,6 +1627,11 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
 #pragma unroll
         for (int i = 0; i < NI; ++i) a[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
+        if (ff && h == 0) {  // fragments first (DMY_P1P_FF): the next stage's LDS-DMA after this half-step's reads
+          __builtin_amdgcn_sched_barrier(0);
+          if (s + NS - 1 < total) issue(s + NS - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -1818,7 +1823,11 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_dgrad_s2_v3(const bf16* __r
 // Per K step a wave reads (128 + 64) x 64 bf16 from LDS for 64 MFMAs, against (64 + 64) x 64 for 32 in the
 // 64 x 64 wave tile: the LDS array (256 B/clk/CU) stops pacing the MFMAs on the MFMA-bound layers.  2 LDS stages
 // of 64 KiB (loads of step k + 1 in flight during step k), 8 waves (2 x 4), 128 accumulator registers per lane.
-template <int BM, int BN, int NS, class LD>
+// FF (fragments first): the first half-step's 12 fragment reads are issued before the next stage's LDS-DMA, so
+// the reads the MFMAs wait on are not queued behind the DMA's LDS writes.  DMY_WIDE_FF = 1 (default), 0 = DMA first.
+// Measured (round 4, profiles/r04/wide_ff_ab.log, cold caches): 3x3 256 @96^2 fwd 430 -> 418 us, 512 @96^2 fwd 1201 ->
+// 1171, dgrad 1156 -> 1114, 1024 @48^2 fwd 1254 -> 1211; DMA-1536 step 153.8 / 153.6 -> 154.8 / 154.4 img/s
+template <int BM, int BN, int NS, bool FF, class LD>
 DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int lane) {
   using C3_ = Cfg3<BM, BN, NS, 128>;
   constexpr int PER = C3_::APW + C3_::BPW;
@@ -1829,7 +1838,7 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
     if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    if (!FF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
     const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
     const bf16* Bs = As + BM * BK;
 #pragma unroll
@@ -1839,6 +1848,11 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
       for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = frag_sw(As, wm * 128 + i * 16, h * 32, lane);
+      if (FF && h == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1853,7 +1867,7 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep,
-                                                  BnB bb) {
+                                                  BnB bb, int ff) {
   constexpr int NS = 2;
   static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
   using C3_ = Cfg3<BM, BN, NS, 128>;
@@ -1871,7 +1885,8 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
   FwdLdsB<BM, BN, NS, P1, DG, false, 2, 128> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
-  mainloop_w<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  if (ff) mainloop_w<BM, BN, NS, true>(ld, nk, smem, acc, wid, lane);
+  else mainloop_w<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
                                       n0, S2Cls{0, 0, 0, 0}, ep, bb);
@@ -3831,6 +3846,7 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
   const long M = (long)gv.N * gv.OH * gv.OW;
   const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
   const double rb = ep.res != nullptr ? 2.0 * ((double)(M - 1) * ep.rps + gv.K) : 0.0;
+  static const int ff = env_int("DMY_P1P_FF", 0);  // fragments first in conv_p1p's K loop (A/B)
   return p1p_plan<DG>(gv, acc, ep, small, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, NS = decltype(ns)::value, WTR = decltype(wtr)::value;
     using PP = v3::P1P<BM, BN, NS, WTR>;
@@ -3839,13 +3855,13 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
     if constexpr (!DG) {
       if (ps != nullptr && !small && gn == 1 && p1p_lane_mode()) {  // one BN partial row per wave (dmy_conv_fwd_bn_rows)
         v3::conv_p1p<BM, BN, NS, WTR, false, true><<<(unsigned)G, PP::NTH, 0, st>>>(
-            x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb);
+            x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb, ff);
         return (int)hipGetLastError();
       }
     }
     const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
     v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
-                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb);
+                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb, ff);
     return (int)hipGetLastError();
   });
 }
@@ -3948,11 +3964,12 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   }
 #define W_GO(BM, BN)                                                                                               \
   {                                                                                                                \
+    static const int ff = env_int("DMY_WIDE_FF", 1);                                                               \
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
     if (p1) v3::conv_fwd_w<BM, BN, true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, \
-                                                                              xbytes, wbytes, ep, bb);            \
+                                                                              xbytes, wbytes, ep, bb, ff);        \
     else v3::conv_fwd_w<BM, BN, false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn,   \
-                                                                               xbytes, wbytes, ep, bb);           \
+                                                                               xbytes, wbytes, ep, bb, ff);       \
     return (int)hipGetLastError();                                                                                 \
   }
   if (tov < 0 && buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
