@@ -3183,7 +3183,8 @@ DEV bf16x8 frag_halo(const bf16* Bs, int kh, int kw, int ch0, int k0, int lane) 
 template <int BM>
 __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                          float* __restrict__ dw, int kt_per_split, Geom g, int gm,
-                                                         int gn, int nk_all, unsigned xbytes, unsigned dybytes) {
+                                                         int gn, int nk_all, unsigned xbytes, unsigned dybytes,
+                                                         int ff) {
   using LD = WgradTapLds<BM>;
   constexpr int NS = 3, STAGE = LD::STAGE, TM = BM / 32;  // 4 waves = 2 (m) x 2 (n); wave tile BM/2 x 144
   constexpr int CTR = BM / 2, CTS = 288 + 4;               // epilogue: half the tile staged at a time
@@ -3210,7 +3211,7 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
       if (kt + 1 < nk) vm_wait<LD::APW + 2>();
       else vm_wait<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      if (!ff && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
       const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
 #pragma unroll
@@ -3218,6 +3219,11 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
         bf16x8 a[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) a[i] = frag_k<BM>(As, wm * (BM / 2) + i * 16, h * 32, lane);
+        if (ff && h == 0) {  // fragments first (DMY_TAP_FF): the next stage's DMA after the first A reads
+          __builtin_amdgcn_sched_barrier(0);
+          if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
           const int f = wn * 9 + j, tap = f >> 1;
@@ -3305,7 +3311,7 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
                                                         bf16* __restrict__ y, float* __restrict__ psum,
                                                         float* __restrict__ psq, Geom g, int twn, int thn, int ntiles,
                                                         int per, unsigned xbytes, unsigned wbytes, unsigned ybytes,
-                                                        int accumulate, Epi ep, unsigned rbytes) {
+                                                        int accumulate, Epi ep, unsigned rbytes, int ff) {
   // the eval instantiation keeps the 64 channels' scale / shift after the ring (512 B, written before the first barrier)
   __shared__ __attribute__((aligned(1024))) char smem[halo::LDS + (EP ? 512 : 0)];
   if (EP && threadIdx.x < 128) {
@@ -3374,7 +3380,7 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
   for (int u = u0, it = 0; u < u1; ++u, ++it) {
     __builtin_amdgcn_s_barrier();  // halo(u) landed for every wave; every wave is done with the other buffer
     const char* const hl = smem + halo::WBYTES + (it & 1) * halo::HBYTES;
-    if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
+    if (!ff && u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
     int b, oh0, ow0;
     tile_pos(u, b, oh0, ow0);
     unsigned mrow[2], prow[2];
@@ -3426,6 +3432,12 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
       }
     };
     load_half(0, fa[0], fb[0]);
+    if (ff) {  // fragments first (DMY_HALO_FF): the next halo's DMA after the first half-tap's reads and the
+      // accumulate / residual loads, so neither queues behind it
+      __builtin_amdgcn_sched_barrier(0);
+      if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int h = 0; h < 18; ++h) {
       if (h + 1 < 18) load_half(h + 1, fa[(h + 1) & 1], fb[(h + 1) & 1]);
@@ -3900,12 +3912,13 @@ int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, con
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps));
   const unsigned yb = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned rb = ep.res != nullptr ? (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * ep.rps)) : 0u;
+  static const int ff = env_int("DMY_HALO_FF", 0);
   if (!DG && ep.on)  // inference epilogue: its own instantiation, so the training kernel's registers are untouched
     v3::conv3_halo64<false, true><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per,
-                                                                           xb, 2u * 64 * 576, yb, acc, ep, rb);
+                                                                           xb, 2u * 64 * 576, yb, acc, ep, rb, ff);
   else
     v3::conv3_halo64<DG><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb,
-                                                                    2u * 64 * 576, yb, acc, ep, rb);
+                                                                    2u * 64 * 576, yb, acc, ep, rb, ff);
   return (int)hipGetLastError();
 }
 
@@ -4434,7 +4447,8 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * 9 * g.C, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
-  v3::conv_wgrad_tap<BM><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db);
+  static const int ff = env_int("DMY_TAP_FF", 0);
+  v3::conv_wgrad_tap<BM><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db, ff);
   wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
