@@ -55,8 +55,10 @@ def parse():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='dma-1536', choices=list(CONFIGS))
-    ap.add_argument('--also', default='v5s-640', choices=list(CONFIGS) + ['none'],
-                    help='second configuration measured in the same run (nested in the JSON line)')
+    ap.add_argument('--also', default='v5s-640,c5-1920',
+                    help='comma list of further configurations measured in the same run, each nested in the JSON '
+                         'line as at_<img> ("none": only --config).  c5-1920 (BASELINE configs[4]) runs with the fp8 '
+                         'forward, plus a bf16 run of the same steps for its step time')
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch of --config (default: the config)')
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -120,7 +122,17 @@ def build(cfg, dtype, device, fp8=False):
 
 def cpu_baseline(cfg, seconds):
     """The oracle (CPU fp32 restatement of the reference) timed on this host: bs1 train step at the bench
-    resolution (fwd + loss + bwd + SGD), repeated for a bounded ~`seconds` sample."""
+    resolution (fwd + loss + bwd + SGD), repeated for a bounded ~`seconds` sample, on every CPU this job is allotted.
+    SURVEY §8(d) asks for all host cores; on the GPU box the job's share is OMP_NUM_THREADS (16 of the machine's 256
+    logical CPUs; the harness sizes every pool to it), and a round-5 run with one thread per machine CPU (256) did not
+    finish the bench within 900 s, so the baseline runs at torch's thread count = that share, and reports both."""
+    v, n, el = _cpu_baseline_run(cfg, seconds)
+    return dict(value=v, unit='images/s', cores=torch.get_num_threads(), kind='port',
+                sample=f'{n} bs1 train steps of {cfg[0]} @{cfg[2]} (fp32 CPU oracle, {el:.1f} s, '
+                       f'{torch.get_num_threads()} threads)', **host_cpu())
+
+
+def _cpu_baseline_run(cfg, seconds):
     from oracle import nn as onn
     from oracle.loss import compute_loss
     from dmayolo.synthetic import CONFIGS as CDIR, HYP_VISDRONE, scaled_hyp, images, targets
@@ -153,8 +165,7 @@ def cpu_baseline(cfg, seconds):
         el = time.perf_counter() - t0
         if (el > seconds and n >= 2) or n >= 2000:
             break
-    return dict(value=n / el, unit='images/s', cores=torch.get_num_threads(), kind='port',
-                sample=f'{n} bs1 train steps of {yml} @{img} (fp32 CPU oracle, {el:.1f} s)', **host_cpu())
+    return n / el, n, el
 
 
 def host_cpu():
@@ -173,7 +184,21 @@ def host_cpu():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    return dict(cpu_model=model, cpus_available=avail, cpus_machine=os.cpu_count())
+    quota = None  # cgroup CPU quota in CPUs (v2 cpu.max, v1 cfs quota / period), if the job has one
+    for path, split in (('/sys/fs/cgroup/cpu.max', True), ('/sys/fs/cgroup/cpu/cpu.cfs_quota_us', False)):
+        try:
+            with open(path) as f:
+                t = f.read().split()
+            if split and t[0] != 'max':
+                quota = round(int(t[0]) / int(t[1]), 2)
+            elif not split and int(t[0]) > 0:
+                with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+                    quota = round(int(t[0]) / int(f.read()), 2)
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return dict(cpu_model=model, cpus_available=avail, cpus_machine=os.cpu_count(), cgroup_cpu_quota=quota,
+                omp_num_threads=os.environ.get('OMP_NUM_THREADS'))
 
 
 def write_launch_table(path, table, ks, cfg_name):
@@ -241,7 +266,9 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
                             % (steps, el_events * 1e3 / steps))
 
 
-def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_seconds=15.0, fp8=False):
+def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_seconds=15.0, fp8=False, light=False):
+    """light: only the timed steps (no roofline pass, detect or CPU baseline) -- the bf16 twin of the fp8 config-5
+    leg, for its step time"""
     from dmayolo.functional import KernelTimer
     from dmayolo.synthetic import images, targets, clustered_predictions
     from dmayolo.infer import GraphedDetector
@@ -281,6 +308,17 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if light:
+        if world > 1:
+            t = torch.tensor([el], device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        res = dict(value=round(world * bs * a.steps / el, 2), ms_per_step=round(el / a.steps * 1e3, 3),
+                   peak_hbm_gib=round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1))
+        del tr, net, model, imgs, tg, loss, items
+        gc.collect()
+        torch.cuda.empty_cache()
+        return res
     # roofline pass: the same K steps again with a HIP event pair around every implicit-GEMM launch on its stream
     # (functional.KernelTimer).  Kept out of the timed region: ~380 event records per yolov5s step cost ~6 % of the
     # step (3400 vs 3184 img/s measured), which would understate `value`.
@@ -390,9 +428,16 @@ def main():
     dtype = torch.bfloat16 if a.dtype == 'bf16' else torch.float32
 
     head = run_config(a.config, a, world, rank, dev_idx, device, dtype, a.batch, a.cpu_seconds, fp8=a.fp8)
-    also = None
-    if a.also != 'none' and a.also != a.config:
-        also = run_config(a.also, a, world, rank, dev_idx, device, dtype, 0, a.cpu_seconds)
+    also = {}
+    for name in [n for n in a.also.split(',') if n and n != 'none' and n != a.config]:
+        assert name in CONFIGS, (name, list(CONFIGS))
+        f8 = name == 'c5-1920' and dtype == torch.bfloat16  # BASELINE configs[4]: "fp8 MFMA conv"
+        r = run_config(name, a, world, rank, dev_idx, device, dtype, 0, a.cpu_seconds, fp8=f8)
+        if f8:
+            b = run_config(name, a, world, rank, dev_idx, device, dtype, 0, fp8=False, light=True)
+            r['dtype'] = 'bf16 storage, fp8 e4m3 forward convs'
+            r['bf16_twin'] = dict(b, fp8_speedup=round(r['value'] / b['value'], 4))
+        also['at_%d' % CONFIGS[name][2]] = dict(config_name=name, **r)
 
     if rank == 0:
         img = CONFIGS[a.config][2]
@@ -406,8 +451,7 @@ def main():
             'config': head.pop('config'), 'roofline': head.pop('roofline'), 'cpu_baseline': head.pop('cpu_baseline'),
             **head,
         }
-        if also is not None:
-            line['at_%d' % CONFIGS[a.also][2]] = dict(config_name=a.also, **also)
+        line.update(also)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -18,6 +18,7 @@
 // Epilogues go through LDS so every global store / atomic is a 16-B vector or a 256-B wave segment.
 // MFMA: bf16 -> v_mfma_f32_16x16x32_bf16, f32 -> v_mfma_f32_16x16x4_f32 (exact fp32, parity mode).
 // Block ids are remapped so consecutive tiles sharing an A panel land on one XCD (L2 reuse).
+#include <mutex>
 #include "common.h"
 #include <cstdlib>
 #include <type_traits>
@@ -1892,6 +1893,222 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
                                       n0, S2Cls{0, 0, 0, 0}, ep, bb);
 }
 
+// ---------------------------------------------------------------- 256 x 256 half-tile pipeline (conv_fwd_8p, round 5)
+// The wide tile above stages whole 64 KiB K steps in a 2-stage ring and drains the DMA queue (vmcnt(0)) before every
+// barrier, so each step's loads have one step of MFMA time to land and the 8 waves run in lockstep: all read LDS, then
+// all issue MFMAs.  This kernel is cdna_hip_programming.md §5's 256² phase template applied to the implicit-GEMM
+// loaders:
+//   * the staging unit is a HALF tile (128 rows x 64 k = 16 KiB = 2 LDS-DMA instructions per wave); A half-tiles are
+//     triple-buffered and B half-tiles double-buffered (10 x 16 KiB = the whole 160 KiB of LDS);
+//   * a K step is 4 phases; in each a wave reads one register subtile (p0: A rows 0-63 + B cols 0-31, p1: B cols
+//     32-63, p2: A rows 64-127, p3: nothing -- every fragment it needs is still in registers), issues ONE half-tile of
+//     a later K step (p0: B1(u+1), p1: A0(u+2), p2: A1(u+2), p3: B0(u+2)), barriers, and runs 16 MFMAs of one quadrant
+//     of its 128 x 64 tile; the counted vmcnt(6) at p3 leaves 3 half-tiles in flight, never 0 inside the loop;
+//   * the two wave groups (waves 0-3 / 4-7, one of each per SIMD) run one barrier apart, so on every SIMD one wave's
+//     LDS reads and DMA issue overlap the other wave's MFMAs.
+// The RAW / WAR safety of exactly this schedule (every slot restaged >= 2 phases after its last read; every read one
+// barrier after all waves' retiring vmcnt) is checked formally by tools/sched8p_check.py.  Same GEMM views, loaders'
+// address arithmetic (FwdLdsB) and epilogue (v3_epilogue, 128 x 64 wave tiles) as conv_fwd_w.
+namespace p8 {
+constexpr int HALF = 16384;
+constexpr int NA = 3, NB = 2;
+constexpr int LDS = (2 * NA + 2 * NB) * HALF;  // 160 KiB
+DEV char* slot_a(char* s, int h, int t) { return s + ((t % NA) * 2 + h) * HALF; }
+DEV char* slot_b(char* s, int h, int t) { return s + (2 * NA + (t % NB) * 2 + h) * HALF; }
+}  // namespace p8
+
+template <bool P1, bool DG>
+struct Lds8 {
+  __amdgpu_buffer_rsrc_t rx, rw;
+  int H, W, C, KW, xps;
+  int kh, kw, ci0, kpos;  // A stream cursor
+  int kposb;              // B stream cursor
+  int kl;
+  int pix[4], ih0[4], iw0[4];
+  bool aval[4];
+  unsigned boff[4];
+  // piece J (half J >> 1, instruction J & 1) of wave wid covers rows (J >> 1) * 128 + wid * 16 + (J & 1) * 8 + lane / 8
+  DEV Lds8(const bf16* x, const bf16* w, const Geom& g, long M, long m0, int n0, int wid, int lane, unsigned xbytes,
+           unsigned wbytes)
+      : H(g.H), W(g.W), C(g.C), KW(g.KW), xps((int)g.xps), kh(0), kw(0), ci0(0), kpos(0), kposb(0) {
+    rx = make_rsrc(x, xbytes);
+    rw = make_rsrc(w, wbytes);
+    const int Ktot = g.KH * g.KW * g.C;
+    kl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int r = (J >> 1) * 128 + wid * 16 + (J & 1) * 8 + (lane >> 3);
+      const long m = m0 + r;
+      aval[J] = m < M;
+      const int mm = (int)(aval[J] ? m : 0);
+      const int ow = mm % g.OW, t = mm / g.OW, oh = t % g.OH, b = t / g.OH;
+      if (P1) {
+        pix[J] = mm * xps;
+        ih0[J] = iw0[J] = 0;
+      } else {
+        ih0[J] = DG ? oh + g.P : oh * g.S - g.P;
+        iw0[J] = DG ? ow + g.P : ow * g.S - g.P;
+        pix[J] = ((b * g.H + ih0[J]) * g.W + iw0[J]) * xps;  // may be negative; valid taps land >= 0
+      }
+      const int n = n0 + r;
+      boff[J] = n < g.K ? (unsigned)(n * Ktot + kl) * 2u : kBufOob;
+    }
+  }
+  // half h of the A stream's next K step into `dst`; the cursor advances after half 1
+  DEV void issue_a(char* dst, int h, int wid) {
+    const int dh = DG ? -kh : kh, dw = DG ? -kw : kw;
+    const int delta = P1 ? kpos + kl : (dh * W + dw) * xps + ci0 + kl;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int J = h * 2 + j;
+      bool ok = aval[J];
+      if (!P1) ok = ok && (unsigned)(ih0[J] + dh) < (unsigned)H && (unsigned)(iw0[J] + dw) < (unsigned)W;
+      blds16(rx, ok ? (unsigned)(pix[J] + delta) * 2u : kBufOob, dst + (wid * 2 + j) * 1024);
+    }
+    if (h == 1) {
+      kpos += BK;
+      if (!P1) {
+        ci0 += BK;
+        if (ci0 == C) {
+          ci0 = 0;
+          if (++kw == KW) {
+            kw = 0;
+            ++kh;
+          }
+        }
+      }
+    }
+  }
+  DEV void issue_b(char* dst, int h, int wid) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int J = h * 2 + j;
+      blds16(rw, boff[J] == kBufOob ? kBufOob : boff[J] + (unsigned)kposb * 2u, dst + (wid * 2 + j) * 1024);
+    }
+    if (h == 1) kposb += BK;
+  }
+};
+
+#define P8_BAR()                          \
+  do {                                    \
+    __builtin_amdgcn_sched_barrier(0);    \
+    __builtin_amdgcn_s_barrier();         \
+    __builtin_amdgcn_sched_barrier(0);    \
+  } while (0)
+
+template <bool P1, bool DG>
+__global__ void __launch_bounds__(512) conv_fwd_8p(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                   const float* __restrict__ bias, bf16* __restrict__ y,
+                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
+                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep,
+                                                   BnB bb) {
+  constexpr int BM = 256, BN = 256;
+  __shared__ __attribute__((aligned(1024))) char smem[p8::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = wid >> 2, wm = wid & 1, wn = wid >> 1;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
+  Lds8<P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+  // prologue: K step 0 whole, step 1's A0, A1, B0 (each operand's halves in stream order)
+  ld.issue_a(p8::slot_a(smem, 0, 0), 0, wid);
+  ld.issue_a(p8::slot_a(smem, 1, 0), 1, wid);
+  ld.issue_b(p8::slot_b(smem, 0, 0), 0, wid);
+  ld.issue_b(p8::slot_b(smem, 1, 0), 1, wid);
+  if (nk > 1) {
+    ld.issue_a(p8::slot_a(smem, 0, 1), 0, wid);
+    ld.issue_a(p8::slot_a(smem, 1, 1), 1, wid);
+    ld.issue_b(p8::slot_b(smem, 0, 1), 0, wid);
+    vm_wait<6>();
+  } else {
+    vm_wait<0>();
+  }
+  P8_BAR();
+  if (grp) P8_BAR();  // group 1 runs one barrier behind group 0
+  const int rb = (wn & 1) * 64;  // this wave's first column (row of the B half-tile)
+  bf16x8 a[2][4], b0[2][2], b1[2][2];
+  for (int u = 0; u < nk; ++u) {
+    const bf16* As = reinterpret_cast<const bf16*>(p8::slot_a(smem, wm, u));
+    const bf16* Bs = reinterpret_cast<const bf16*>(p8::slot_b(smem, wn >> 1, u));
+    // ---- p0: A rows 0-63, B cols 0-31; stage B1(u+1)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[h][i] = frag_sw(As, i * 16, h * 32, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[h][j] = frag_sw(Bs, rb + j * 16, h * 32, lane);
+    }
+    if (u + 1 < nk) ld.issue_b(p8::slot_b(smem, 1, u + 1), 1, wid);
+    P8_BAR();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b0[h][j], acc[i][j], 0, 0, 0);
+    P8_BAR();
+    // ---- p1: B cols 32-63; stage A0(u+2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[h][j] = frag_sw(Bs, rb + 32 + j * 16, h * 32, lane);
+    if (u + 2 < nk) ld.issue_a(p8::slot_a(smem, 0, u + 2), 0, wid);
+    P8_BAR();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b1[h][j], acc[i][2 + j], 0, 0, 0);
+    P8_BAR();
+    // ---- p2: A rows 64-127; stage A1(u+2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[h][i] = frag_sw(As, 64 + i * 16, h * 32, lane);
+    if (u + 2 < nk) ld.issue_a(p8::slot_a(smem, 1, u + 2), 1, wid);
+    P8_BAR();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b1[h][j], acc[4 + i][2 + j], 0, 0, 0);
+    P8_BAR();
+    // ---- p3: no reads; stage B0(u+2); step u+1 must have landed before the next p0 (3 halves stay in flight)
+    if (u + 2 < nk) {
+      ld.issue_b(p8::slot_b(smem, 0, u + 2), 0, wid);
+      vm_wait<6>();
+    } else if (u + 1 < nk) {
+      vm_wait<0>();
+    }
+    P8_BAR();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b0[h][j], acc[4 + i][j], 0, 0, 0);
+    P8_BAR();
+  }
+  if (!grp) P8_BAR();  // group 0 catches up with group 1's extra barrier
+  __syncthreads();
+  v3_epilogue<BM, BN, 2, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
+                                     S2Cls{0, 0, 0, 0}, ep, bb);
+}
+#undef P8_BAR
+
 // ---------------------------------------------------------------- 1x1 streaming GEMM (p1s)
 // Y[m][n] = sum_k X[m][k] W[n][k] for the stride-1 1x1 layers with a short reduction (KD = 64 / 128 / 256). Those
 // GEMMs are HBM-bound, and on the LDS-DMA tiles above they ran at 25-50 % of the HBM rate: one block per CU walks
@@ -3693,6 +3910,11 @@ inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+// DMY_W8P: 1 = the 256 x 256 tiles run the half-tile pipeline (v3::conv_fwd_8p), 0 = the 2-stage wide loop (conv_fwd_w)
+inline int w8p_mode() {
+  static const int t = env_int("DMY_W8P", 0);
+  return t;
+}
 // DMY_P1S = 0 off, 1 (default) the output-heavy forwards (K >= 2 C), 3 those and the output-heavy data-grads, 2 every
 // eligible GEMM view (A/B)
 inline int p1s_mode() {
@@ -3811,6 +4033,12 @@ inline int p1p_lane_mode() {
   return t;
 }
 // conv_p1p's persistent grid: blocks per CU from the LDS footprint, capped at the tile count, a multiple of 8 (XCDs)
+// BN partial rows written by the last training forward launched on this host thread (dmy_conv_fwd_last_rows).  The
+// persistent kernels (halo, LANE conv_p1p) write one row per wave of their grid; every other kernel writes
+// dmy_conv_fwd_partial_rows(M, K).  The host allocates dmy_conv_fwd_bound_rows rows and reads the count back, so no
+// second copy of the routing decides it; a persistent launch whose rows would pass the bound declines.
+thread_local long t_prow_last = 0;
+inline long prow_persist_cap() { return 64L * num_cus(); }
 inline int p1p_grid(int ntiles, int lds) {
   const int bpc = (160 * 1024) / lds;
   int G = num_cus() * (bpc < 1 ? 1 : bpc);
@@ -3849,7 +4077,8 @@ inline int p1p_lane_rows(const Geom& gv) {
   return p1p_plan<false>(gv, 0, Epi{}, false, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
     using PP = v3::P1P<decltype(bm)::value, decltype(bn)::value, decltype(ns)::value, decltype(wtr)::value>;
     const int gm = ceil_div(M, decltype(bm)::value), gn = ceil_div(gv.K, decltype(bn)::value);
-    return gn == 1 ? p1p_grid(gm * gn, PP::LDS) * PP::C3_::WM : 0;
+    const long r = gn == 1 ? (long)p1p_grid(gm * gn, PP::LDS) * PP::C3_::WM : 0;
+    return r <= prow_persist_cap() ? (int)r : 0;
   });
 }
 template <bool DG>
@@ -3865,7 +4094,9 @@ int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps,
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN), ntiles = gm * gn;
     const int G = p1p_grid(ntiles, PP::LDS);
     if constexpr (!DG) {
-      if (ps != nullptr && !small && gn == 1 && p1p_lane_mode()) {  // one BN partial row per wave (dmy_conv_fwd_bn_rows)
+      if (ps != nullptr && !small && gn == 1 && p1p_lane_mode() && (long)G * PP::C3_::WM <= prow_persist_cap()) {
+        // one BN partial row per wave (dmy_conv_fwd_last_rows)
+        t_prow_last = (long)G * PP::C3_::WM;
         v3::conv_p1p<BM, BN, NS, WTR, false, true><<<(unsigned)G, PP::NTH, 0, st>>>(
             x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb, ff);
         return (int)hipGetLastError();
@@ -3986,8 +4217,17 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
     return (int)hipGetLastError();                                                                                 \
   }
   if (tov < 0 && buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
-      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus())
+      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
+    if (w8p_mode() && bb.z == nullptr) {  // the half-tile pipeline (conv_fwd_8p)
+      const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 256);
+      if (p1) v3::conv_fwd_8p<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
+                                                                         wbytes, ep, bb);
+      else v3::conv_fwd_8p<false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
+                                                                          wbytes, ep, bb);
+      return (int)hipGetLastError();
+    }
     W_GO(256, 256)
+  }
   if (tov < 0 && buf && tall_mode() && !p1 && gv.K > 64 && gv.K <= 128 &&
       (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
     W_GO(512, 128)
@@ -4076,10 +4316,20 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   // 1.17 ms): 256 KB of slabs per tile read serially by one reducer block + a release per block
   static const int fz = env_int("DMY_SPLITK_FUSED", 0);
   // the tickets are one device array: the stream of the first fused launch owns them, any other stream takes the
-  // two-launch path (two streams' fused launches would share counters)
-  static std::atomic<hipStream_t> owner{nullptr};
-  hipStream_t none = nullptr;
-  const bool mine = fz && (owner.compare_exchange_strong(none, st) || none == st);
+  // two-launch path (two streams' fused launches would share counters).  Ownership is a separate claimed
+  // flag, not a null-pointer sentinel: torch's default stream IS the null stream
+  bool mine = false;
+  if (fz) {
+    static std::mutex mu;
+    static bool claimed = false;
+    static hipStream_t owner = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!claimed) {
+      claimed = true;
+      owner = st;
+    }
+    mine = owner == st;
+  }
   const int fused = mine && gm * gn <= v3::kSplitCnt ? 1 : 0;
   if (g.K > 64) {
     if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
@@ -4152,11 +4402,15 @@ template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
+  if (ps != nullptr) t_prow_last = dmy_conv_fwd_partial_rows(M, g.K);
   if constexpr (sizeof(T) == 2) {
-    if (b == nullptr && halo_ok(g, x, w, y) && (!ep.on || ps == nullptr) &&
+    if (b == nullptr && halo_ok(g, x, w, y) && (!ep.on || ps == nullptr) && halo_rows(g) <= prow_persist_cap() &&
         (!ep.on || ep.res == nullptr ||
          (ep.rps % 8 == 0 && aligned16(ep.res) && 2.0 * ((double)g.N * g.OH * g.OW * ep.rps) < (double)v3::kBufOob)))
+    {
+      if (ps != nullptr) t_prow_last = halo_rows(g);
       return launch_halo<false>((const bf16*)x, (const bf16*)w, (bf16*)y, ps, pq, g, st, 0, ep);
+    }
     if (conv_buf_mode() && sk_ok(g, x, w, y, ps, ep))
       return launch_sk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, st, ep);
     // small-M 1x1 layers (batch-1 inference: M < 65536): the register-epilogue GEMM on one-wave 64 x 64 tiles
@@ -4642,11 +4896,18 @@ inline bool fp8_fwd_ok(int C, int K, long yps, const void* x8, const void* w8, c
 
 DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile(M, K) ? 128 : 64); }
 
+DMY_API long dmy_conv_fwd_bound_rows(long M, int K) {
+  const long r = dmy_conv_fwd_partial_rows(M, K);
+  return r > prow_persist_cap() ? r : prow_persist_cap();
+}
+DMY_API long dmy_conv_fwd_last_rows() { return t_prow_last; }
+
 DMY_API int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w, const float* bias, const void* y,
                                         int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P,
                                         int OH, int OW, long yps) {
   const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  if (dtype && bias == nullptr && halo_ok(g, x, w, y)) return halo_rows(g);  // one row per wave (conv3_halo64)
+  if (dtype && bias == nullptr && halo_ok(g, x, w, y) && halo_rows(g) <= prow_persist_cap())
+    return halo_rows(g);  // one row per wave (conv3_halo64)
   if (dtype) {  // the training forward's route through conv_fwd_t / launch_v3 to a LANE conv_p1p: one row per wave
     const long M = (long)N * OH * OW;
     const bool p1 = KH == 1 && KW == 1 && S == 1 && P == 0;

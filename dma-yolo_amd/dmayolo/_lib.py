@@ -22,6 +22,8 @@ P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 SIGNATURES = {
     # conv.hip
     'dmy_conv_fwd_partial_rows': [L, I],
+    'dmy_conv_fwd_bound_rows': [L, I],
+    'dmy_conv_fwd_last_rows': [],
     'dmy_conv_fwd_bn_rows': [I, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L],
     'dmy_conv_fwd': [I, P, P, P, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
     'dmy_conv_dgrad': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P],
@@ -139,7 +141,7 @@ SIGNATURES = {
 
 # symbols whose argtypes dmayolo/optim.py sets itself (multi-tensor optimizer / GradScaler / EMA kernels)
 SELF_BOUND = {'dmy_chunk_size', 'dmy_sgd', 'dmy_adam', 'dmy_ema', 'dmy_amp_check', 'dmy_amp_update'}
-LONG_RET = {'dmy_conv_dgrad_bn_rows'}
+LONG_RET = {'dmy_conv_dgrad_bn_rows', 'dmy_conv_fwd_bound_rows', 'dmy_conv_fwd_last_rows'}
 
 
 def restype(name):

@@ -21,9 +21,10 @@ parameter order), so here the buckets ARE contiguous slices of that buffer and n
   * buffers (BN running statistics) are broadcast from rank 0 before each forward and the initial state once at
     construction, as DDP's defaults (broadcast_buffers=True).
 
-Assumes, as DDP without find_unused_parameters does, that the same parameters receive gradients on every rank (a
-static graph: true for every model here; a parameter with no gradient on this rank keeps .grad None and its zero slice
-is reduced with the rest).  The loss * WORLD_SIZE of train.py:440 stays in the backward seed (GradScaler.upstream), so
+A parameter that gets no gradient on this rank still has its (zeroed) slice reduced with the rest, and after backward
+its .grad is that slice -- the rank average, zero when no rank used it -- as torch DDP writes the reduced gradient into
+locally unused parameters, so replicas cannot diverge.  The hooks act only for a backward this wrapper armed (a
+training forward through it); `close()` removes them, and a model may be wrapped again after that.  The loss * WORLD_SIZE of train.py:440 stays in the backward seed (GradScaler.upstream), so
 the averaged gradient is the sum over ranks, exactly as with DDP.
 """
 import torch
@@ -79,12 +80,32 @@ class ArenaDDP(torch.nn.Module):
                 self.bucket_of[id(p)] = b
         self._bw = None
         self._buf = None
+        self._handles = []
+        self.trace = None  # a list to record ('hook', name) / ('launch', bucket) events in order (tests: overlap)
         with torch.no_grad():
             state = [t for t in module.state_dict().values() if torch.is_tensor(t)]
             if state:
                 dist._broadcast_coalesced(self._group(), state, 250 * 2 ** 20, 0)
         for p in self.reduced:
-            p.register_post_accumulate_grad_hook(self._hook)
+            if getattr(p, '_dmy_arena_ddp', None) is not None:
+                raise RuntimeError('ArenaDDP: a parameter is already hooked by another live wrapper; close() it first')
+            p._dmy_arena_ddp = True
+            self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def close(self):
+        """remove the gradient hooks (the model can then be used unwrapped, or wrapped again)"""
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+        for p in self.reduced:
+            p._dmy_arena_ddp = None
+        self._bw = self._buf = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _group(self):
         return self.pg if self.pg is not None else dist.group.WORLD
@@ -115,14 +136,14 @@ class ArenaDDP(torch.nn.Module):
         return buf[o:o + k].view_as(p)
 
     def _begin(self):
-        if self._buf is None:
-            raise RuntimeError('ArenaDDP: backward without a training forward through the wrapper')
         self._bw = _Backward(self._buf, [len(ps) for _, _, ps in self.buckets])
         self._buf = None
         torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
         return self._bw
 
     def _hook(self, p):
+        if self._bw is None and self._buf is None:
+            return  # a backward this wrapper did not arm (e.g. through de_parallel(model) under no wrapper forward)
         bw = self._bw if self._bw is not None else self._begin()
         sl = self._slice(bw.buf, p)
         if p.grad is not None and p.grad.data_ptr() != sl.data_ptr():
@@ -131,6 +152,8 @@ class ArenaDDP(torch.nn.Module):
         if id(p) in bw.seen:  # a parameter used twice accumulates once more: its slice already holds the total
             return
         bw.seen.add(id(p))
+        if self.trace is not None:
+            self.trace.append(('hook', id(p)))
         b = self.bucket_of[id(p)]
         bw.pending[b] -= 1
         if bw.pending[b] == 0:
@@ -142,6 +165,8 @@ class ArenaDDP(torch.nn.Module):
         while bw.next < len(self.buckets) and (upto == 'all' or bw.ready[bw.next]):
             lo, hi, _ = self.buckets[bw.next]
             view = bw.buf[lo:hi]
+            if self.trace is not None:
+                self.trace.append(('launch' if upto is None else 'launch_final', bw.next))
             if self.world == 1:
                 bw.works.append((None, None, view))
             elif self.compress == 'bf16':
@@ -161,3 +186,6 @@ class ArenaDDP(torch.nn.Module):
                 work.wait()  # RCCL: the current stream waits on the collective's stream (no host sync)
             if c is not None:
                 view.copy_(c)
+        for p in self.reduced:
+            if id(p) not in bw.seen:  # no gradient on this rank: it still gets the rank average (DDP semantics)
+                p.grad = self._slice(bw.buf, p)

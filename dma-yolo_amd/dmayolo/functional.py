@@ -648,11 +648,12 @@ class ConvBNActFn(torch.autograd.Function):
             if train_bn:
                 if f8 is not None:
                     P = call('dmy_conv_fwd_fp8_partial_rows', M, K)
-                else:  # the row count of the kernel the dispatch picks for exactly this launch (halo: per wave)
-                    P = call('dmy_conv_fwd_bn_rows', dcode(x), ptr(x), ptr(wf), ptr(bias), ptr(z), N, Hg, Wg, Cg,
-                             xps, K, kg, kg, sg, pg, OH, OW, K)
+                else:  # rows for any route; the launch reports the rows its kernel wrote (halo / LANE: per wave)
+                    P = call('dmy_conv_fwd_bound_rows', M, K)
                 psum, psq = f32(P * K, dev), f32(P * K, dev)
                 _launch_conv_fwd(x, xps, wf, bias, z, K, psum, psq, K, kg, sg, pg, OH, OW, C, k, f8=f8)
+                if f8 is None:
+                    P = call('dmy_conv_fwd_last_rows')
                 if P > 256:  # two-stage column reduction of the epilogue partials
                     S = call('dmy_colsum2_rows', P)
                     ps2, pq2 = f32(S * K, dev), f32(S * K, dev)
@@ -676,11 +677,15 @@ class ConvBNActFn(torch.autograd.Function):
                 # the consumer (SCGateFn) reads z and applies scale / shift itself, and hands this layer's backward the
                 # reduce partials (BnLink): the tensor returned is z, valid only for that consumer
                 ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
-                ctx.bnlink = BnLink(z, scale, shift, mean, invstd, spec.act, K)
+                # the link must NOT hold z here: z is this Function's OUTPUT, so ctx -> link -> z -> grad_fn -> ctx would
+                # be a reference cycle through the C++ autograd node that Python's GC cannot break (round 4 leaked
+                # every SCConv's z, ~4 GiB per DMA-1536 step).  The gate receives z as its own input.
+                ctx.bnlink = BnLink(None, scale, shift, mean, invstd, spec.act, K)
                 z._dmy_affine, z._dmy_bnlink = (scale, shift, mean, invstd), ctx.bnlink
                 ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, False
-                ctx.link_in = link_in if (link_in is not None and not s2d and Cp == C and link_in.K == C and
-                                          link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
+                ctx.link_in = link_in if (link_in is not None and link_in.z is not None and not s2d and Cp == C and
+                                          link_in.K == C and link_in.z.shape[0] == N and
+                                          link_in.z.shape[2:] == (H, W)) else None
                 ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
                 ctx.ggeom = (Hg, Wg, kg, sg, pg)
                 ctx.cp = Cp
@@ -717,8 +722,8 @@ class ConvBNActFn(torch.autograd.Function):
                 y = z
             ctx.save_for_backward(x, wt, z)
         ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
-        ctx.link_in = link_in if (link_in is not None and not s2d and Cp == C and link_in.K == C and
-                                  link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
+        ctx.link_in = link_in if (link_in is not None and link_in.z is not None and not s2d and Cp == C and
+                                  link_in.K == C and link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
         ctx.ggeom = (Hg, Wg, kg, sg, pg)
         ctx.cp = Cp

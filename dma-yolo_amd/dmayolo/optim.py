@@ -105,7 +105,8 @@ class FusedAdam(torch.optim.Optimizer):
     device int32 counter (a cohort), and each cohort of a group is one kernel launch -- normally one per group.  The
     counters live in the optimizer (not in param_groups / state), and state_dict() stores torch's format: a float32
     CPU 'step' per parameter, from which load_state_dict + the next step() rebuild the counters on the parameters'
-    device (a checkpoint loaded with map_location='cpu' works)."""
+    device (a checkpoint loaded with map_location='cpu' works).  A member that has no gradient in some step leaves
+    its cohort on a copy of the counter, so its count stops as torch's would."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -141,6 +142,12 @@ class FusedAdam(torch.optim.Optimizer):
                 c = self._counter(p, fresh)
                 st['step'] = c  # torch keeps Adam's step as a tensor too; read it (host sync) only to log / save
                 cohorts.setdefault(id(c), (c, []))[1].append(p)
+            # a cohort member without a gradient this step must keep its count (torch leaves its 'step' alone): it
+            # leaves the cohort on a copy of the counter taken before the launch advances it
+            for q in g['params']:
+                cq = self._ctr.get(id(q)) if q.grad is None else None
+                if cq is not None and id(cq) in cohorts:
+                    self._ctr[id(q)] = self.state[q]['step'] = cq.clone()
             b1, b2 = g['betas']
             PARAM_GEN[0] += 1
             for c, cp in cohorts.values():

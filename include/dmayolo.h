@@ -27,6 +27,13 @@ int dmy_conv_fwd_partial_rows(long M, int K);
 /* BN partial rows dmy_conv_fwd writes for exactly these arguments (psum / psq must hold that many rows of K floats):
  * the per-tile count of dmy_conv_fwd_partial_rows, or one row per wave of the persistent halo kernel
  * (3x3 stride-1 64 -> 64-channel layers, csrc/conv.hip conv3_halo64) */
+/* BN partial rows: an upper bound for any route of a training forward with these M / K (allocate this many rows of
+ * psum / psq), and the rows the last training forward launched on this host thread actually wrote (pass that count
+ * to dmy_colsum2 / dmy_bn_finalize).  Replaces the host-side prediction dmy_conv_fwd_bn_rows for allocation: the
+ * count comes from the routing that launched.  BatchNorm2d.forward's batch statistics,
+ * torch/nn/modules/batchnorm.py via models/common.py:72 */
+long dmy_conv_fwd_bound_rows(long M, int K);
+long dmy_conv_fwd_last_rows(void);
 int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w_ohwi, const float* bias, const void* y, int N,
                                 int H, int W, int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW,
                                 long yps);

@@ -162,3 +162,101 @@ def test_arena_reducer_world2_matches_ddp_sum(compress):
             de, dg = v.detach() - init[k], got[k] - init[k]
             # bf16 carries ~3 significant digits of each rank's half; floor for the near-cancelling BN sums
             assert float((dg - de).norm()) <= 1e-2 * max(float(de.norm()), 1e-2 * dmax), k
+
+
+def _overlap_worker(rank, world, port, out):
+    """the first bucket's collective is issued from a gradient hook while backward still runs (before the last
+    parameter's hook), i.e. communication overlaps the rest of backward (train.py:322-326 DDP behaviour)"""
+    _setup()
+    from dmayolo.ddp import ArenaDDP
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    model = _model()
+    net = ArenaDDP(model, bucket_cap_mb=0.25, first_bucket_mb=0.05)
+    net.trace = []
+    x, t = _batch(rank)
+    loss, _ = _loss_fn(model)(net(x), t)
+    loss.backward()
+    kinds = [k for k, _ in net.trace]
+    last_hook = max(i for i, k in enumerate(kinds) if k == 'hook')
+    first_launch = kinds.index('launch')
+    early = sum(1 for i, k in enumerate(kinds) if k == 'launch' and i < last_hook)
+    buckets = [b for k, b in net.trace if k.startswith('launch')]
+    if rank == 0:
+        torch.save(dict(first_launch=first_launch, last_hook=last_hook, early=early, n=len(net.buckets),
+                        order=buckets), out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_arena_reducer_overlaps_backward():
+    _setup()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, 'r.pt')
+        mp.spawn(_overlap_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        r = torch.load(out, weights_only=True)
+    assert r['first_launch'] < r['last_hook'], r
+    assert r['early'] >= r['n'] // 2, r  # most buckets go out before backward ends
+    assert r['order'] == list(range(r['n'])), r  # every bucket once, in bucket order
+
+
+class _Branchy(torch.nn.Module):
+    """a parameter (`b`) that only rank 0 uses"""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = torch.nn.Linear(8, 8)
+        self.b = torch.nn.Linear(8, 8)
+
+    def forward(self, x, use_b):
+        y = self.a(x)
+        return self.b(y) if use_b else y
+
+
+def _unused_worker(rank, world, port, out):
+    _setup()
+    from dmayolo.ddp import ArenaDDP
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    m = _Branchy()
+    net = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4)
+    x = torch.randn(4, 8, generator=torch.Generator().manual_seed(rank))
+    net(x, use_b=rank == 0).square().sum().backward()
+    g = {k: p.grad.clone() for k, p in m.named_parameters()}
+    # the wrapper's hooks act only for backward passes it armed; close() removes them and the model can be wrapped
+    # again (ADVICE r4): a backward through the bare model, then a second wrapper
+    m.zero_grad(set_to_none=True)
+    m(x, True).sum().backward()
+    net.close()
+    m.zero_grad(set_to_none=True)
+    net2 = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4)
+    net2(x, use_b=rank == 0).square().sum().backward()
+    g2 = {k: p.grad.clone() for k, p in m.named_parameters()}
+    torch.save(dict(g=g, g2=g2), out + f'.{rank}')
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_arena_reducer_unused_parameter_and_rewrap():
+    """a parameter with a gradient on rank 0 only gets the rank average on BOTH ranks (torch DDP writes the reduced
+    gradient into locally unused parameters); wrapping a model twice works after close()"""
+    _setup()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, 'r.pt')
+        mp.spawn(_unused_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        r = [torch.load(out + f'.{k}', weights_only=True) for k in range(2)]
+    exp = {}
+    for rank in range(2):
+        m = _Branchy()
+        x = torch.randn(4, 8, generator=torch.Generator().manual_seed(rank))
+        m(x, rank == 0).square().sum().backward()
+        for k, p in m.named_parameters():
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            exp[k] = exp.get(k, 0) + g / 2
+    for key in ('g', 'g2'):
+        for k in exp:
+            torch.testing.assert_close(r[0][key][k], exp[k], rtol=1e-5, atol=1e-7)
+            assert torch.equal(r[0][key][k], r[1][key][k]), (key, k)

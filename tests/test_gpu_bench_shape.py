@@ -72,45 +72,63 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     t = targets(bs, nc, seed=1)
     anchors = m.model[-1].anchors.cpu()
 
-    p = m(x.cuda())
-    loss, items = ComputeLoss(m)(p, t.cuda())
-    loss.backward()
+    def perturbed(seed):  # every float tensor moved by up to one fp32 ulp (relative 2^-24), seeded
+        g = torch.Generator().manual_seed(seed)
+        return {k: (v * (1 + (torch.rand(v.shape, generator=g) * 2 - 1) * 2.0 ** -24)).to(v.dtype)
+                if v.is_floating_point() else v for k, v in sd.items()}
+
+    def product_run(sd_):
+        m.load_state_dict(sd_)
+        m.zero_grad(set_to_none=True)
+        p_ = m(x.cuda())
+        lo_, it_ = ComputeLoss(m)(p_, t.cuda())
+        lo_.backward()
+        return ([o.detach().float().cpu() for o in p_], lo_.detach(), it_,
+                {k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
+
+    chaotic = yml in CHAOTIC
+    # product realizations: the state_dict as is, and (chaotic configs) ulp-perturbed copies, seeds 1..3 -- the product
+    # decides its bf16 roundings on slightly different fp32 values, exactly as the emulation realizations below do
+    prods = [product_run(sd)] + ([product_run(perturbed(s_)) for s_ in (1, 2, 3)] if chaotic else [])
+    p, loss, items, pgrads = prods[0]
     ref, pr, lr_, ir_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, None)
     emu, pe_, le_, ie_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16')
     h16, ph_, lh_, ih_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'fp16')
     snk, ps_, ls_, is_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16_sink')
     # more realizations of the bf16 emulation: the same roundings after fp32 sums in another order (GPU torch ops), and
-    # with the weights moved by one fp32 ulp (relative 2^-24 noise, seeds 1 / 2) -- each decides its bf16 roundings on
-    # slightly different fp32 values, as the product's kernels do
+    # with the weights moved by one fp32 ulp (relative 2^-24 noise, seeds 1 / 2 / 3) -- each decides its bf16 roundings
+    # on slightly different fp32 values, as the product's kernels do
     reals = [_oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16', 'cuda')]
-    for seed in (1, 2):
-        g = torch.Generator().manual_seed(seed)
-        sdp = {k: (v * (1 + (torch.rand(v.shape, generator=g) * 2 - 1) * 2.0 ** -24)).to(v.dtype)
-               if v.is_floating_point() else v for k, v in sd.items()}
-        reals.append(_oracle_grads(yml, nc, sdp, x, t, anchors, hyp, 'bf16', 'cuda'))
+    for seed in ((1, 2, 3) if chaotic else (1, 2)):
+        reals.append(_oracle_grads(yml, nc, perturbed(seed), x, t, anchors, hyp, 'bf16', 'cuda'))
 
     def errs(po, lo, io, pg):
+        """pg: parameter name -> its gradient tensor"""
         out = [_rel(a.detach().float().cpu(), b.detach()) for a, b in zip(po, pr)]
         le = abs(float(lo) - float(lr_)) / abs(float(lr_))
         ie = [abs(float(a) - float(b)) / max(abs(float(b)), 1e-12) for a, b in zip(io.cpu(), ir_)]
-        gn = torch.tensor([float(pg[k].grad.norm()) if pg[k].grad is not None else 0.0 for k in names], dtype=torch.float64)
-        g = torch.cat([pg[k].grad.double().cpu().flatten() for k in names])
+        gn = torch.tensor([float(pg[k].norm()) if pg.get(k) is not None else 0.0 for k in names], dtype=torch.float64)
+        g = torch.cat([pg[k].double().cpu().flatten() for k in names])
         layers = {}  # per top-level layer: relative L2 of its concatenated parameter gradients
         for lid in sorted({int(k.split('.')[1]) for k in names}):
             ks = [k for k in names if int(k.split('.')[1]) == lid]
-            layers[lid] = _rel(torch.cat([pg[k].grad.double().cpu().flatten() for k in ks]),
+            layers[lid] = _rel(torch.cat([pg[k].double().cpu().flatten() for k in ks]),
                                torch.cat([pq[k].grad.double().flatten() for k in ks]))
         return out, le, ie, (_rel(gn, gn_b), _rel(g, gb), layers), float(g @ gb / (g.norm() * gb.norm()))
+
+    def grads_of(mod):
+        return {k: q.grad for k, q in mod.named_parameters() if q.grad is not None}
 
     pq = dict(ref.named_parameters())
     names = [k for k in pq if pq[k].grad is not None]
     gn_b = torch.tensor([float(pq[k].grad.norm()) for k in names], dtype=torch.float64)
     gb = torch.cat([pq[k].grad.double().flatten() for k in names])
-    out_err, loss_err, item_err, gn_err, cos = errs(p, loss, items, dict(m.named_parameters()))
-    e_out, e_loss, e_item, e_gn, e_cos = errs(pe_, le_, ie_, dict(emu.named_parameters()))
-    h_out, h_loss, h_item, h_gn, h_cos = errs(ph_, lh_, ih_, dict(h16.named_parameters()))
-    s_out, s_loss, s_item, s_gn, s_cos = errs(ps_, ls_, is_, dict(snk.named_parameters()))
-    rerr = [errs(pp, ll, ii, dict(mm.named_parameters())) for mm, pp, ll, ii in reals]
+    out_err, loss_err, item_err, gn_err, cos = errs(p, loss, items, pgrads)
+    perr = [errs(*pr_) for pr_ in prods]
+    e_out, e_loss, e_item, e_gn, e_cos = errs(pe_, le_, ie_, grads_of(emu))
+    h_out, h_loss, h_item, h_gn, h_cos = errs(ph_, lh_, ih_, grads_of(h16))
+    s_out, s_loss, s_item, s_gn, s_cos = errs(ps_, ls_, is_, grads_of(snk))
+    rerr = [errs(pp, ll, ii, grads_of(mm)) for mm, pp, ll, ii in reals]
     # envelope over the realizations (CPU one included): worst output / loss / item / gradient metrics, lowest cosine
     r_out = [max(v) for v in zip(*[r[0] for r in rerr])]
     r_loss = max(r[1] for r in rerr)
@@ -150,24 +168,42 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     print('  worst layers (id: product err / emulation err): ' +
           ', '.join(f'{i}: {gn_err[2][i]:.2e}/{e_gn[2][i]:.2e}' for i in worst))
     # the parameters that carry the grad-norm-vector error: |norm(product grad) - norm(fp32 grad)|, largest first
-    pm, pe = dict(m.named_parameters()), dict(emu.named_parameters())
-    dn = sorted(((abs(float(pm[k].grad.norm()) - float(gn_b[j])), k, float(gn_b[j])) for j, k in enumerate(names)
-                 if pm[k].grad is not None), reverse=True)[:6]
+    pm, pe = pgrads, grads_of(emu)
+    dn = sorted(((abs(float(pm[k].norm()) - float(gn_b[j])), k, float(gn_b[j])) for j, k in enumerate(names)
+                 if pm.get(k) is not None), reverse=True)[:6]
     lids = sorted({int(k.split('.')[1]) for k in names})
 
     def lnorm(pg, lid):
-        return float(torch.cat([pg[k].grad.double().flatten().cpu() for k in names if int(k.split('.')[1]) == lid]).norm())
-    prs = [dict(mm.named_parameters()) for mm, _, _, _ in reals]
+        return float(torch.cat([pg[k].double().flatten().cpu() for k in names if int(k.split('.')[1]) == lid]).norm())
+    prs = [grads_of(mm) for mm, _, _, _ in reals]
+    pq = grads_of(ref)
     print('  per-layer gradient norm / fp32 (product, bf16 emulation CPU, GPU realizations): ' + ' '.join(
         f'{lid}:{lnorm(pm, lid) / lnorm(pq, lid):.3f},{lnorm(pe, lid) / lnorm(pq, lid):.3f},' +
         ','.join(f'{lnorm(q, lid) / lnorm(pq, lid):.3f}' for q in prs) for lid in lids))
     print('  largest grad-norm differences (fp32 norm: product, bf16 emulation): ' +
-          ', '.join(f'{k} {b:.3e}: {float(pm[k].grad.norm()):.3e}, {float(pe[k].grad.norm()):.3e}' for d, k, b in dn))
-    if yml in CHAOTIC:
-        # see CHAOTIC: the whole-model single-step gradient of this config is a noise realization; its gradient is
-        # pinned by test_bench_shape_fp32_product_vs_oracle and test_bench_shape_layers_bf16_vs_emulation instead.
-        # Sanity only: the same order of magnitude as the emulations' spread
-        assert gn_err[0] <= 0.3 and gn_err[1] <= 1.5 and cos >= 0.3, (gn_err[:2], cos)
+          ', '.join(f'{k} {b:.3e}: {float(pm[k].norm()):.3e}, {float(pe[k].norm()):.3e}' for d, k, b in dn))
+    if chaotic:
+        # see CHAOTIC: the whole-model single-step gradient of this config is a noise realization, so one product
+        # realization against one emulation realization says nothing.  Compared as DISTRIBUTIONS instead (VERDICT r4
+        # item 2b): 4 product realizations (ulp-perturbed weights) against 5 emulation realizations (CPU order, GPU
+        # order, 3 ulp-perturbed) -- the product's MEDIAN grad-norm-vector error, whole-gradient error and cosine must lie
+        # inside the emulation realizations' range (median cosine >= their minimum)
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731 (upper median of an even count: the stricter one)
+        p_gn = [r[3][0] for r in perr]
+        p_wg = [r[3][1] for r in perr]
+        p_cos = sorted(r[4] for r in perr)
+        e_all = rerr + [(e_out, e_loss, e_item, e_gn, e_cos)]
+        e_gnv = [r[3][0] for r in e_all]
+        e_wg = [r[3][1] for r in e_all]
+        e_cs = [r[4] for r in e_all]
+        print(f'  distribution: product grad-norm vector {f(p_gn)} whole {f(p_wg)} cos {f(p_cos)}\n'
+              f'                emulation    grad-norm vector {f(e_gnv)} whole {f(e_wg)} cos {f(e_cs)}')
+        assert med(p_gn) <= max(e_gnv), (p_gn, e_gnv)
+        assert med(p_wg) <= max(e_wg), (p_wg, e_wg)
+        assert p_cos[(len(p_cos) - 1) // 2] >= min(e_cs), (p_cos, e_cs)
+        for r in perr:  # every product realization's outputs / loss inside the per-realization bounds too
+            for a, e in zip(r[0], env_out):
+                assert a <= 1.1 * e + 2e-3, (r[0], env_out)
     else:
         assert gn_err[1] <= 1.1 * max(e_gn[1], r_gn[1]) + 1e-2, (gn_err[:2], e_gn[:2], r_gn[:2])
         assert med <= 1.1, ratios

@@ -101,6 +101,8 @@ def _check_shape(N, C, H, W, K, k, s, seed):
     pq = torch.full((P, K), float('nan'), device=dev)
     assert call('dmy_conv_fwd', 1, ptr(x), ptr(wf), None, ptr(y), ptr(ps), ptr(pq), N, H, W, C, C, K, k, k, s, p, OH,
                 OW, K, stream()) == 0
+    # the rows the launch reports writing (what the product passes to the finalize) = the prediction, and fit the bound
+    assert call('dmy_conv_fwd_last_rows') == P <= call('dmy_conv_fwd_bound_rows', M, K)
     out['fwd'] = (_rel(y.float(), ry), _nr(y.float(), ry))
     s1 = ry.double().sum((0, 2, 3))
     s2 = (ry.double() ** 2).sum((0, 2, 3))

@@ -240,3 +240,26 @@ def test_fused_adam_checkpoint_resume_cpu_map_location(tmp_path):
     torch.testing.assert_close(a.detach().cpu(), ra.detach(), **TOL_ADAM)
     torch.testing.assert_close(b.detach().cpu(), rb.detach(), **TOL_ADAM)
     assert int(opt2.state[a]['step'].cpu()) == 6 and int(opt2.state[b]['step'].cpu()) == 4
+
+
+def test_fused_adam_member_that_skips_a_step_keeps_its_count():
+    """a and b start together (one device counter); b has no gradient in step 3.  torch leaves b's 'step'
+    (and so its bias corrections) alone in that step; FusedAdam moves b onto its own copy of the counter before the
+    launch, so both parameters and both counts equal torch.optim.Adam's after 5 steps."""
+    from dmayolo.optim import FusedAdam
+    g = torch.Generator().manual_seed(7)
+    a0, b0 = torch.randn(4000, generator=g), torch.randn(500, generator=g)
+    a, b = torch.nn.Parameter(a0.cuda()), torch.nn.Parameter(b0.cuda())
+    ra, rb = torch.nn.Parameter(a0.clone()), torch.nn.Parameter(b0.clone())
+    opt = FusedAdam([a, b], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    ref = torch.optim.Adam([ra, rb], lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    for i in range(5):
+        ga, gb = torch.randn(4000, generator=g), torch.randn(500, generator=g)
+        a.grad, ra.grad = ga.cuda(), ga.clone()
+        b.grad, rb.grad = (None, None) if i == 2 else (gb.cuda(), gb.clone())
+        opt.step()
+        ref.step()
+    torch.cuda.synchronize()
+    assert int(opt.state[a]['step'].cpu()) == 5 and int(opt.state[b]['step'].cpu()) == 4
+    torch.testing.assert_close(a.detach().cpu(), ra.detach(), **TOL_ADAM)
+    torch.testing.assert_close(b.detach().cpu(), rb.detach(), **TOL_ADAM)

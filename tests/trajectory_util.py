@@ -175,20 +175,21 @@ def oracle_trajectory(cfg, nc, sd, batches, hyp, steps, mode=None, dev='cuda', p
     return torch.tensor(losses, dtype=torch.float64), out
 
 
-def pin_device_oracle(cfg, nc, sd, batch, hyp):
-    """first step of the device-run fp32 oracle vs the CPU oracle: (loss rel err, max Detect-output rel L2, whole-grad
-    rel L2).  The forward agrees to fp32 summation order; the gradient of these networks at random init routes through
-    max-pool / CBAM argmaxes sitting on near-ties, so fp32 reordering alone moves it by 1e-3 (yolov5s) .. 1e-1 (config 5)
-    -- the reason every comparison here is against emulations run the same way, never a fixed gradient tolerance."""
+def pin_device_oracle(cfg, nc, sd, batch, hyp, dtype=torch.float64):
+    """first step of the device-run oracle vs the CPU oracle, both in float64 (default): (loss rel err, max
+    Detect-output rel L2, whole-grad rel L2).  In fp64 the two summation orders agree to ~1e-12, so this pins that the
+    device run computes the same FUNCTION as the CPU oracle (in fp32 the same comparison measured only
+    summation order, 1e-4 .. 1.6e-4 on the outputs and up to 1e-1 on the gradient through max-pool / CBAM near-ties).
+    The loss restatement (oracle/loss.py) returns fp32 whatever its inputs, so its pin is at fp32 resolution."""
     from oracle.loss import compute_loss
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     res = []
     for dev in ('cpu', 'cuda'):
-        ref = oracle_model(cfg, nc, sd, None, dev)
-        anchors = sd['model.%d.anchors' % (len(ref.model) - 1)].float().cpu()
+        ref = oracle_model(cfg, nc, sd, None, dev).to(dtype)
+        anchors = sd['model.%d.anchors' % (len(ref.model) - 1)].to(dtype).cpu()
         x, t = batch
-        pr = ref(x.to(dev).float() / 255)
+        pr = ref(x.to(dev).to(dtype) / 255)
         lo, _ = compute_loss([p.cpu() for p in pr], t, anchors, hyp, nc)
         lo.backward()
         res.append((float(lo), [p.detach().double().cpu() for p in pr],

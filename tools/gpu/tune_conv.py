@@ -40,6 +40,11 @@ SETS = {
             (1, 512, 48, 48, 512, 1, 1), (1, 128, 192, 192, 128, 3, 1), (1, 256, 96, 96, 256, 3, 1),
             (1, 64, 384, 384, 64, 3, 1), (1, 512, 48, 48, 512, 3, 1), (1, 128, 384, 384, 128, 1, 1)],
     'halo': [(32, 64, 768, 768, 64, 3, 1), (32, 64, 384, 384, 64, 3, 1), (8, 64, 256, 256, 64, 3, 1)],
+    # every >= 256-column GEMM view of DMA-YOLO-l @1536 bs32 on the 256 x 256 tiles (conv_fwd_w / conv_fwd_8p)
+    'wide': [(32, 256, 96, 96, 256, 3, 1), (32, 512, 96, 96, 512, 3, 1), (32, 1024, 48, 48, 1024, 3, 1),
+             (32, 512, 48, 48, 512, 3, 1), (32, 1024, 48, 48, 1024, 1, 1), (32, 2048, 48, 48, 1024, 1, 1),
+             (32, 512, 96, 96, 512, 1, 1), (32, 256, 96, 96, 1024, 1, 1), (32, 256, 96, 96, 768, 1, 1),
+             (32, 4096, 48, 48, 1024, 1, 1)],
     'one': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1)],
     'v5s': [(64, 128, 40, 40, 128, 3, 1), (64, 64, 80, 80, 64, 3, 1), (64, 256, 20, 20, 256, 3, 1),
             (64, 512, 20, 20, 256, 1, 1), (64, 32, 160, 160, 32, 3, 1), (64, 64, 160, 160, 32, 1, 1)],
