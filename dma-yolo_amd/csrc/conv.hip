@@ -1820,6 +1820,162 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_dgrad_s2_v3(const bf16* __r
                                     m0, n0, cls, Epi{}, BnB{});
 }
 
+// ---------------------------------------------------------------- persistent stride-2 data-grad (conv_s2p, round 5)
+// The stride-2 data-grads (SCConv's k4 and the backbone's downsampling convs, models/common.py:1303, 50-77) as four
+// parity-class GEMMs of 1, 2, 2 and 4 taps: with 128-256 dy channels a class tile has only 2-16 K steps, and the
+// one-tile-per-block kernels above spent most of each tile in the load prologue and the LDS-staged epilogue with
+// nothing in flight (357-760 TF/s on the DMA-1536 shapes, round 4).  Here the (class, row tile, column tile) units of
+// all four classes run through conv_p1p's persistent structure: one continuous LDS-DMA ring of K steps across a
+// block's units (the next unit's first stages load under this unit's last MFMAs and its epilogue), transposed MFMAs
+// (D[channel][pixel]) so a lane ends with 8 consecutive channels of one pixel, and a register epilogue that maps the
+// class row straight to its dx pixel (2 i2 + a, 2 j2 + b) with one 16-B buffer store (accumulating data-grads load
+// the previous dx vector first).  Units are dispatched class-fastest in XCD-contiguous order, so the four classes over
+// the same dy rows run together on one XCD and share its L2.
+template <int BM, int BN, int NS, int WTR>
+__global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_s2p(const bf16* __restrict__ dy,
+                                                                      const bf16* __restrict__ wt, bf16* __restrict__ dx,
+                                                                      int accumulate, Geom g, int gmax, int gn,
+                                                                      unsigned xbytes, unsigned wbytes, unsigned ybytes) {
+  using PP = P1P<BM, BN, NS, WTR>;
+  using C3_ = typename PP::C3_;
+  constexpr int PER = PP::PER, NI = PP::NI;
+  static_assert(NS == 2 || NS == 3, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * C3_::STAGE];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
+  const int q = lane >> 4, pl = lane & 15;
+  const int nunits = 4 * gmax * gn, G = gridDim.x;
+  const int kpt = g.K / BK;  // K steps per tap
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dx, ybytes);
+  // unit L (dispatch order) -> class (a, b), row tile, column tile; returns its K steps (0: no rows in this class)
+  auto unit = [&](int L, int& a, int& b, int& tm, int& tn) -> int {
+    const int u = xcd_remap(L, nunits);
+    a = (u >> 1) & 1;
+    b = u & 1;
+    const int t = u >> 2;
+    tm = t / gn;
+    tn = t % gn;
+    const int oh = (g.H - a + 1) / 2, ow = (g.W - b + 1) / 2;
+    if (oh <= 0 || ow <= 0 || (long)tm * BM >= (long)g.N * oh * ow) return 0;
+    return ((g.KH - ((a + g.P) & 1) + 1) / 2) * ((g.KW - ((b + g.P) & 1) + 1) / 2) * kpt;
+  };
+  auto view = [&](int a, int b) {  // the class's GEMM view (conv_dgrad_s2_v3)
+    Geom gv = g;
+    gv.H = g.OH; gv.W = g.OW; gv.C = g.K; gv.xps = g.yps; gv.K = g.C; gv.S = 2;
+    gv.OH = (g.H - a + 1) / 2; gv.OW = (g.W - b + 1) / 2; gv.yps = g.xps;
+    return gv;
+  };
+  using LD = FwdLdsB<BM, BN, NS, false, true, true, 2, WTR>;
+  // issue cursor: unit lL (dispatch index), its K steps lnk, step lk
+  int lL = (int)blockIdx.x, la = 0, lb = 0, ltm = 0, ltn = 0, lnk = 0, lk = 0;
+  while (lL < nunits && (lnk = unit(lL, la, lb, ltm, ltn)) == 0) lL += G;
+  if (lL >= nunits) return;
+  Geom lgv = view(la, lb);
+  LD ld(dy, wt, lgv, (long)lgv.N * lgv.OH * lgv.OW, (long)ltm * BM, ltn * BN, wid, lane, xbytes, wbytes,
+        S2Cls{la, lb, g.H, g.W});
+  int issued = 0;
+  auto issue = [&]() {
+    if (lL >= nunits) return;
+    ld.issue(smem + (issued % NS) * C3_::STAGE, wid);
+    ++issued;
+    if (++lk == lnk) {
+      lk = 0;
+      do lL += G;
+      while (lL < nunits && (lnk = unit(lL, la, lb, ltm, ltn)) == 0);
+      if (lL < nunits) {
+        lgv = view(la, lb);
+        ld = LD(dy, wt, lgv, (long)lgv.N * lgv.OH * lgv.OW, (long)ltm * BM, ltn * BN, wid, lane, xbytes, wbytes,
+                S2Cls{la, lb, g.H, g.W});
+      }
+    }
+  };
+  issue();
+  if (NS == 3) issue();
+  int s = 0, r = 0;
+  for (int L = (int)blockIdx.x; L < nunits; L += G) {
+    int a, b, tm, tn;
+    const int nk = unit(L, a, b, tm, tn);
+    if (nk == 0) continue;
+    const Geom gv = view(a, b);
+    const long M = (long)gv.N * gv.OH * gv.OW;
+    f32x4 acc[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++s) {
+      // stage s landed: younger VMEM ops allowed = the next stage (if issued) + the previous unit's epilogue stores
+      // when they were issued after stage s (kt < NS - 1 on every unit but the block's first)
+      const bool nxt = issued > s + 1;
+      const bool epi = r > 0 && kt < NS - 1;
+      if (epi && accumulate) {
+        vm_wait<0>();
+      } else if (epi) {
+        if (nxt) vm_wait<PER + PP::NST>();
+        else vm_wait<PP::NST>();
+      } else {
+        if (nxt) vm_wait<PER>();
+        else vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (issued < s + NS) issue();
+      const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
+      const bf16* Bs = As + BM * BK;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 af[NI], bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) af[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    // ---- register epilogue: acc[i][j][rr] = dX[class row m0 + wm WTR + 16 i + pl][channel n0 + wn 64 + 16 j + 4 q + rr]
+    const long mw = (long)tm * BM + wm * WTR;
+    const int nw = tn * BN + wn * 64;
+    const int chq = (q & 1) * 16 + (q >> 1) * 8;
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const long m = mw + 16 * i + pl;
+      const int j2 = (int)(m % gv.OW);
+      const long tq = m / gv.OW;
+      const int i2 = (int)(tq % gv.OH), bb = (int)(tq / gv.OH);
+      const long pix = ((long)bb * g.H + 2 * i2 + a) * g.W + 2 * j2 + b;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const f32x4 &p0 = acc[i][2 * jp], &p1 = acc[i][2 * jp + 1];
+        const int n = nw + 32 * jp + chq;
+        const unsigned off = (m < M && n < g.C) ? (unsigned)((pix * g.xps + n) * 2) : kBufOob;
+        if (accumulate) {
+          const u4 o = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+          float f[8];
+          unpack<bf16>(make_uint4(o[0], o[1], o[2], o[3]), f);
+          // this lane's 8 channels: (p0, p1) of 4 channels each, exchanged across the lane pair by the swap below --
+          // add in fp32 after the swap so the order matches the plain path
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[0], p0[1]), pk2_bf16(p1[0], p1[1]), false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[2], p0[3]), pk2_bf16(p1[2], p1[3]), false, false);
+          float v[8];
+          unpack<bf16>(make_uint4(s0[0], s1[0], s0[1], s1[1]), v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += f[e];
+          const uint4 w4 = pack<bf16>(v);
+          __builtin_amdgcn_raw_buffer_store_b128(u4{w4.x, w4.y, w4.z, w4.w}, ry, off, 0, 0);
+        } else {
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[0], p0[1]), pk2_bf16(p1[0], p1[1]), false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[2], p0[3]), pk2_bf16(p1[2], p1[3]), false, false);
+          __builtin_amdgcn_raw_buffer_store_b128(u4{s0[0], s1[0], s0[1], s1[1]}, ry, off, 0, 0);
+        }
+      }
+    }
+    ++r;
+  }
+}
+
 // ---------------------------------------------------------------- wide tile: 256 x 256 block, 128 x 64 per wave
 // Per K step a wave reads (128 + 64) x 64 bf16 from LDS for 64 MFMAs, against (64 + 64) x 64 for 32 in the
 // 64 x 64 wave tile: the LDS array (256 B/clk/CU) stops pacing the MFMAs on the MFMA-bound layers.  2 LDS stages
@@ -3910,9 +4066,13 @@ inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
-// DMY_W8P: 1 = the 256 x 256 tiles run the half-tile pipeline (v3::conv_fwd_8p), 0 = the 2-stage wide loop (conv_fwd_w)
+// DMY_W8P: which 256 x 256 tiles run the half-tile pipeline (v3::conv_fwd_8p) instead of the 2-stage wide loop
+// (conv_fwd_w): 0 none, 1 (default) the 1x1 GEMM views, 2 all.  Measured (round 5, gpurun_out/r5/ab_w8p.log, cold
+// caches, two interleaved passes): 1x1 C1024 -> K1024 @48^2 bs32 fwd 200 -> 175 us, dgrad 186 -> 161; C2048 -> K1024
+// fwd 329 -> 288; C4096 -> K1024 fwd 592 -> 526, dgrad 629 -> 595; the other 1x1 shapes and every 3x3 shape within
+// +-1.5 % (3x3 256 @96^2 fwd 411 / 414, 1024 @48^2 1167 / 1149)
 inline int w8p_mode() {
-  static const int t = env_int("DMY_W8P", 0);
+  static const int t = env_int("DMY_W8P", 1);
   return t;
 }
 // DMY_P1S = 0 off, 1 (default) the output-heavy forwards (K >= 2 C), 3 those and the output-heavy data-grads, 2 every
@@ -4218,7 +4378,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
   }
   if (tov < 0 && buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
       (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
-    if (w8p_mode() && bb.z == nullptr) {  // the half-tile pipeline (conv_fwd_8p)
+    if ((w8p_mode() == 2 || (w8p_mode() == 1 && p1)) && bb.z == nullptr) {  // the half-tile pipeline (conv_fwd_8p)
       const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 256);
       if (p1) v3::conv_fwd_8p<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
                                                                          wbytes, ep, bb);
@@ -4445,9 +4605,37 @@ inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const 
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
 }
+// DMY_S2P: 1 the stride-2 data-grads run the persistent class kernel (v3::conv_s2p), 0 (default) the one-tile kernels.
+// Built, parity-green (tests/test_gpu_conv*.py: 269 passed with it on) and measured SLOWER on every DMA-1536 shape
+// (gpurun_out/r5/ab_s2p.log, cold caches, two passes): 64 -> 128 @768^2 bs32 1997 -> 2511 us, 128 -> 256 @384^2
+// 1289 -> 1483, 256 -> 512 @192^2 947 -> 1320, 512 -> 1024 @96^2 857 -> 1244.  Its register epilogue writes each dx
+// pixel's 128-B line as two 64-B halves one instruction apart (every second pixel of a row, the class stride), the
+// store order round 4 measured at 3.3-4.1 TB/s against 5.6-5.9 for whole lines, and the persistent grid keeps one
+// 8-wave block per CU where the one-tile kernels overlap several
+inline int s2p_mode() {
+  static const int t = env_int("DMY_S2P", 0);
+  return t;
+}
 inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc, const Geom& g, hipStream_t st) {
   const unsigned xbytes = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned wbytes = (unsigned)(2.0 * g.C * g.KH * g.KW * g.K);
+  const double dxb = 2.0 * ((double)g.N * g.H * g.W * g.xps);
+  if (s2p_mode() && g.C % 64 == 0 && g.xps % 8 == 0 && dxb < (double)v3::kBufOob && aligned16(dx)) {
+    const long Mmax = (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2);  // class (0, 0) has the most rows
+    const int gmax = ceil_div(Mmax, 256);
+    if (g.C > 64) {
+      using PP = v3::P1P<256, 128, 3, 64>;
+      const int gn = ceil_div(g.C, 128), G = p1p_grid(4 * gmax * gn, 3 * PP::C3_::STAGE);
+      v3::conv_s2p<256, 128, 3, 64><<<(unsigned)G, PP::NTH, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes, wbytes,
+                                                                   (unsigned)dxb);
+    } else {
+      using PP = v3::P1P<256, 64, 2, 64>;
+      const int gn = 1, G = p1p_grid(4 * gmax * gn, 2 * PP::C3_::STAGE);
+      v3::conv_s2p<256, 64, 2, 64><<<(unsigned)G, PP::NTH, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes, wbytes,
+                                                                  (unsigned)dxb);
+    }
+    return (int)hipGetLastError();
+  }
   // DMY_S2_MERGE: 0 one launch per parity class, 1 (default) one launch for <= 64-channel data-grads, 2 always.
   // Measured (profiles/r02/ab_s2_merge.log): +4..14 % at 32 / 64 channels, 16-33 % slower on the 1-block-per-CU
   // 256 x 128 tiles of the 128 / 256-channel layers, where the per-class launches stay.

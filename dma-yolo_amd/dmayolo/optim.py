@@ -28,10 +28,14 @@ for _f in (lib.dmy_sgd, lib.dmy_adam, lib.dmy_ema, lib.dmy_amp_check, lib.dmy_am
 class _Table:
     """Device-side pointer table + (tensor, chunk) map for a list of tensors.
 
-    Tables are cached by the tensors' addresses: with the caching allocator the gradients of one
-    parameter list land at the same addresses every step, so after the first step no table is
-    rebuilt.  A new table is staged in pinned host memory and copied asynchronously -- a pageable
-    H2D copy would block the host until the GPU drained its queue (no run-ahead across steps)."""
+    One table per tensor LIST (keyed by the identity of its first list -- the parameters -- and the sizes), kept for
+    the run.  With the caching allocator the gradients of a parameter list usually land at the same addresses every
+    step; when they do not (gradients autograd assembles from slices, e.g. nn.MultiheadAttention's in_proj_weight in
+    config 5's C3TR) only the changed pointer arrays are rewritten in place -- round 4 cached a NEW table per pointer
+    set, so those models built and kept (up to 64) tables, ~190 KB of device memory a step.  A table is staged in
+    pinned host memory and copied asynchronously, stream-ordered behind the kernels that read the old pointers (a
+    pageable H2D copy would block the host until the GPU drained its queue); before its pinned buffer is rewritten
+    the previous copy's event is waited on (long complete by then)."""
     _cache = {}
 
     def __init__(self, lists, dev):
@@ -42,20 +46,41 @@ class _Table:
                 tid.append(i)
                 off.append(o)
         self.nchunks = len(tid)
-        host = [torch.tensor([t.data_ptr() for t in L], dtype=torch.int64) for L in lists]
+        self.ptrs = [tuple(t.data_ptr() for t in L) for L in lists]
+        host = [torch.tensor(list(pl), dtype=torch.int64) for pl in self.ptrs]
         host += [torch.tensor(n, dtype=torch.int64), torch.tensor(tid, dtype=torch.int32),
                  torch.tensor(off, dtype=torch.int64)]
         self.pinned = [h.pin_memory() for h in host]  # kept alive with the cached table
         self.dev = [h.to(dev, non_blocking=True) for h in self.pinned]
+        self.ev = torch.cuda.Event() if torch.device(dev).type == 'cuda' else None
+        if self.ev is not None:
+            self.ev.record()
+
+    def refresh(self, lists):
+        for i, L in enumerate(lists):
+            pl = tuple(t.data_ptr() for t in L)
+            if pl == self.ptrs[i]:
+                continue
+            if self.ev is not None:
+                self.ev.synchronize()  # the previous async copy out of this pinned buffer has finished
+            self.pinned[i].copy_(torch.tensor(list(pl), dtype=torch.int64))
+            self.dev[i].copy_(self.pinned[i], non_blocking=True)
+            self.ptrs[i] = pl
+            if self.ev is not None:
+                self.ev.record()
 
     @classmethod
-    def get(cls, lists, dev):
-        key = (str(dev),) + tuple(tuple(t.data_ptr() for t in L) for L in lists) + (tuple(t.numel() for t in lists[0]),)
+    def get(cls, lists, dev, ident=None):
+        """ident: the tensors whose identity names the table (default lists[0])"""
+        ident = lists[0] if ident is None else ident
+        key = (str(dev), len(lists), tuple(id(t) for t in ident), tuple(t.numel() for t in lists[0]))
         tb = cls._cache.get(key)
         if tb is None:
-            if len(cls._cache) > 64:
+            if len(cls._cache) > 256:
                 cls._cache.clear()
             tb = cls._cache[key] = cls(lists, dev)
+        else:
+            tb.refresh(lists)
         return tb
 
     def p(self, i):
@@ -203,9 +228,10 @@ class GradScaler:
     def step(self, optimizer):
         if not self.enabled:
             return optimizer.step()
-        gs = [p.grad for g in optimizer.param_groups for p in g['params'] if p.grad is not None]
+        ps = [p for g in optimizer.param_groups for p in g['params'] if p.grad is not None]
+        gs = [p.grad for p in ps]
         if gs:
-            tb = _Table.get([gs], gs[0].device)
+            tb = _Table.get([gs], gs[0].device, ident=ps)
             _check(lib.dmy_amp_check(tb.p(0), tb.p(1), tb.p(2), tb.p(3), tb.nchunks, ctypes.c_void_p(self.scale.data_ptr()),
                                      ctypes.c_void_p(self.found.data_ptr()), stream()), 'dmy_amp_check')
         optimizer._amp = (self.scale, self.found)

@@ -138,10 +138,14 @@ def test_model_ema_matches_reference():
             assert torch.equal(g.to(v.dtype), v), k
 
 
-def test_trainer_steady_state_reuses_pointer_tables():
+@pytest.mark.parametrize('yml', ['yolov5n.yaml', 'yolov5l-xs-tr-cbam-spp-bifpn.yaml'])
+def test_trainer_steady_state_reuses_pointer_tables(yml):
     """Every gradient the conv path produces (weights, BN gamma / beta, conv biases) is a slice of the per-forward
     gradient arena, so after the first steps the optimizer / scaler / EMA pointer tables are cache hits: no
-    per-step host tensor pinning or H2D table uploads (they showed up as ~100 runtime copy kernels per step)."""
+    per-step host tensor pinning or H2D table uploads (they showed up as ~100 runtime copy kernels per step).  Config
+    5 (C3TR: nn.MultiheadAttention's in_proj_weight gradient is assembled by autograd from three slices, at addresses
+    that move between steps) refreshes its tables in place instead of building new ones (round 5; round 4 cached a
+    new table per pointer set: ~190 KB of device memory per step)."""
     import os
     from dmayolo import optim
     from dmayolo.models.yolo import Model
@@ -149,7 +153,7 @@ def test_trainer_steady_state_reuses_pointer_tables():
     from dmayolo.synthetic import images, targets, HYP_VISDRONE, scaled_hyp
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     torch.manual_seed(0)
-    m = Model(os.path.join(root, 'dma-yolo_amd', 'dmayolo', 'configs', 'yolov5n.yaml'), nc=10).cuda()
+    m = Model(os.path.join(root, 'dma-yolo_amd', 'dmayolo', 'configs', yml), nc=10).cuda()
     m.hyp = scaled_hyp(HYP_VISDRONE, 10, 256)
     tr = Trainer(m, m.hyp, 64, nb=100)
     x, t = images(4, 256, device='cuda'), targets(4, 10, device='cuda')

@@ -40,6 +40,10 @@ SETS = {
             (1, 512, 48, 48, 512, 1, 1), (1, 128, 192, 192, 128, 3, 1), (1, 256, 96, 96, 256, 3, 1),
             (1, 64, 384, 384, 64, 3, 1), (1, 512, 48, 48, 512, 3, 1), (1, 128, 384, 384, 128, 1, 1)],
     'halo': [(32, 64, 768, 768, 64, 3, 1), (32, 64, 384, 384, 64, 3, 1), (8, 64, 256, 256, 64, 3, 1)],
+    # the stride-2 layers of DMA-YOLO-l @1536 bs32 (SCConv k4 and the downsampling convs) and of yolov5s @640 bs64
+    's2dma': [(32, 64, 768, 768, 128, 3, 2), (32, 128, 384, 384, 256, 3, 2), (32, 256, 192, 192, 512, 3, 2),
+              (32, 512, 96, 96, 1024, 3, 2), (32, 256, 192, 192, 256, 3, 2), (64, 32, 320, 320, 64, 3, 2),
+              (64, 64, 160, 160, 128, 3, 2), (64, 128, 80, 80, 256, 3, 2), (64, 256, 40, 40, 512, 3, 2)],
     # every >= 256-column GEMM view of DMA-YOLO-l @1536 bs32 on the 256 x 256 tiles (conv_fwd_w / conv_fwd_8p)
     'wide': [(32, 256, 96, 96, 256, 3, 1), (32, 512, 96, 96, 512, 3, 1), (32, 1024, 48, 48, 1024, 3, 1),
              (32, 512, 48, 48, 512, 3, 1), (32, 1024, 48, 48, 1024, 1, 1), (32, 2048, 48, 48, 1024, 1, 1),
