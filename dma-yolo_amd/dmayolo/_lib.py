@@ -39,6 +39,9 @@ SIGNATURES = {
     'dmy_conv_wgrad_ws_elems': [I, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I],
     'dmy_conv_wgrad_det': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L, I, P, L, P],
     'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
+    # bwd1x1.hip
+    'dmy_conv1x1_bwd_bn_ok': [L, I, I, L, L, L, P, P, P, P],
+    'dmy_conv1x1_bwd_bn': [P, L, P, P, L, P, P, P, P, P, I, P, P, P, P, L, I, P, L, I, I, P],
     # augment.hip
     'dmy_aug_desc_bytes': [],
     'dmy_augment_batch': [P, I, P, I, I, P],
@@ -169,7 +172,7 @@ lib = _load()
 
 def call(name, *args):
     rc = getattr(lib, name)(*args)
-    if name.endswith(('_rows', '_blocks', '_groups', '_bytes', '_elems')):
+    if name.endswith(('_rows', '_blocks', '_groups', '_bytes', '_elems', '_ok')):
         return rc
     if rc != 0:
         raise RuntimeError(f'{name} failed with hipError {rc}')

@@ -118,6 +118,11 @@ class GradSink:
             return self.buf, C, 0
         return self.buf, self.ps, 1
 
+    def peek(self, N, C, H, W):
+        """(buffer, pixel stride) a target() call would return now without allocating, or None when it would
+        allocate a fresh dense buffer"""
+        return (self.buf, self.ps) if self.buf is not None else None
+
     def done(self):
         return self._tick()
 
@@ -559,6 +564,37 @@ DEFER_AFFINE = [os.environ.get('DMY_DEFER_AFFINE', '1') == '1']
 BWD_COLSUM = [os.environ.get('DMY_BWD_COLSUM', '1') == '1']
 
 
+# fused 1x1 backward (bwd1x1.hip): BN apply + data-grad + weight-grad of a train-mode 1x1 Conv-BN-act layer in one
+# launch, dz never stored.  DMY_BWD1X1=0 restores the three-pass path (A/B, parity tests)
+BWD1X1 = [os.environ.get('DMY_BWD1X1', '1') == '1']
+
+
+def _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc, N, C, H, W, K, k, s, p, M):
+    """-> (dx, dw) when the fused kernel took the layer's apply + data-grad + weight-grad, else None.  Eligible: bf16
+    storage, train-mode BN, 1x1 stride 1, both gradients wanted, not deterministic mode (its fp32 weight-grad atomics
+    are unordered), no producer-BN reduce link, a (K, C) pair the kernel is built for (dmy_conv1x1_bwd_bn_ok)."""
+    if not (BWD1X1[0] and ctx.train_bn and k == 1 and s == 1 and p == 0 and not ctx.s2d and ctx.cp == C and
+            dy.dtype == torch.bfloat16 and wt is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and
+            not DETERMINISTIC[0] and not (ctx.link_in is not None and FUSE_BN_REDUCE[0])):
+        return None
+    buf_probe = ctx.xsink.peek(N, C, H, W) if ctx.xsink is not None else None
+    bps_probe = buf_probe[1] if buf_probe is not None else C
+    if not call('dmy_conv1x1_bwd_bn_ok', M, K, C, dps, xps, bps_probe, ptr(dy), ptr(z), ptr(x),
+                ptr(buf_probe[0]) if buf_probe is not None else ptr(z)):
+        return None
+    dev = dy.device
+    buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
+    dw = ctx.arena.take(ctx.wkey, (K, C, 1, 1)) if ctx.arena is not None else None
+    if dw is None:
+        dw = torch.zeros((K, C, 1, 1), dtype=torch.float32, device=dev)
+    es = z.element_size()
+    KernelTimer.run('conv_bwd1x1', 4.0 * M * K * C, 'dmy_conv1x1_bwd_bn', ptr(dy), dps, ptr(z), ptr(x), xps, ptr(wt),
+                    ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ctx.spec.act, ptr(ca), ptr(cb), ptr(cc), ptr(buf),
+                    bps, acc, ptr(dw), M, K, C, stream(), tag=(N, C, H, W, K, k, s),
+                    nbytes=es * (2 * M * K + (2 + acc) * M * C + K * C) + 4 * K * C)
+    return sink_result(ctx.xsink, buf), dw
+
+
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None, grad_on=True):
@@ -783,6 +819,13 @@ class ConvBNActFn(torch.autograd.Function):
                 ca.copy_(scale)
                 cb.zero_()
                 cc.zero_()
+            fused = _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc, N, C, H, W, K, k, s,
+                            p, M)
+            if fused is not None:
+                dx, dw = fused
+                dbias = pgrad(ctx.pkeys[0], zero=True) if ctx.has_bias else None  # sum(dz) == 0 behind train-mode BN
+                dres = (dy if ctx.rsink is None else ctx.rsink.passthrough(dy)) if ctx.has_res else None
+                return dx, dw, dbias, dgamma, dbeta, dres, None, None, None, None
             call('dmy_bn_bwd_apply', dt, ptr(z), K, ptr(dy), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd),
                  spec.act, ptr(ca), ptr(cb), ptr(cc), ptr(dz), K, M, K, stream())
             dzps = K

@@ -66,6 +66,18 @@ int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* w_ihwo, void* dx, i
                       float* pdb, float* pdg, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
                    int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
+/* bwd1x1.hip: fused backward of a train-mode 1x1 stride-1 Conv -> BatchNorm -> act (models/common.py:67-73, k = 1),
+ * bf16: dz = dmy_bn_bwd_apply's value on (dy, z) in registers (never stored), then dx (+)= dz Wt and dw += dz^T x in
+ * one persistent launch.  Replaces dmy_bn_bwd_apply + dmy_conv_dgrad + dmy_conv_wgrad_ex(OIHW) of such a layer; the
+ * reduce / finalize that produce ca, cb, cc run before it as before.  x / dx / dy: [M][C] / [M][C] / [M][K] rows of
+ * pixel stride xps / bps / dps; z dense [M][K]; wt = the IHWO copy [C][K]; dw fp32 [K][C], ACCUMULATED (the caller
+ * zeroes it).  _ok: 1 when this shape / alignment is supported (else the call returns -1 and launches nothing). */
+int dmy_conv1x1_bwd_bn_ok(long M, int K, int C, long dps, long xps, long bps, const void* dy, const void* z,
+                          const void* x, const void* dx);
+int dmy_conv1x1_bwd_bn(const void* dy, long dps, const void* z, const void* x, long xps, const void* wt,
+                       const float* scale, const float* shift, const float* mean, const float* invstd, int act,
+                       const float* ca, const float* cb, const float* cc, void* dx, long bps, int accumulate,
+                       float* dw, long M, int K, int C, void* stream);
 /* flags: 1 = write dw in torch OIHW order (the parameter's .grad layout, no wgrad_to_oihw pass; needs Cp == C),
  *        2 = dw is already zero (a per-step gradient arena cleared once), skip the memset.  Same sums as above. */
 int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C, long xps, int K,

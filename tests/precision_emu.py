@@ -55,7 +55,9 @@ class RoundGrad(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, dt):
         ctx.dt = dt
-        return x.view_as(x)
+        # a copy, not x.view_as(x): a module that updates its input in place (the C3TR transformer's residual adds)
+        # may not modify a view created inside a custom Function
+        return x.clone()
 
     @staticmethod
     def backward(ctx, g):
