@@ -21,9 +21,10 @@
 //   * Weight-grad: dW[k][c] += sum_px dz[px][k] x[px][c], both operands read transposed from LDS
 //     (ds_read_b64_tr_b16); each wave owns a (K/2) x (C/2) block of fp32 accumulators for the whole launch and adds it
 //     to dw with fp32 atomics at the end (dw is the caller-zeroed arena slice, OIHW = [K][C] for a 1x1).
-// Shapes: (K, C) in {(64, 64), (128, 64), (64, 128), (128, 128), (128, 256)} (K * C <= 32768: Wt + the two tiles fit
-// the LDS and the weight-grad accumulators fit the registers; see tile_px), 16-B aligned pixel strides; the host query
-// dmy_conv1x1_bwd_bn_ok says which, everything else keeps the three-pass path.
+// Shapes: the (K, C) pairs of plan() (K in {64, 128, 256}, C <= 512; Wt + the two tiles fit the LDS and the
+// weight-grad accumulators fit the registers, with the dx channels split over 2 blocks per tile where one block's would
+// not), 16-B aligned pixel strides; the host query dmy_conv1x1_bwd_bn_ok says which, everything else keeps the
+// three-pass path.
 #include "common.h"
 
 namespace {
@@ -74,37 +75,49 @@ DEV unsigned pk2(float a, float b) {
          ((unsigned)*reinterpret_cast<const unsigned short*>(&y) << 16);
 }
 
-template <int K, int C, int TP>
+// K = dz channels, CB = the block's slice of dx channels (C / nsplit), TP = pixels per tile, PX = 16-pixel tiles per
+// data-grad unit (a unit = 16 PX pixels x 64 channels)
+template <int K, int CB, int TP, int PX>
 struct Shape {
-  static constexpr int NT = 256, KCH = K / 8, CCH = C / 8;
+  static constexpr int NT = 256, KCH = K / 8, CCH = CB / 8;
   static constexpr int NDZ = TP * KCH / NT, NX = TP * CCH / NT;  // 16-B chunks per thread and tile (dy / z, x)
   static constexpr int RDZ = NT / KCH, RXS = NT / CCH;            // pixel rows between a thread's chunks
-  static constexpr int KW = K / 2, CW = C / 2, MI = KW / 16, NJ = CW / 16;  // weight-grad block of a wave (2 x 2)
-  static constexpr int PGN = TP / 32, U = PGN * (C / 64), UPW = U / 4;     // data-grad units (32 px x 64 ch)
-  static constexpr int LDS = (C * K + TP * K + TP * C) * 2;
-  static_assert(K % 64 == 0 && C % 64 == 0 && NT % KCH == 0 && NT % CCH == 0, "channels");
-  static_assert(NDZ >= 1 && NX >= 1 && TP % 32 == 0 && U % 4 == 0, "tile");
+  static constexpr int KW = K / 2, CW = CB / 2, MI = KW / 16, NJ = CW / 16;  // weight-grad block of a wave (2 x 2)
+  static constexpr int PGN = TP / (16 * PX), U = PGN * (CB / 64), UPW = U / 4;  // data-grad units
+  static constexpr int LDS = (CB * K + TP * K + TP * CB) * 2;
+  static_assert(K % 64 == 0 && CB % 64 == 0 && NT % KCH == 0 && NT % CCH == 0, "channels");
+  static_assert(NDZ >= 1 && NX >= 1 && TP % 32 == 0 && TP % (16 * PX) == 0 && U % 4 == 0, "tile");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <int K, int C, int TP>
+// nsplit > 1 (layers whose Wt or weight-grad accumulators do not fit one block): the dx channels are split over nsplit
+// blocks, each with its own slice of Wt, x, dx and dw, all computing the tile's whole dz (the transform runs nsplit
+// times, dy / z are read once from HBM and nsplit - 1 times from L2).  Blocks b and b + 8 share an XCD (dispatch is
+// round-robin over the 8 XCDs), so the nsplit blocks of one tile group are placed 8 apart and walk the same tiles.
+template <int K, int CB, int TP, int PX>
 __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
     const bf16* __restrict__ dy, long dps, const bf16* __restrict__ z, const bf16* __restrict__ x, long xps,
     const bf16* __restrict__ wt, const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd, int act, const float* __restrict__ ca,
     const float* __restrict__ cb, const float* __restrict__ cc, bf16* __restrict__ dx, long bps, int accumulate,
-    float* __restrict__ dw, long M, int ntiles, unsigned dyb, unsigned zb, unsigned xb) {
-  using S = Shape<K, C, TP>;
+    float* __restrict__ dw, long M, int ntiles, int C, int nsplit, unsigned dyb, unsigned zb, unsigned xb) {
+  using S = Shape<K, CB, TP, PX>;
   extern __shared__ __attribute__((aligned(16))) char b1_smem[];
-  bf16* ws = reinterpret_cast<bf16*>(b1_smem);  // Wt [C][K]
-  bf16* dzs = ws + C * K;                        // dz tile [TP][K]
-  bf16* xs = dzs + TP * K;                       // x tile [TP][C]
+  bf16* ws = reinterpret_cast<bf16*>(b1_smem);  // the block's Wt rows [CB][K]
+  bf16* dzs = ws + CB * K;                       // dz tile [TP][K]
+  bf16* xs = dzs + TP * K;                       // x tile [TP][CB]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, il = lane & 15;
+  const int slot = blockIdx.x >> 3, cs = slot % nsplit;
+  const int grp = (blockIdx.x & 7) + 8 * (slot / nsplit), ngrp = gridDim.x / nsplit;
+  const int cbase = cs * CB;  // first dx channel of this block
+  x += cbase;
+  dx += cbase;
+  dw += cbase;
 
-  for (int e = tid; e < C * S::KCH; e += S::NT) {
+  for (int e = tid; e < CB * S::KCH; e += S::NT) {
     const int r = e / S::KCH, ch = e % S::KCH;
     *reinterpret_cast<uint4*>(ws + r * K + (wsw<K>(r, ch) << 3)) =
-        *reinterpret_cast<const uint4*>(wt + (long)r * K + ch * 8);
+        *reinterpret_cast<const uint4*>(wt + (long)(cbase + r) * K + ch * 8);
   }
 
   // this thread's fixed 8-channel chunk of dz, and dmy_bn_bwd_apply's coefficients for it:
@@ -127,7 +140,8 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
     }
   }
 
-  const __amdgpu_buffer_rsrc_t rdy = rsrc(dy, dyb), rz = rsrc(z, zb), rx = rsrc(x, xb);
+  // x's descriptor starts at the block's channel slice: the record count shrinks by the same bytes
+  const __amdgpu_buffer_rsrc_t rdy = rsrc(dy, dyb), rz = rsrc(z, zb), rx = rsrc(x, xb - 2u * cbase);
   uint4 pg[S::NDZ], pz[S::NDZ], pxv[S::NX];
   auto issue = [&](int t) {
     const long m0 = (long)t * TP;
@@ -153,10 +167,10 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
   const int wk = wid >> 1, wc = wid & 1;
   const int chq = (g & 1) * 16 + (g >> 1) * 8;  // this lane's 8 channels of a 32-channel pair after the permlane swap
 
-  int t = blockIdx.x;
+  int t = grp;
   if (t < ntiles) issue(t);
   __syncthreads();  // Wt in LDS
-  for (; t < ntiles; t += gridDim.x) {
+  for (; t < ntiles; t += ngrp) {
     const long m0 = (long)t * TP;
 #pragma unroll
     for (int j = 0; j < S::NDZ; ++j) {
@@ -176,18 +190,18 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
       *reinterpret_cast<uint4*>(dzs + ksw<K>(tid / S::KCH + j * S::RDZ, kc8)) = pg[j];
 #pragma unroll
     for (int j = 0; j < S::NX; ++j)
-      *reinterpret_cast<uint4*>(xs + ksw<C>(tid / S::CCH + j * S::RXS, xc8)) = pxv[j];
+      *reinterpret_cast<uint4*>(xs + ksw<CB>(tid / S::CCH + j * S::RXS, xc8)) = pxv[j];
     __syncthreads();
 
     // the stored dx of an accumulating data-grad: loaded before the next tile's prefetch so waiting for them does not
     // wait for the prefetch (one in-order vmcnt)
-    uint4 old[S::UPW][2][2];
+    uint4 old[S::UPW][PX][2];
     if (accumulate) {
 #pragma unroll
       for (int s = 0; s < S::UPW; ++s) {
-        const int u = wid + 4 * s, p0 = (u % S::PGN) * 32, c0 = (u / S::PGN) * 64;
+        const int u = wid + 4 * s, p0 = (u % S::PGN) * 16 * PX, c0 = (u / S::PGN) * 64;
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
+        for (int pt = 0; pt < PX; ++pt) {
           const long m = m0 + p0 + pt * 16 + il;
 #pragma unroll
           for (int h = 0; h < 2; ++h)
@@ -196,34 +210,34 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
         }
       }
     }
-    if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x);
+    if (t + ngrp < ntiles) issue(t + ngrp);
 
     // data-grad units
 #pragma unroll
     for (int s = 0; s < S::UPW; ++s) {
-      const int u = wid + 4 * s, p0 = (u % S::PGN) * 32, c0 = (u / S::PGN) * 64;
-      f32x4 acc[4][2];
+      const int u = wid + 4 * s, p0 = (u % S::PGN) * 16 * PX, c0 = (u / S::PGN) * 64;
+      f32x4 acc[4][PX];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) acc[ct][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+        for (int pt = 0; pt < PX; ++pt) acc[ct][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
       for (int kc = 0; kc < K / 32; ++kc) {
-        bf16x8 b[2];
+        bf16x8 b[PX];
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
+        for (int pt = 0; pt < PX; ++pt)
           b[pt] = *reinterpret_cast<const bf16x8*>(dzs + ksw<K>(p0 + pt * 16 + il, kc * 32 + 8 * g));
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
           const int r = c0 + ct * 16 + il;
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(ws + r * K + (wsw<K>(r, kc * 4 + g) << 3));
 #pragma unroll
-          for (int pt = 0; pt < 2; ++pt)
+          for (int pt = 0; pt < PX; ++pt)
             acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[pt], acc[ct][pt], 0, 0, 0);
         }
       }
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
+      for (int pt = 0; pt < PX; ++pt) {
         const long m = m0 + p0 + pt * 16 + il;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // channels c0 + 32 h .. + 32: the two halves of the pixel's 128-B line
@@ -248,7 +262,7 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
       }
     }
 
-    // weight-grad: this wave's (K / 2) x (C / 2) block over the tile's pixels (rows past M are zero in xs)
+    // weight-grad: this wave's (K / 2) x (CB / 2) block over the tile's pixels (rows past M are zero in xs)
 #pragma unroll
     for (int ps = 0; ps < TP / 32; ++ps) {
       bf16x8 a[S::MI];
@@ -256,7 +270,7 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
       for (int i = 0; i < S::MI; ++i) a[i] = frag_t<K>(dzs, wk * S::KW + i * 16, ps * 32, lane);
 #pragma unroll
       for (int j = 0; j < S::NJ; ++j) {
-        const bf16x8 b = frag_t<C>(xs, wc * S::CW + j * 16, ps * 32, lane);
+        const bf16x8 b = frag_t<CB>(xs, wc * S::CW + j * 16, ps * 32, lane);
 #pragma unroll
         for (int i = 0; i < S::MI; ++i)
           wacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, wacc[i][j], 0, 0, 0);
@@ -283,40 +297,49 @@ int num_cus() {
   return n;
 }
 
-// (K, C) -> pixels per tile; 0 = unsupported.  TP keeps >= 4 data-grad units (one per wave) and the LDS <= 160 KiB.
-// K = 256 (with C = 128 or 256: 128-256 weight-grad accumulator registers per lane) was built and measured: 49 / 106
-// spilled VGPRs, 0.42-0.68x the three launches (gpurun_out/r5/ab_b1a.log), so those layers keep the three-pass path
-constexpr int tile_px(int K, int C) {
-  return (K == 64 && C == 64) ? 128 : (K == 128 && C == 64) ? 128 : (K == 64 && C == 128) ? 64
-       : (K == 128 && C == 128) ? 64 : (K == 128 && C == 256) ? 64 : 0;
+// the configurations built, (K, C) -> (dx channels per block CB, pixels per tile TP, 16-px tiles per data-grad unit
+// PX).  CB = C: one block per tile; CB < C: C / CB blocks per tile (column split).  K = 256 on one block per tile (C =
+// 128 / 256: 128-256 weight-grad accumulator registers per lane) was measured at 0.42-0.68x the three launches with
+// 49 / 106 spilled VGPRs (profiles/r05/bwd1x1_ab_v1.log)
+struct Plan {
+  int cb, tp, px;
+};
+constexpr Plan plan(int K, int C) {
+  return (K == 64 && C == 64) ? Plan{64, 128, 2} : (K == 128 && C == 64) ? Plan{64, 128, 2}
+       : (K == 64 && C == 128) ? Plan{128, 64, 2} : (K == 128 && C == 128) ? Plan{128, 64, 2}
+       : (K == 128 && C == 256) ? Plan{256, 64, 2} : (K == 128 && C == 512) ? Plan{256, 64, 2}
+       : (K == 256 && C == 256) ? Plan{128, 32, 1} : (K == 256 && C == 128) ? Plan{128, 32, 1}
+       : Plan{0, 0, 0};
 }
 
 template <int K, int C>
 int launch(const bf16* dy, long dps, const bf16* z, const bf16* x, long xps, const bf16* wt, const float* scale,
            const float* shift, const float* mean, const float* invstd, int act, const float* ca, const float* cb,
            const float* cc, bf16* dx, long bps, int acc, float* dw, long M, hipStream_t st) {
-  constexpr int TP = tile_px(K, C);
-  using S = Shape<K, C, TP>;
+  constexpr Plan pl = plan(K, C);
+  constexpr int CB = pl.cb, TP = pl.tp, PX = pl.px, NS = C / CB;
+  using S = Shape<K, CB, TP, PX>;
   static bool raised = false;
   if (!raised) {
-    (void)hipFuncSetAttribute((const void*)conv1x1_bwd_bn<K, C, TP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              S::LDS);
+    (void)hipFuncSetAttribute((const void*)conv1x1_bwd_bn<K, CB, TP, PX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     raised = true;
   }
   const int ntiles = ceil_div(M, TP);
-  const int grid = ntiles < num_cus() ? ntiles : num_cus();
-  conv1x1_bwd_bn<K, C, TP><<<grid, 256, S::LDS, st>>>(
-      dy, dps, z, x, xps, wt, scale, shift, mean, invstd, act, ca, cb, cc, dx, bps, acc, dw, M, ntiles,
+  // whole XCD groups of NS blocks; no more groups than tiles
+  int ngrp = num_cus() / NS;
+  if (ngrp > ntiles) ngrp = (ntiles + 7) / 8 * 8;
+  conv1x1_bwd_bn<K, CB, TP, PX><<<ngrp * NS, 256, S::LDS, st>>>(
+      dy, dps, z, x, xps, wt, scale, shift, mean, invstd, act, ca, cb, cc, dx, bps, acc, dw, M, ntiles, C, NS,
       (unsigned)(2.0 * (double)M * dps), (unsigned)(2.0 * (double)M * K), (unsigned)(2.0 * (double)M * xps));
   return (int)hipGetLastError();
 }
-
 }  // namespace b1
 }  // namespace
 
 DMY_API int dmy_conv1x1_bwd_bn_ok(long M, int K, int C, long dps, long xps, long bps, const void* dy, const void* z,
                                   const void* x, const void* dx) {
-  if (b1::tile_px(K, C) == 0 || M <= 0) return 0;
+  if (b1::plan(K, C).cb == 0 || M <= 0) return 0;
   if (dps % 8 || xps % 8 || bps % 8 || dps < K || xps < C || bps < C) return 0;
   for (const void* p : {dy, z, x, dx})
     if (((uintptr_t)p & 15) != 0) return 0;
@@ -341,6 +364,9 @@ DMY_API int dmy_conv1x1_bwd_bn(const void* dy, long dps, const void* z, const vo
   B1_GO(64, 128)
   B1_GO(128, 128)
   B1_GO(128, 256)
+  B1_GO(128, 512)
+  B1_GO(256, 128)
+  B1_GO(256, 256)
 #undef B1_GO
   return -1;
 }

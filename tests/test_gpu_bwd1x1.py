@@ -11,7 +11,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-PAIRS = [(64, 64), (128, 64), (64, 128), (128, 128), (128, 256)]
+PAIRS = [(64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (128, 512), (256, 128), (256, 256)]
 
 
 def _rel(a, b):
@@ -75,7 +75,7 @@ def test_bwd1x1_unsupported_shapes_launch_nothing():
     t = torch.zeros(64, 96, dtype=torch.bfloat16, device='cuda')
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 96, 64, 96, 64, 64, ptr(t), ptr(t), ptr(t), ptr(t)) == 0  # K = 96
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 512, 512, 512, 512, 512, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
-    assert call('dmy_conv1x1_bwd_bn_ok', 64, 256, 256, 256, 256, 256, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
+    assert call('dmy_conv1x1_bwd_bn_ok', 64, 256, 512, 256, 512, 512, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 64, 64, 68, 64, 64, ptr(t), ptr(t), ptr(t), ptr(t)) == 0  # dps % 8
     with pytest.raises(RuntimeError, match='hipError -1'):
         call('dmy_conv1x1_bwd_bn', ptr(t), 64, ptr(t), ptr(t), 64, ptr(t), None, None, None, None, 1, None, None, None,
@@ -99,7 +99,8 @@ def _module_grads(mod, x, gup, fused):
 
 @pytest.mark.parametrize('kind,c1,c2,hw,bs', [('conv', 128, 128, 48, 8), ('conv', 256, 128, 40, 6),
                                               ('conv', 128, 256, 33, 7), ('c3', 128, 128, 40, 4),
-                                              ('c3', 256, 256, 24, 4)])
+                                              ('c3', 256, 256, 24, 4), ('conv', 512, 128, 40, 4),
+                                              ('conv', 256, 256, 30, 5)])
 def test_module_backward_fused_equals_three_pass(kind, c1, c2, hw, bs):
     """the same module, the same bf16 input and upstream gradient: the fused backward against the three-pass path
     (both product kernels): input gradient to one bf16 rounding of reordered sums, parameter gradients to fp32 order"""

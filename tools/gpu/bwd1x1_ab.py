@@ -15,7 +15,7 @@ from dmayolo.functional import call, ptr, stream  # noqa: E402
 from tune_conv import bench_cold  # noqa: E402
 
 # (N, C = fwd in = dx channels, H, W, K = fwd out = dz channels)
-SHAPES = [(32, 256, 96, 96, 256), (32, 128, 192, 192, 128), (32, 64, 384, 384, 64), (32, 128, 384, 384, 64),
+SHAPES = [(32, 512, 192, 192, 128), (32, 256, 96, 96, 256), (32, 128, 192, 192, 128), (32, 64, 384, 384, 64), (32, 128, 384, 384, 64),
           (32, 256, 192, 192, 128), (32, 256, 192, 192, 256), (32, 128, 384, 384, 128), (32, 128, 192, 192, 256),
           (64, 64, 160, 160, 64), (64, 128, 80, 80, 128), (64, 256, 40, 40, 256), (64, 128, 80, 80, 64)]
 
