@@ -83,10 +83,10 @@ struct Shape {
   static constexpr int NDZ = TP * KCH / NT, NX = TP * CCH / NT;  // 16-B chunks per thread and tile (dy / z, x)
   static constexpr int RDZ = NT / KCH, RXS = NT / CCH;            // pixel rows between a thread's chunks
   static constexpr int KW = K / 2, CW = CB / 2, MI = KW / 16, NJ = CW / 16;  // weight-grad block of a wave (2 x 2)
-  static constexpr int PGN = TP / (16 * PX), U = PGN * (CB / 64), UPW = U / 4;  // data-grad units
+  static constexpr int PGN = TP / (16 * PX), U = PGN * (CB / 64), UPW = (U + 3) / 4;  // data-grad units
   static constexpr int LDS = (CB * K + TP * K + TP * CB) * 2;
   static_assert(K % 64 == 0 && CB % 64 == 0 && NT % KCH == 0 && NT % CCH == 0, "channels");
-  static_assert(NDZ >= 1 && NX >= 1 && TP % 32 == 0 && TP % (16 * PX) == 0 && U % 4 == 0, "tile");
+  static_assert(NDZ >= 1 && NX >= 1 && TP % 32 == 0 && TP % (16 * PX) == 0 && U >= 1, "tile");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -100,7 +100,8 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
     const bf16* __restrict__ wt, const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd, int act, const float* __restrict__ ca,
     const float* __restrict__ cb, const float* __restrict__ cc, bf16* __restrict__ dx, long bps, int accumulate,
-    float* __restrict__ dw, long M, int ntiles, int C, int nsplit, unsigned dyb, unsigned zb, unsigned xb) {
+    float* __restrict__ dw, float* __restrict__ dws, long M, int ntiles, int C, int nsplit, unsigned dyb, unsigned zb,
+    unsigned xb) {
   using S = Shape<K, CB, TP, PX>;
   extern __shared__ __attribute__((aligned(16))) char b1_smem[];
   bf16* ws = reinterpret_cast<bf16*>(b1_smem);  // the block's Wt rows [CB][K]
@@ -200,6 +201,7 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
 #pragma unroll
       for (int s = 0; s < S::UPW; ++s) {
         const int u = wid + 4 * s, p0 = (u % S::PGN) * 16 * PX, c0 = (u / S::PGN) * 64;
+        if (u >= S::U) break;
 #pragma unroll
         for (int pt = 0; pt < PX; ++pt) {
           const long m = m0 + p0 + pt * 16 + il;
@@ -216,6 +218,7 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
 #pragma unroll
     for (int s = 0; s < S::UPW; ++s) {
       const int u = wid + 4 * s, p0 = (u % S::PGN) * 16 * PX, c0 = (u / S::PGN) * 64;
+      if (u >= S::U) break;  // fewer units than waves (narrow column slices): the idle waves go on to the weight-grad
       f32x4 acc[4][PX];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
@@ -277,14 +280,32 @@ __global__ void __launch_bounds__(256, 1) conv1x1_bwd_bn(
       }
     }
   }
-  // lane (g, il) holds dW[k = .. + 4 g + r][c = .. + il]: 16 consecutive floats per (g, r)
+  // lane (g, il) holds dW[k = .. + 4 g + r][c = .. + il]: 16 consecutive floats per (g, r).  fp32 atomics into dw, or
+  // (deterministic mode, dws != null) the block's partial [K][CB] in its own workspace slot, summed in block order by
+  // wgrad_slots_reduce: the tiles a block walks are fixed by its id, so every partial is run-to-run identical
+  float* part = dws != nullptr ? dws + (long)blockIdx.x * K * CB : nullptr;
 #pragma unroll
   for (int i = 0; i < S::MI; ++i)
 #pragma unroll
     for (int j = 0; j < S::NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        atomicAdd(dw + (long)(wk * S::KW + i * 16 + 4 * g + r) * C + wc * S::CW + j * 16 + il, wacc[i][j][r]);
+      for (int r = 0; r < 4; ++r) {
+        const int kk = wk * S::KW + i * 16 + 4 * g + r, c = wc * S::CW + j * 16 + il;
+        if (part != nullptr) part[kk * CB + c] = wacc[i][j][r];
+        else atomicAdd(dw + (long)kk * C + c, wacc[i][j][r]);
+      }
+}
+
+// deterministic mode: dw[k][c] += sum over the blocks b holding channel slice c / CB, in increasing b, of their slots
+__global__ void __launch_bounds__(256) wgrad_slots_reduce(const float* __restrict__ dws, float* __restrict__ dw, int K,
+                                                          int C, int CB, int nblocks, int nsplit) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)K * C) return;
+  const int k = (int)(e / C), c = (int)(e % C), cs = c / CB, cl = c % CB;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b)
+    if (((b >> 3) % nsplit) == cs) s += dws[((long)b * K + k) * CB + cl];
+  dw[e] += s;
 }
 
 int num_cus() {
@@ -300,7 +321,9 @@ int num_cus() {
 // the configurations built, (K, C) -> (dx channels per block CB, pixels per tile TP, 16-px tiles per data-grad unit
 // PX).  CB = C: one block per tile; CB < C: C / CB blocks per tile (column split).  K = 256 on one block per tile (C =
 // 128 / 256: 128-256 weight-grad accumulator registers per lane) was measured at 0.42-0.68x the three launches with
-// 49 / 106 spilled VGPRs (profiles/r05/bwd1x1_ab_v1.log)
+// 49 / 106 spilled VGPRs (profiles/r05/bwd1x1_ab_v1.log).  K = 512 x C = 128 split over 2 blocks (CB 64, TP 32, no
+// spills) measured 0.86x (1733 vs 1491 us @192^2 bs32, profiles/r05/bwd1x1_ab_v3.log): its dz transform, ~20 VALU
+// issue cycles per element run twice for 512 channels, is worth ~0.6 ms of VALU on its own, so it is not built
 struct Plan {
   int cb, tp, px;
 };
@@ -309,13 +332,22 @@ constexpr Plan plan(int K, int C) {
        : (K == 64 && C == 128) ? Plan{128, 64, 2} : (K == 128 && C == 128) ? Plan{128, 64, 2}
        : (K == 128 && C == 256) ? Plan{256, 64, 2} : (K == 128 && C == 512) ? Plan{256, 64, 2}
        : (K == 256 && C == 256) ? Plan{128, 32, 1} : (K == 256 && C == 128) ? Plan{128, 32, 1}
-       : Plan{0, 0, 0};
+       : (K == 64 && C == 256) ? Plan{256, 64, 2} : Plan{0, 0, 0};
+}
+
+// blocks of a launch: whole XCD groups of nsplit blocks (one per CU), no more groups than tiles
+inline int grid_blocks(long M, int K, int C) {
+  const Plan pl = plan(K, C);
+  const int ns = C / pl.cb, ntiles = ceil_div(M, pl.tp);
+  int ngrp = num_cus() / ns;
+  if (ngrp > ntiles) ngrp = (ntiles + 7) / 8 * 8;
+  return ngrp * ns;
 }
 
 template <int K, int C>
 int launch(const bf16* dy, long dps, const bf16* z, const bf16* x, long xps, const bf16* wt, const float* scale,
            const float* shift, const float* mean, const float* invstd, int act, const float* ca, const float* cb,
-           const float* cc, bf16* dx, long bps, int acc, float* dw, long M, hipStream_t st) {
+           const float* cc, bf16* dx, long bps, int acc, float* dw, float* ws, long M, hipStream_t st) {
   constexpr Plan pl = plan(K, C);
   constexpr int CB = pl.cb, TP = pl.tp, PX = pl.px, NS = C / CB;
   using S = Shape<K, CB, TP, PX>;
@@ -325,13 +357,12 @@ int launch(const bf16* dy, long dps, const bf16* z, const bf16* x, long xps, con
                               hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     raised = true;
   }
-  const int ntiles = ceil_div(M, TP);
-  // whole XCD groups of NS blocks; no more groups than tiles
-  int ngrp = num_cus() / NS;
-  if (ngrp > ntiles) ngrp = (ntiles + 7) / 8 * 8;
-  conv1x1_bwd_bn<K, CB, TP, PX><<<ngrp * NS, 256, S::LDS, st>>>(
-      dy, dps, z, x, xps, wt, scale, shift, mean, invstd, act, ca, cb, cc, dx, bps, acc, dw, M, ntiles, C, NS,
-      (unsigned)(2.0 * (double)M * dps), (unsigned)(2.0 * (double)M * K), (unsigned)(2.0 * (double)M * xps));
+  const int nb = grid_blocks(M, K, C);
+  conv1x1_bwd_bn<K, CB, TP, PX><<<nb, 256, S::LDS, st>>>(
+      dy, dps, z, x, xps, wt, scale, shift, mean, invstd, act, ca, cb, cc, dx, bps, acc, dw, ws, M, ceil_div(M, TP), C,
+      NS, (unsigned)(2.0 * (double)M * dps), (unsigned)(2.0 * (double)M * K), (unsigned)(2.0 * (double)M * xps));
+  if (ws != nullptr)
+    wgrad_slots_reduce<<<ceil_div((long)K * C, 256), 256, 0, st>>>(ws, dw, K, C, CB, nb, NS);
   return (int)hipGetLastError();
 }
 }  // namespace b1
@@ -349,16 +380,22 @@ DMY_API int dmy_conv1x1_bwd_bn_ok(long M, int K, int C, long dps, long xps, long
   return 1;
 }
 
+DMY_API long dmy_conv1x1_bwd_bn_ws_elems(long M, int K, int C) {
+  if (b1::plan(K, C).cb == 0 || M <= 0) return 0;
+  return (long)b1::grid_blocks(M, K, C) * K * b1::plan(K, C).cb;
+}
+
 DMY_API int dmy_conv1x1_bwd_bn(const void* dy, long dps, const void* z, const void* x, long xps, const void* wt,
                                const float* scale, const float* shift, const float* mean, const float* invstd, int act,
                                const float* ca, const float* cb, const float* cc, void* dx, long bps, int accumulate,
-                               float* dw, long M, int K, int C, void* stream) {
+                               float* dw, float* ws, long ws_elems, long M, int K, int C, void* stream) {
   if (!dmy_conv1x1_bwd_bn_ok(M, K, C, dps, xps, bps, dy, z, x, dx)) return -1;
+  if (ws != nullptr && ws_elems < dmy_conv1x1_bwd_bn_ws_elems(M, K, C)) return -1;
   hipStream_t st = (hipStream_t)stream;
 #define B1_GO(K_, C_)                                                                                                 \
   if (K == K_ && C == C_)                                                                                            \
     return b1::launch<K_, C_>((const bf16*)dy, dps, (const bf16*)z, (const bf16*)x, xps, (const bf16*)wt, scale,     \
-                              shift, mean, invstd, act, ca, cb, cc, (bf16*)dx, bps, accumulate, dw, M, st);
+                              shift, mean, invstd, act, ca, cb, cc, (bf16*)dx, bps, accumulate, dw, ws, M, st);
   B1_GO(64, 64)
   B1_GO(128, 64)
   B1_GO(64, 128)
@@ -367,6 +404,7 @@ DMY_API int dmy_conv1x1_bwd_bn(const void* dy, long dps, const void* z, const vo
   B1_GO(128, 512)
   B1_GO(256, 128)
   B1_GO(256, 256)
+  B1_GO(64, 256)
 #undef B1_GO
   return -1;
 }

@@ -41,7 +41,8 @@ SIGNATURES = {
     'dmy_conv_wprep': [I, P, P, P, I, I, I, I, I, P],
     # bwd1x1.hip
     'dmy_conv1x1_bwd_bn_ok': [L, I, I, L, L, L, P, P, P, P],
-    'dmy_conv1x1_bwd_bn': [P, L, P, P, L, P, P, P, P, P, I, P, P, P, P, L, I, P, L, I, I, P],
+    'dmy_conv1x1_bwd_bn': [P, L, P, P, L, P, P, P, P, P, I, P, P, P, P, L, I, P, P, L, L, I, I, P],
+    'dmy_conv1x1_bwd_bn_ws_elems': [L, I, I],
     # augment.hip
     'dmy_aug_desc_bytes': [],
     'dmy_augment_batch': [P, I, P, I, I, P],

@@ -571,11 +571,12 @@ BWD1X1 = [os.environ.get('DMY_BWD1X1', '1') == '1']
 
 def _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc, N, C, H, W, K, k, s, p, M):
     """-> (dx, dw) when the fused kernel took the layer's apply + data-grad + weight-grad, else None.  Eligible: bf16
-    storage, train-mode BN, 1x1 stride 1, both gradients wanted, not deterministic mode (its fp32 weight-grad atomics
-    are unordered), no producer-BN reduce link, a (K, C) pair the kernel is built for (dmy_conv1x1_bwd_bn_ok)."""
+    storage, train-mode BN, 1x1 stride 1, both gradients wanted, no producer-BN reduce link, a (K, C) pair the kernel
+    is built for (dmy_conv1x1_bwd_bn_ok).  Deterministic mode: the weight-grad partials go through a workspace summed
+    in block order instead of fp32 atomics."""
     if not (BWD1X1[0] and ctx.train_bn and k == 1 and s == 1 and p == 0 and not ctx.s2d and ctx.cp == C and
             dy.dtype == torch.bfloat16 and wt is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and
-            not DETERMINISTIC[0] and not (ctx.link_in is not None and FUSE_BN_REDUCE[0])):
+            not (ctx.link_in is not None and FUSE_BN_REDUCE[0])):
         return None
     buf_probe = ctx.xsink.peek(N, C, H, W) if ctx.xsink is not None else None
     bps_probe = buf_probe[1] if buf_probe is not None else C
@@ -588,9 +589,11 @@ def _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc,
     if dw is None:
         dw = torch.zeros((K, C, 1, 1), dtype=torch.float32, device=dev)
     es = z.element_size()
+    ne = call('dmy_conv1x1_bwd_bn_ws_elems', M, K, C) if DETERMINISTIC[0] else 0
+    ws = f32(ne, dev) if ne else None
     KernelTimer.run('conv_bwd1x1', 4.0 * M * K * C, 'dmy_conv1x1_bwd_bn', ptr(dy), dps, ptr(z), ptr(x), xps, ptr(wt),
                     ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ctx.spec.act, ptr(ca), ptr(cb), ptr(cc), ptr(buf),
-                    bps, acc, ptr(dw), M, K, C, stream(), tag=(N, C, H, W, K, k, s),
+                    bps, acc, ptr(dw), ptr(ws), ne, M, K, C, stream(), tag=(N, C, H, W, K, k, s),
                     nbytes=es * (2 * M * K + (2 + acc) * M * C + K * C) + 4 * K * C)
     return sink_result(ctx.xsink, buf), dw
 

@@ -71,13 +71,16 @@ int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int
  * one persistent launch.  Replaces dmy_bn_bwd_apply + dmy_conv_dgrad + dmy_conv_wgrad_ex(OIHW) of such a layer; the
  * reduce / finalize that produce ca, cb, cc run before it as before.  x / dx / dy: [M][C] / [M][C] / [M][K] rows of
  * pixel stride xps / bps / dps; z dense [M][K]; wt = the IHWO copy [C][K]; dw fp32 [K][C], ACCUMULATED (the caller
- * zeroes it).  _ok: 1 when this shape / alignment is supported (else the call returns -1 and launches nothing). */
+ * zeroes it).  _ok: 1 when this shape / alignment is supported (else the call returns -1 and launches nothing).
+ * ws (nullable): deterministic mode -- the per-block weight-grad partials go to ws (ws_elems >= _ws_elems) and are
+ * summed in block order (run-to-run bit-identical dw), instead of fp32 atomics. */
 int dmy_conv1x1_bwd_bn_ok(long M, int K, int C, long dps, long xps, long bps, const void* dy, const void* z,
                           const void* x, const void* dx);
 int dmy_conv1x1_bwd_bn(const void* dy, long dps, const void* z, const void* x, long xps, const void* wt,
                        const float* scale, const float* shift, const float* mean, const float* invstd, int act,
                        const float* ca, const float* cb, const float* cc, void* dx, long bps, int accumulate,
-                       float* dw, long M, int K, int C, void* stream);
+                       float* dw, float* ws, long ws_elems, long M, int K, int C, void* stream);
+long dmy_conv1x1_bwd_bn_ws_elems(long M, int K, int C);
 /* flags: 1 = write dw in torch OIHW order (the parameter's .grad layout, no wgrad_to_oihw pass; needs Cp == C),
  *        2 = dw is already zero (a per-step gradient arena cleared once), skip the memset.  Same sums as above. */
 int dmy_conv_wgrad_ex(int dtype, const void* x, const void* dy, float* dw, int N, int H, int W, int C, long xps, int K,

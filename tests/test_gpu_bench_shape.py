@@ -87,9 +87,11 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
                 {k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
 
     chaotic = yml in CHAOTIC
-    # product realizations: the state_dict as is, and (chaotic configs) ulp-perturbed copies, seeds 1..3 -- the product
-    # decides its bf16 roundings on slightly different fp32 values, exactly as the emulation realizations below do
-    prods = [product_run(sd)] + ([product_run(perturbed(s_)) for s_ in (1, 2, 3)] if chaotic else [])
+    # product realizations: the state_dict as is, and (chaotic configs) ulp-perturbed copies, seeds 1..4 -- the product
+    # decides its bf16 roundings on slightly different fp32 values, exactly as the emulation realizations below do.  An
+    # odd count, so the median is one realization (round 5: with 4 the upper median of [2.8e-2 .. 8.4e-2] failed against
+    # the max of 5 emulation realizations in one run, 6.5e-2, and passed in another, 1.4e-1)
+    prods = [product_run(sd)] + ([product_run(perturbed(s_)) for s_ in (1, 2, 3, 4)] if chaotic else [])
     p, loss, items, pgrads = prods[0]
     ref, pr, lr_, ir_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, None)
     emu, pe_, le_, ie_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16')
@@ -99,7 +101,7 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     # with the weights moved by one fp32 ulp (relative 2^-24 noise, seeds 1 / 2 / 3) -- each decides its bf16 roundings
     # on slightly different fp32 values, as the product's kernels do
     reals = [_oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16', 'cuda')]
-    for seed in ((1, 2, 3) if chaotic else (1, 2)):
+    for seed in ((1, 2, 3, 4, 5, 6) if chaotic else (1, 2)):
         reals.append(_oracle_grads(yml, nc, perturbed(seed), x, t, anchors, hyp, 'bf16', 'cuda'))
 
     def errs(po, lo, io, pg):
@@ -185,10 +187,10 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     if chaotic:
         # see CHAOTIC: the whole-model single-step gradient of this config is a noise realization, so one product
         # realization against one emulation realization says nothing.  Compared as DISTRIBUTIONS instead (VERDICT r4
-        # item 2b): 4 product realizations (ulp-perturbed weights) against 5 emulation realizations (CPU order, GPU
-        # order, 3 ulp-perturbed) -- the product's MEDIAN grad-norm-vector error, whole-gradient error and cosine must lie
+        # item 2b): 5 product realizations (ulp-perturbed weights) against 8 emulation realizations (CPU order, GPU
+        # order, 6 ulp-perturbed) -- the product's MEDIAN grad-norm-vector error, whole-gradient error and cosine must lie
         # inside the emulation realizations' range (median cosine >= their minimum)
-        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731 (upper median of an even count: the stricter one)
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
         p_gn = [r[3][0] for r in perr]
         p_wg = [r[3][1] for r in perr]
         p_cos = sorted(r[4] for r in perr)
@@ -264,9 +266,11 @@ def test_bench_shape_layers_bf16_vs_emulation(yml, img, bs):
     """Every top-level layer of a bench model alone at its bench resolution on the inputs the fp32 oracle sees there
     (tests/module_parity.py): the bf16 product module and the bf16-storage emulation of the oracle module against the
     fp32 oracle module, for one seeded upstream gradient.  DMA-YOLO-l @1536 (config 3) and config 5 @1920 -- there
-    C3TR's global attention runs over 60 x 60 = 3,600 tokens per image, as in the bench.  Bounds per layer (round 4
-    measured on DMA-YOLO-l: product / emulation input-gradient error 1.0-1.6x, parameter-gradient error 0.97-1.26x,
-    norms within 2e-4 of fp32 for both): input and parameter gradient relative L2 <= 1.75 x the emulation's + 5e-4,
+    C3TR's global attention runs over 60 x 60 = 3,600 tokens per image, as in the bench.  The emulation is 'bf16_sink'
+    with the layer's input gradient rounded as the product stores it (module_parity): round 4's 1.13x excess on every
+    plain Conv was exactly that one rounding.  Bounds per layer (round 5 measured, profiles/r05/layers_*.log: product /
+    emulation input-gradient error 0.89-1.21x, parameter-gradient error 0.78-1.21x, CoorAttention the highest at
+    1.21x, norms within 2e-4 of fp32 for both): input and parameter gradient relative L2 <= 1.25 x the emulation's + 5e-4,
     norm ratios within 1e-3 of 1 or of 1.5 x the emulation's own deviation + 2e-3 (config 5's C3TR over 3,600 tokens
     loses 42-51 % of its gradient to bf16 storage in product and emulation alike, norms 0.9962 vs 0.9978)."""
     from module_parity import layer_parity, fmt
@@ -281,7 +285,7 @@ def test_bench_shape_layers_bf16_vs_emulation(yml, img, bs):
             continue
         checks = [('dx', row['dx']), ('w', row.get('w'))]
         for kd, v in checks:
-            if v is not None and v[0] > 1.75 * v[1] + 5e-4:
+            if v is not None and v[0] > 1.25 * v[1] + 5e-4:
                 bad.append((i, name, kd, v))
         for kd in ('dxn', 'wn'):
             if kd in row and abs(row[kd][0] - 1) > max(1e-3, 1.5 * abs(row[kd][1] - 1) + 2e-3):

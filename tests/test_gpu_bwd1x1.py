@@ -11,7 +11,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-PAIRS = [(64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (128, 512), (256, 128), (256, 256)]
+PAIRS = [(64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (128, 512), (256, 128), (256, 256), (64, 256)]
 
 
 def _rel(a, b):
@@ -48,8 +48,18 @@ def test_bwd1x1_matches_apply_then_gemms(K, C, M, strided, acc):
     assert call('dmy_conv1x1_bwd_bn_ok', M, K, C, dps, xps, bps, ptr(dyb), ptr(z), ptr(xb), ptr(dxb)) == 1
     dw = torch.zeros(K, C, device='cuda')
     rc = call('dmy_conv1x1_bwd_bn', ptr(dyb), dps, ptr(z), ptr(xb), xps, ptr(wt), ptr(scale), ptr(shift), ptr(mean),
-              ptr(invstd), act, ptr(ca), ptr(cb), ptr(cc), ptr(dxb), bps, acc, ptr(dw), M, K, C, stream())
+              ptr(invstd), act, ptr(ca), ptr(cb), ptr(cc), ptr(dxb), bps, acc, ptr(dw), None, 0, M, K, C, stream())
     assert rc == 0
+    # deterministic mode (workspace partials summed in block order): the same sums, bit-identical run to run
+    ne = call('dmy_conv1x1_bwd_bn_ws_elems', M, K, C)
+    dets = []
+    for _ in range(2):
+        dwd, dxd = torch.zeros(K, C, device='cuda'), old.clone()
+        ws = torch.full((ne,), float('nan'), device='cuda')
+        call('dmy_conv1x1_bwd_bn', ptr(dyb), dps, ptr(z), ptr(xb), xps, ptr(wt), ptr(scale), ptr(shift), ptr(mean),
+             ptr(invstd), act, ptr(ca), ptr(cb), ptr(cc), ptr(dxd), bps, acc, ptr(dwd), ptr(ws), ne, M, K, C, stream())
+        dets.append((dwd, dxd))
+    assert torch.equal(dets[0][0], dets[1][0]) and torch.equal(dets[0][1], dets[1][1])
     # reference: the apply kernel's dz, then float64 GEMMs of the same bf16 operands
     dz = torch.empty(M, K, dtype=torch.bfloat16, device='cuda')
     assert call('dmy_bn_bwd_apply', 1, ptr(z), K, ptr(dyb), dps, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), act,
@@ -65,6 +75,7 @@ def test_bwd1x1_matches_apply_then_gemms(K, C, M, strided, acc):
     assert _rel(dx, dx_ref) < (3e-3 if acc else 2e-3), _rel(dx, dx_ref)
     assert (dx.float() - dx_ref.float()).abs().max() <= 2e-2 * dx_ref.float().abs().max()
     assert _rel(dw, dw_ref) < 1e-5, _rel(dw, dw_ref)
+    assert _rel(dets[0][0], dw_ref) < 1e-5 and torch.equal(dets[0][1], dxb)
     # the slice bounds of the strided dx buffer are untouched
     if bps > C:
         assert torch.equal(dxb[:, C:], old[:, C:])
@@ -76,10 +87,11 @@ def test_bwd1x1_unsupported_shapes_launch_nothing():
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 96, 64, 96, 64, 64, ptr(t), ptr(t), ptr(t), ptr(t)) == 0  # K = 96
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 512, 512, 512, 512, 512, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 256, 512, 256, 512, 512, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
+    assert call('dmy_conv1x1_bwd_bn_ok', 64, 512, 128, 512, 128, 128, ptr(t), ptr(t), ptr(t), ptr(t)) == 0
     assert call('dmy_conv1x1_bwd_bn_ok', 64, 64, 64, 68, 64, 64, ptr(t), ptr(t), ptr(t), ptr(t)) == 0  # dps % 8
     with pytest.raises(RuntimeError, match='hipError -1'):
         call('dmy_conv1x1_bwd_bn', ptr(t), 64, ptr(t), ptr(t), 64, ptr(t), None, None, None, None, 1, None, None, None,
-             ptr(t), 64, 0, None, 64, 96, 64, stream())
+             ptr(t), 64, 0, None, None, 0, 64, 96, 64, stream())
 
 
 def _module_grads(mod, x, gup, fused):
@@ -100,7 +112,7 @@ def _module_grads(mod, x, gup, fused):
 @pytest.mark.parametrize('kind,c1,c2,hw,bs', [('conv', 128, 128, 48, 8), ('conv', 256, 128, 40, 6),
                                               ('conv', 128, 256, 33, 7), ('c3', 128, 128, 40, 4),
                                               ('c3', 256, 256, 24, 4), ('conv', 512, 128, 40, 4),
-                                              ('conv', 256, 256, 30, 5)])
+                                              ('conv', 256, 256, 30, 5), ('conv', 256, 64, 40, 4)])
 def test_module_backward_fused_equals_three_pass(kind, c1, c2, hw, bs):
     """the same module, the same bf16 input and upstream gradient: the fused backward against the three-pass path
     (both product kernels): input gradient to one bf16 rounding of reordered sums, parameter gradients to fp32 order"""

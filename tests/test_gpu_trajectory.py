@@ -35,11 +35,12 @@ def test_bf16_training_trajectory(case):
     m, sd = tu.product_model(cfg, nc, fp8=fp8)
     hyp = scaled_hyp(HYP_VISDRONE, nc, img, m.model[-1].nl)
     pin_loss, pin_out, pin_grad = tu.pin_device_oracle(cfg, nc, sd, batches[0], hyp)
-    lp, op = tu.product_trajectory(m, batches, hyp, steps)
-    lr_, or_ = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, None)
-    lh, oh = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp16')
-    lb, ob = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp8' if fp8 else 'bf16')
-    ls, os_ = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'bf16' if fp8 else 'bf16_sink')
+    with tu.deterministic():
+        lp, op = tu.product_trajectory(m, batches, hyp, steps)
+        lr_, or_ = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, None)
+        lh, oh = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp16')
+        lb, ob = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp8' if fp8 else 'bf16')
+        ls, os_ = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'bf16' if fp8 else 'bf16_sink')
     cp, ch, cb, cs = tu.curve_err(lp, lr_), tu.curve_err(lh, lr_), tu.curve_err(lb, lr_), tu.curve_err(ls, lr_)
     ep, eh, eb, es = tu.out_err(op, or_), tu.out_err(oh, or_), tu.out_err(ob, or_), tu.out_err(os_, or_)
     f = lambda v: ' '.join('%.3e' % e for e in v)  # noqa: E731
@@ -58,8 +59,9 @@ def test_bf16_training_trajectory(case):
     print('  loss curves (every %d steps): fp32 %s\n  product %s\n  fp16 %s\n  bf16 %s\n  bf16_sink %s' % (
         q, f(lr_[::q].tolist()), f(lp[::q].tolist()), f(lh[::q].tolist()), f(lb[::q].tolist()),
         f(ls[::q].tolist())))
-    # the device-run fp32 oracle against the CPU one (fp32 summation order only; config 5's outputs 1.6e-4 measured)
-    assert pin_loss < 1e-5 and pin_out < 5e-4, (pin_loss, pin_out)
+    # the device-run oracle against the CPU one, both in float64 (round 5 measured: outputs 5e-14 .. 4.3e-9, gradient
+    # 6e-13 .. 8.2e-8): the same function, not just the same function up to fp32 summation order
+    assert pin_loss < 1e-6 and pin_out < 1e-6 and pin_grad < 1e-5, (pin_loss, pin_out, pin_grad)
     assert torch.isfinite(lp).all()
     # the run learns: the last eighth's mean loss is well under the first step's, for product and oracle alike
     assert float(lr_[-q:].mean()) < learn * float(lr_[0])
@@ -70,10 +72,10 @@ def test_bf16_training_trajectory(case):
     # realizations is about that wide (chaotic divergence of 120 SGD steps)
     emu_curve = max(ch[0], cb[0], cs[0])
     assert cp[0] <= 0.08 and cp[0] <= 2.0 * emu_curve, (cp, emu_curve)
-    # outputs: every level <= 0.3, and the mean over levels <= 1.5 x the mean of the furthest emulation per level -- a
-    # single level is a realization (config 5's level 0 measured 1.8e-2 and 7.3e-2 in two runs of the same code, the
-    # device fp32 oracle's own last-eighth loss 0.443 and 0.462: its torch backward sums with atomics)
+    # outputs: every level <= 0.3 and <= 1.5 x the furthest emulation's at that level + 0.01 (both trajectories are
+    # deterministic now, tu.deterministic: round 4 had summed the levels because one run's level 0 had moved 4x between
+    # runs of the same code -- the fp32 oracle's own loss curve moved with it, its backward summing with atomics)
     emu_out = [max(eh[lvl], eb[lvl], es[lvl]) for lvl in range(len(ep))]
-    assert max(ep) <= 0.3 and sum(ep) <= 1.5 * sum(emu_out), (ep, emu_out)
+    assert max(ep) <= 0.3 and all(a <= 1.5 * e + 0.01 for a, e in zip(ep, emu_out)), (ep, emu_out)
     # the final loss level (last eighth) within 8 % of the fp32 oracle's
     assert abs(float(lp[-q:].mean()) / float(lr_[-q:].mean()) - 1) <= 0.08

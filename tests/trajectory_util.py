@@ -80,6 +80,28 @@ def product_model(cfg, nc, seed=0, fp8=False):
     return _no_drop(m), sd
 
 
+class deterministic:
+    """context: run-to-run identical trajectories.  The product in its deterministic mode (functional.set_deterministic:
+    the split-K and fused-backward weight gradients through workspaces summed in a fixed order instead of fp32 atomics)
+    and torch's deterministic algorithms for the oracle's GPU ops (warn_only: adaptive_max_pool2d's backward has no
+    deterministic kernel, measured bit-identical across runs all the same, profiles/r05/traj_determinism.log).  Both
+    curves being fixed, the trajectory bounds need no allowance for either side's run-to-run noise."""
+
+    def __enter__(self):
+        from dmayolo import functional as fn
+        os.environ.setdefault('CUBLAS_WORKSPACE_CONFIG', ':4096:8')
+        self.prev = (fn.DETERMINISTIC[0], torch.are_deterministic_algorithms_enabled(),
+                     torch.is_deterministic_algorithms_warn_only_enabled())
+        fn.set_deterministic(True)
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        return self
+
+    def __exit__(self, *a):
+        from dmayolo import functional as fn
+        fn.set_deterministic(self.prev[0])
+        torch.use_deterministic_algorithms(self.prev[1], warn_only=self.prev[2])
+
+
 def product_trajectory(m, batches, hyp, steps, probe=0):
     """bench.py's training step (forward, ComputeLoss, backward seeded by the GradScaler, FusedSGD) for `steps` steps
     over the batches in turn; returns (losses [steps], train-mode outputs on batches[probe] after the last step)"""

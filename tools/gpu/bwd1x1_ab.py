@@ -17,7 +17,8 @@ from tune_conv import bench_cold  # noqa: E402
 # (N, C = fwd in = dx channels, H, W, K = fwd out = dz channels)
 SHAPES = [(32, 512, 192, 192, 128), (32, 256, 96, 96, 256), (32, 128, 192, 192, 128), (32, 64, 384, 384, 64), (32, 128, 384, 384, 64),
           (32, 256, 192, 192, 128), (32, 256, 192, 192, 256), (32, 128, 384, 384, 128), (32, 128, 192, 192, 256),
-          (64, 64, 160, 160, 64), (64, 128, 80, 80, 128), (64, 256, 40, 40, 256), (64, 128, 80, 80, 64)]
+          (64, 64, 160, 160, 64), (64, 128, 80, 80, 128), (64, 256, 40, 40, 256), (64, 128, 80, 80, 64),
+          (32, 128, 192, 192, 512), (64, 256, 80, 80, 64)]
 
 
 def main():
@@ -51,7 +52,7 @@ def main():
 
         def fused():
             call('dmy_conv1x1_bwd_bn', ptr(dy), K, ptr(z), ptr(x), C, ptr(wt), sc, sh, mu, inv, 1, ca, cb, cc,
-                 ptr(dx), C, acc, ptr(dw), M, K, C, stream())
+                 ptr(dx), C, acc, ptr(dw), None, 0, M, K, C, stream())
 
         ta, td, tw = bench_cold(apply), bench_cold(dgrad), bench_cold(wgrad)
         tf = bench_cold(fused)
