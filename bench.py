@@ -370,16 +370,29 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
                 z, _ = fwd(x1)
-                non_max_suppression(z, 0.25, 0.45, max_det=1000)
+                dets = non_max_suppression(z, 0.25, 0.45, max_det=1000)
                 torch.cuda.synchronize()
                 lat.append(time.perf_counter() - t1)
             lat = sorted(lat[10:])
-            return z, round(lat[len(lat) // 2] * 1e3, 3)
+            return z, dets, round(lat[len(lat) // 2] * 1e3, 3)
+
+        def p50_graph(n=60):  # forward + NMS recorded in ONE graph, one host read of the keep counts (infer.py)
+            lat = []
+            for i in range(n):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                dets, (z, _) = graphed.detect(x1, 0.25, 0.45, max_det=1000)
+                torch.cuda.synchronize()
+                lat.append(time.perf_counter() - t1)
+            lat = sorted(lat[10:])
+            return z, dets, round(lat[len(lat) // 2] * 1e3, 3)
 
         with torch.no_grad():
-            z, res['detect_eager_p50_ms'] = p50(ev)
-            zg, res['detect_p50_ms'] = p50(graphed)  # HIP-graph replay of the forward + NMS (infer.py)
-            assert torch.equal(z, zg), 'graph replay differs from the eager forward'
+            z, de, res['detect_eager_p50_ms'] = p50(ev)
+            zg, dg, res['detect_graph_fwd_p50_ms'] = p50(graphed)  # graph-replayed forward, eager NMS
+            zd, dd, res['detect_p50_ms'] = p50_graph()  # forward + NMS in one graph replay
+            assert torch.equal(z, zg) and torch.equal(z, zd), 'graph replay differs from the eager forward'
+            assert len(de) == len(dd) and all(torch.equal(a, b) for a, b in zip(de, dd)), 'graphed NMS differs'
             # NMS under load: random-init weights leave ~0 boxes above conf, so time NMS on Detect-shaped synthetic
             # predictions with 2,000 candidates (200 clusters x 10), alone and in the same timed loop as
             # the replayed forward (detect p50 as a loaded detector would see it)

@@ -86,19 +86,33 @@ __global__ void bitonic_global_kernel(unsigned long long* keys, long cap, long k
   }
 }
 
-// all passes with j < 1024 for a 2048-element tile in LDS
-__global__ void __launch_bounds__(1024) bitonic_local_kernel(unsigned long long* keys, long cap, long k_begin, long k_end) {
+// all passes with j < 1024 for a 2048-element tile in LDS.  In the first call (k_begin 2: no global pass has moved a key
+// between tiles yet) a tile wholly past the image's candidate count holds only pad keys (pad_keys_kernel), sorted in
+// either direction: it is skipped -- later calls may not skip, a descending merge carries real keys to a block's end.
+// When the whole segment is one tile (cap 2048), only the first P = pow2 >= count keys are sorted: the rest are pad
+// keys, already in place, so the network over the prefix leaves the segment ascending (batch-1 detect at random init:
+// ~0 candidates, 27 us -> a few)
+__global__ void __launch_bounds__(1024) bitonic_local_kernel(unsigned long long* keys, long cap, long k_begin, long k_end,
+                                                             const int* counts) {
   __shared__ unsigned long long s[2048];
   const int b = blockIdx.y;
   unsigned long long* K = keys + (long)b * cap + (long)blockIdx.x * 2048;
   const long g0 = (long)blockIdx.x * 2048;
+  const long n = min((long)counts[b], cap);
+  if (k_begin == 2 && g0 >= n) return;
+  int P = 2048;
+  if (cap == 2048 && k_begin == 2) {
+    P = 2;
+    while (P < n) P <<= 1;
+    k_end = P;
+  }
   s[threadIdx.x] = K[threadIdx.x];
   s[threadIdx.x + 1024] = K[threadIdx.x + 1024];
   __syncthreads();
   for (long k = k_begin; k <= k_end; k <<= 1) {
     for (long j = (k >> 1) < 1024 ? (k >> 1) : 1024; j > 0; j >>= 1) {
       if (j >= 2048) continue;
-      for (int t = threadIdx.x; t < 2048; t += 1024) {
+      for (int t = threadIdx.x; t < P; t += 1024) {
         const int l = t ^ (int)j;
         if (l > t) {
           const unsigned long long a = s[t], c = s[l];
@@ -300,10 +314,10 @@ DMY_API int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, 
   dim3 gp(grid_cap(ceil_div(cap, 256), 1024), nimg);
   pad_keys_kernel<<<gp, 256, 0, st>>>(keys, cap, counts, nimg);
   dim3 gl((unsigned)(cap / 2048), nimg);
-  bitonic_local_kernel<<<gl, 1024, 0, st>>>(keys, cap, 2, 2048);
+  bitonic_local_kernel<<<gl, 1024, 0, st>>>(keys, cap, 2, 2048, counts);
   for (long k = 4096; k <= cap; k <<= 1) {
     for (long j = k >> 1; j >= 2048; j >>= 1) bitonic_global_kernel<<<gp, 256, 0, st>>>(keys, cap, k, j);
-    bitonic_local_kernel<<<gl, 1024, 0, st>>>(keys, cap, k, k);
+    bitonic_local_kernel<<<gl, 1024, 0, st>>>(keys, cap, k, k, counts);
   }
   return (int)hipGetLastError();
 }

@@ -928,12 +928,17 @@ def conv_bn_act(x, weight, bias, bn, stride, pad, act, res=None, spec=None, xsin
 
 class MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, sink=None):
+    def forward(ctx, x, k, sink=None, out=None):
+        """out: None or [view] -- a concat_buffer channel slice the pooled map is written into (SPPF / SPPFCSPC), in a
+        list so autograd does not treat the buffer as an input"""
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
-        y = new_act(N, C, H, W, x)
+        o = out[0] if out else None
+        if o is not None and (tuple(o.shape) != (N, C, H, W) or o.dtype != x.dtype or pixel_stride(o)[0] is not o):
+            o = None
+        y, yps = (o, pixel_stride(o)[1]) if o is not None else (new_act(N, C, H, W, x), C)
         arg = torch.empty((N, H, W, C), dtype=torch.uint8, device=x.device)
-        call('dmy_maxpool_fwd', dcode(x), ptr(x), xps, ptr(y), C, ptr(arg), N, H, W, C, k, stream())
+        call('dmy_maxpool_fwd', dcode(x), ptr(x), xps, ptr(y), yps, ptr(arg), N, H, W, C, k, stream())
         ctx.save_for_backward(arg)
         ctx.k, ctx.shape, ctx.sink = k, (N, C, H, W), sink
         return y
@@ -945,7 +950,7 @@ class MaxPoolFn(torch.autograd.Function):
         dy, dps = pixel_stride(dy)
         buf, bps, acc = sink_target(ctx.sink, N, C, H, W, dy)
         call('dmy_maxpool_bwd', dcode(dy), ptr(dy), dps, ptr(arg), ptr(buf), bps, acc, N, H, W, C, ctx.k, stream())
-        return sink_result(ctx.sink, buf), None, None
+        return sink_result(ctx.sink, buf), None, None, None
 
 
 class AvgPoolFn(torch.autograd.Function):
@@ -971,11 +976,15 @@ class ResizeFn(torch.autograd.Function):
     """nearest resize with ATen's index rule (F.interpolate(mode='nearest'), nn.Upsample)."""
 
     @staticmethod
-    def forward(ctx, x, OH, OW):
+    def forward(ctx, x, OH, OW, out=None):
+        """out: None or [view] -- a concat_buffer channel slice the result is written into (Model's concat plan)"""
         x, xps = pixel_stride(x)
         N, C, H, W = x.shape
-        y = new_act(N, C, OH, OW, x)
-        call('dmy_resize_fwd', dcode(x), ptr(x), xps, ptr(y), C, 1.0, N, H, W, OH, OW, C, stream())
+        o = out[0] if out else None
+        if o is not None and (tuple(o.shape) != (N, C, OH, OW) or o.dtype != x.dtype or pixel_stride(o)[0] is not o):
+            o = None
+        y, yps = (o, pixel_stride(o)[1]) if o is not None else (new_act(N, C, OH, OW, x), C)
+        call('dmy_resize_fwd', dcode(x), ptr(x), xps, ptr(y), yps, 1.0, N, H, W, OH, OW, C, stream())
         ctx.shape = (N, C, H, W, OH, OW)
         return y
 
@@ -985,7 +994,7 @@ class ResizeFn(torch.autograd.Function):
         dy, dps = pixel_stride(dy)
         dx = new_act(N, C, H, W, dy)
         call('dmy_resize_bwd', dcode(dy), ptr(dy), dps, ptr(dx), C, N, H, W, OH, OW, C, stream())
-        return dx, None, None
+        return dx, None, None, None
 
 
 class ConcatFn(torch.autograd.Function):

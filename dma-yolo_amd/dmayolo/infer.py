@@ -3,8 +3,11 @@
 At batch 1 the eval forward is ~60 small kernel launches, and issuing them from Python costs more than
 running them.  GraphedDetector records one eval forward (every launch goes to torch's current stream,
 ctypes launches included) into a HIP graph with a static input buffer and replays it with a single
-launch.  NMS stays outside the graph: it reads one candidate count back to the host (variable-length
-output).
+launch.  `detect()` records the NMS kernels into the same graph (utils.general.nms_launch: no host read
+inside), so a detection is one graph launch and one host read of the keep counts (variable-length output,
+SURVEY §8(b)); eager NMS issued its 5-7 launches from Python after the forward, ~100-170 us of host gaps
+per call.  When some image had more candidates than the recorded sort capacity (the read says so) the call
+falls back to the eager NMS at the exact capacity once, and the next call re-records at that capacity.
 
 The graph bakes in the prepped weights and eval BN coefficients of the moment of capture: a call
 re-captures automatically when a parameter / buffer changed since (torch _version or
@@ -40,6 +43,45 @@ class GraphedDetector:
         with torch.cuda.graph(self.graph), torch.no_grad():
             self.static_out = self.model(self.static_in)
         self.key = self._state_key(x)
+
+    def _capture_detect(self, x, nms_args):
+        from .utils.general import nms_prepare, nms_launch
+        self._capture(x)  # warm-up forwards fill every per-layer cache; the forward-only graph stays usable
+        z = self.static_out[0]
+        pred, plan = nms_prepare(z, **nms_args)  # NMS plan from the recorded output's shape (the cap hint)
+        for _ in range(self.warmup):  # the NMS path's own allocations, outside the capture
+            nms_launch(pred, plan)
+        torch.cuda.synchronize()
+        self.dgraph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.dgraph), torch.no_grad():
+            out = self.model(self.static_in)
+            dpred = out[0].detach().float().contiguous()  # nms_prepare's conversion (the plan, cls_ok included, is made)
+            self.dstate = (out, plan, plan['cap']) + nms_launch(dpred, plan)
+        self.dkey = (self.key, tuple(sorted((k, str(v)) for k, v in nms_args.items())), plan['cap'])
+
+    @torch.no_grad()
+    def detect(self, x, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False, multi_label=False,
+               max_det=300):
+        """eval forward + non_max_suppression (utils/general.py:633-725 arguments, merge=False) as one graph replay:
+        returns (list of (k, 6) detections per image, (z, per-level outputs)).  The detections are views of the
+        graph's static output buffer, valid until the next call (as the forward's outputs are)."""
+        from .utils.general import nms_finish, non_max_suppression, _CAP_HINT
+        if self.model.training:
+            self.model.eval()
+        args = dict(conf_thres=conf_thres, iou_thres=iou_thres, classes=classes, agnostic=agnostic,
+                    multi_label=multi_label, max_det=max_det)
+        key = tuple(sorted((k, str(v)) for k, v in args.items()))
+        cur = getattr(self, 'dkey', None)
+        if (self.graph is None or self._state_key(x) != self.key or cur is None or cur[1] != key or
+                _CAP_HINT.get(self.dstate[1]['key'], cur[2]) != cur[2]):
+            self._capture_detect(x, args)
+        self.static_in.copy_(x)
+        self.dgraph.replay()
+        out, plan, cap, cnt, dets = self.dstate
+        res = nms_finish(plan, cap, cnt, dets)
+        if res is None:  # more candidates than the recorded capacity: this call eager at the exact one, next re-records
+            res = non_max_suppression(out[0], **args)
+        return res, out
 
     @torch.no_grad()
     def __call__(self, x):

@@ -108,13 +108,14 @@ class C3(nn.Module):
         self.cv3 = Conv(2 * c_, c2, 1)
         self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, e=1.0) for _ in range(n)))
 
-    def forward(self, x):
+    def forward(self, x, out=None):
+        """out: a concat_buffer slice cv3 writes the block's output into (Model's concat plan)"""
         sk = Fn.GradSink(2)  # x -> cv1 and cv2
         a = self.cv1(x, xsink=sk)
         blocks = list(self.m) if isinstance(self.m, nn.Sequential) else []
         seq = bool(blocks) and type(blocks[-1]) is Bottleneck and _INPLACE_CAT >= 1
         if not seq and not (getattr(self.m, 'dmy_out', False) and _INPLACE_CAT >= 2):
-            return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(a), self.cv2(x, xsink=sk)))
+            return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(a), self.cv2(x, xsink=sk)), out=out)
         # the last Bottleneck (or the Swin block) and cv2 write their activations straight into the two halves of the
         # concat buffer; a producer that cannot (e.g. an active DropPath) returns its own tensor and ConcatFn copies
         c_ = a.shape[1]
@@ -125,7 +126,7 @@ class C3(nn.Module):
             a = blocks[-1](a, out=cat[:, :c_])
         else:
             a = self.m(a, out=cat[:, :c_])
-        return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, a, self.cv2(x, xsink=sk, out=cat[:, c_:])))
+        return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, a, self.cv2(x, xsink=sk, out=cat[:, c_:])), out=out)
 
 
 class SPPF(nn.Module):
@@ -140,11 +141,18 @@ class SPPF(nn.Module):
 
     def forward(self, x):
         k = self.m.kernel_size
-        x = self.cv1(x)
+        c_ = self.cv1.conv.out_channels
+        if _INPLACE_CAT >= 1:  # cv1 and the three pools write straight into the concat buffer's slices: no copies
+            cat = Fn.concat_buffer(x.shape[0], 4 * c_, x.shape[2], x.shape[3], x)
+            sl = [cat[:, i * c_:(i + 1) * c_] for i in range(4)]
+        else:
+            sl = [None] * 4
+        x = self.cv1(x, out=sl[0])
         s0, s1, s2 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)  # each pool input -> next pool + concat
-        y1 = Fn.MaxPoolFn.apply(x, k, s0)
-        y2 = Fn.MaxPoolFn.apply(y1, k, s1)
-        return self.cv2(Fn.ConcatFn.apply(None, 0.0, (s0, s1, s2, None), x, y1, y2, Fn.MaxPoolFn.apply(y2, k, s2)))
+        y1 = Fn.MaxPoolFn.apply(x, k, s0, sl[1:2])
+        y2 = Fn.MaxPoolFn.apply(y1, k, s1, sl[2:3])
+        return self.cv2(Fn.ConcatFn.apply(None, 0.0, (s0, s1, s2, None), x, y1, y2,
+                                          Fn.MaxPoolFn.apply(y2, k, s2, sl[3:4])))
 
 
 class SPPFCSPC(nn.Module):
@@ -164,14 +172,23 @@ class SPPFCSPC(nn.Module):
 
     def forward(self, x):
         k = self.m.kernel_size
+        c_ = self.cv1.conv.out_channels
+        N, H, W = x.shape[0], x.shape[2], x.shape[3]
+        if _INPLACE_CAT >= 1:  # every concat input written straight into its slice (cv4 + the pools, cv6 + cv2)
+            cat = Fn.concat_buffer(N, 4 * c_, H, W, x)
+            sl = [cat[:, i * c_:(i + 1) * c_] for i in range(4)]
+            cat2 = Fn.concat_buffer(N, 2 * c_, H, W, x)
+            s2l = [cat2[:, :c_], cat2[:, c_:]]
+        else:
+            sl, s2l = [None] * 4, [None] * 2
         sx = Fn.GradSink(2)  # x -> cv1 and cv2
-        x1 = self.cv4(self.cv3(self.cv1(x, xsink=sx)))
+        x1 = self.cv4(self.cv3(self.cv1(x, xsink=sx)), out=sl[0])
         s1, s2, s3 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)
-        x2 = Fn.MaxPoolFn.apply(x1, k, s1)
-        x3 = Fn.MaxPoolFn.apply(x2, k, s2)
+        x2 = Fn.MaxPoolFn.apply(x1, k, s1, sl[1:2])
+        x3 = Fn.MaxPoolFn.apply(x2, k, s2, sl[2:3])
         y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, (s1, s2, s3, None), x1, x2, x3,
-                                                 Fn.MaxPoolFn.apply(x3, k, s3))))
-        y2 = self.cv2(x, xsink=sx)
+                                                 Fn.MaxPoolFn.apply(x3, k, s3, sl[3:4]))), out=s2l[0])
+        y2 = self.cv2(x, xsink=sx, out=s2l[1])
         return self.cv7(Fn.ConcatFn.apply(None, 0.0, None, y1, y2))
 
 
@@ -309,9 +326,15 @@ class SPP(nn.Module):
         self.m = nn.ModuleList([nn.MaxPool2d(kernel_size=x, stride=1, padding=x // 2) for x in k])
 
     def forward(self, x):
-        x = self.cv1(x)
-        sk = Fn.GradSink(len(self.m) + 1)  # x -> every pool and the concat
-        ys = [Fn.MaxPoolFn.apply(x, m.kernel_size, sk) for m in self.m]
+        c_, n = self.cv1.conv.out_channels, len(self.m)
+        if _INPLACE_CAT >= 1:  # cv1 and every pool write straight into the concat buffer's slices: no copies
+            cat = Fn.concat_buffer(x.shape[0], (n + 1) * c_, x.shape[2], x.shape[3], x)
+            sl = [cat[:, i * c_:(i + 1) * c_] for i in range(n + 1)]
+        else:
+            sl = [None] * (n + 1)
+        x = self.cv1(x, out=sl[0])
+        sk = Fn.GradSink(n + 1)  # x -> every pool and the concat
+        ys = [Fn.MaxPoolFn.apply(x, m.kernel_size, sk, sl[i + 1:i + 2]) for i, m in enumerate(self.m)]
         return self.cv2(Fn.ConcatFn.apply(None, 0.0, (sk,) + (None,) * len(ys), x, *ys))
 
 
@@ -375,9 +398,10 @@ class space_to_depth(nn.Module):
 
 
 class Upsample(nn.Upsample):
-    """nn.Upsample(None, 2, 'nearest') as used by the YAML heads; nearest only."""
+    """nn.Upsample(None, 2, 'nearest') as used by the YAML heads; nearest only.  out: a concat_buffer slice to write
+    the result into (Model's concat plan)."""
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         assert self.mode == 'nearest'
         H, W = x.shape[2:]
         if self.size is not None:
@@ -385,7 +409,7 @@ class Upsample(nn.Upsample):
         else:
             sf = self.scale_factor if isinstance(self.scale_factor, (tuple, list)) else (self.scale_factor,) * 2
             OH, OW = int(math.floor(H * sf[0])), int(math.floor(W * sf[1]))
-        return Fn.ResizeFn.apply(x, OH, OW)
+        return Fn.ResizeFn.apply(x, OH, OW, [out] if out is not None else None)
 
 
 # ------------------------------------------------------------------ Swin (C3STR) — layers in swin.py

@@ -24,6 +24,7 @@ from .tdetect import TDetect
 from ..utils.general import make_divisible
 from ..utils.torch_utils import initialize_weights, fuse_conv_and_bn
 
+_CAT_PLAN = os.environ.get('DMY_CAT_PLAN', '1') == '1'  # see Model._make_cat_plan
 _MODEL_SINKS = os.environ.get('DMY_MODEL_SINKS', '0') != '0'  # Model-level gradient fan-out sinks
 
 
@@ -218,6 +219,8 @@ class Model(nn.Module):
 
     def _forward_once(self, x, profile=False, visualize=False):
         x = self.to_input(x)
+        if self._cat_plans is None:
+            self._cat_plans = {}
         y = []
         arena = self.training and torch.is_grad_enabled() and x.is_cuda
         prev = Fn.WgradArena.current, Fn.WeightPrep.current
@@ -227,18 +230,66 @@ class Model(nn.Module):
             Fn.WeightPrep.current = self._weight_prep(x.device).launch()
         fan = self._fanout() if _MODEL_SINKS and torch.is_grad_enabled() and self.training else {}
         sinks = {}
+        skey = tuple(x.shape) + (x.dtype,)
+        plan = self._cat_plans.get(skey) if _CAT_PLAN else None
+        shapes = [] if _CAT_PLAN and plan is None else None
+        bufs = {}
         try:
             for m in self.model:
                 if m.f != -1:
                     x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
                 kw = self._sink_kw(m, sinks) if sinks else None
+                if plan is not None and m.i in plan:  # write straight into a later plain Concat's channel slice
+                    c, c0, C, shp = plan[m.i]
+                    if c not in bufs:
+                        bufs[c] = Fn.concat_buffer(*shp, x if torch.is_tensor(x) else x[0])
+                    kw = dict(kw or {}, out=bufs[c][:, c0:c0 + C])
                 x = m(x, **kw) if kw else m(x)
                 y.append(x if m.i in self.save else None)
+                if shapes is not None:
+                    shapes.append(tuple(x.shape) if torch.is_tensor(x) else None)
                 if m.i in fan:
                     sinks[m.i] = Fn.GradSink(0)
         finally:
             Fn.WgradArena.current, Fn.WeightPrep.current = prev
+        if shapes is not None:
+            self._cat_plans[skey] = self._make_cat_plan(shapes)
         return x
+
+    # In-place plain Concat across layers (DMY_CAT_PLAN=0 turns it off): after a first forward at an input shape has
+    # recorded every layer's output shape, each later forward at that shape allocates every plain Concat's buffer
+    # ahead and hands its producers (Conv, C3, Upsample: the modules whose forward takes out=) their channel slice,
+    # so ConcatFn recognises the in-place slices and copies nothing (yolov5s's head: 8 slice copies per forward).
+    # The producers' other consumers read the slice through its pixel stride.  Only concats whose every input comes
+    # from such a producer, each feeding no other concat.
+    _cat_plans = None
+
+    def _make_cat_plan(self, shapes):
+        import inspect
+        takes_out = lambda m: 'out' in inspect.signature(m.forward).parameters  # noqa: E731
+        users = {}
+        for m in self.model:
+            if type(m).__name__ == 'Concat':
+                for j in ([m.f] if isinstance(m.f, int) else m.f):
+                    users.setdefault(m.i - 1 if j == -1 else j, []).append(m.i)
+        plan = {}
+        for m in self.model:
+            if type(m).__name__ != 'Concat' or isinstance(m.f, int):
+                continue
+            src = [m.i - 1 if j == -1 else j for j in m.f]
+            shp = [shapes[j] for j in src]
+            if any(sh is None or len(sh) != 4 for sh in shp) or len(set(src)) != len(src):
+                continue
+            if any(len(users.get(j, [])) != 1 or not takes_out(self.model[j]) for j in src):
+                continue
+            if len({(sh[0], sh[2], sh[3]) for sh in shp}) != 1:
+                continue
+            Ct, c0 = sum(sh[1] for sh in shp), 0
+            N, _, H, W = shp[0]
+            for j, sh in zip(src, shp):
+                plan[j] = (m.i, c0, sh[1], (N, Ct, H, W))
+                c0 += sh[1]
+        return plan
 
     # gradient fan-out: a layer output read by several layers (the BiFPN skips, the P3-P5 outputs read by a Conv and
     # Detect) gets one GradSink that the sink-aware consumers' backward kernels write / accumulate into, so autograd

@@ -74,6 +74,68 @@ def _mask_cap():
     return _MASK_CAP[0]
 
 
+def nms_prepare(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False, multi_label=False,
+                labels=(), max_det=300):
+    """argument checks and the launch plan of non_max_suppression: (fp32 contiguous prediction, plan dict) -- the
+    plan's `cap` is the sort capacity the launch will use (the hint from earlier calls of this shape)"""
+    assert 0 <= conf_thres <= 1 and 0 <= iou_thres <= 1
+    if labels is not None and len(labels) and any(len(l) for l in labels):
+        raise NotImplementedError('autolabel (labels=...) is outside the DMA-YOLO hot path')
+    pred = prediction.detach()
+    if pred.dtype != torch.float32:
+        pred = pred.float()
+    pred = pred.contiguous()
+    nimg, A, no = pred.shape
+    nc = no - 5
+    multi = bool(multi_label and nc > 1)
+    cls_ok = None
+    if classes is not None:
+        cls_ok = torch.zeros(nc, dtype=torch.uint8, device=pred.device)
+        cls_ok[torch.tensor([c for c in classes if 0 <= c < nc], dtype=torch.long, device=pred.device)] = 1
+    key = (A, nc, multi)
+    plan = dict(conf=float(conf_thres), iou=float(iou_thres), multi=multi, cls_ok=cls_ok, agnostic=bool(agnostic),
+                max_det=int(max_det), key=key, cap=min(_CAP_HINT.get(key, 2048), _pow2(A * (nc if multi else 1))))
+    return pred, plan
+
+
+def nms_launch(pred, plan, cap=None):
+    """the NMS kernels of one call at sort capacity `cap`, no host synchronisation (so it can be recorded into a HIP
+    graph, infer.GraphedDetector.detect): returns (cnt, out) -- cnt = [candidate counts | keep counts] (int32, device),
+    out = (nimg, max_det, 6) rows; nms_finish reads them"""
+    nimg, A, no = pred.shape
+    dev = pred.device
+    cap = plan['cap'] if cap is None else cap
+    max_nms = 30000
+    cnt = torch.zeros(2 * nimg, dtype=torch.int32, device=dev)
+    keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
+    call('dmy_nms_candidates', ptr(pred), nimg, A, no, plan['conf'], int(plan['multi']), ptr(plan['cls_ok']), ptr(keys),
+         cap, ptr(cnt), stream())
+    call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), nimg, stream())
+    boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
+    out = torch.empty((nimg, plan['max_det'], 6), dtype=torch.float32, device=dev)
+    if cap <= _mask_cap():  # IoU bitmask + one-wave scan (same keep set and order as the lazy greedy kernel)
+        mask = torch.empty(nimg * cap * (cap // 64), dtype=torch.int64, device=dev)
+        call('dmy_nms_greedy_mask', ptr(pred), nimg, A, no, plan['iou'], int(plan['agnostic']), plan['max_det'],
+             max_nms, ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(mask), ptr(out), ptr(cnt[nimg:]), stream())
+    else:
+        call('dmy_nms_greedy', ptr(pred), nimg, A, no, plan['iou'], int(plan['agnostic']), plan['max_det'], max_nms,
+             ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
+    return cnt, out
+
+
+def nms_finish(plan, cap, cnt, out):
+    """the one host read of a launch: the per-image detections, or None when some image had more candidates than the
+    sort capacity held (the caller reruns at the capacity this records as the new hint)"""
+    nimg = out.shape[0]
+    h = cnt.tolist()  # the one host synchronisation
+    need = max(h[:nimg])
+    if need > cap:
+        _CAP_HINT[plan['key']] = _pow2(need)  # overflow: every candidate must enter the sort
+        return None
+    nk = h[nimg:]
+    return [out[b, :nk[b]] for b in range(nimg)]
+
+
 def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False,
                         multi_label=False, labels=(), max_det=300):
     """Drop-in for utils/general.py:633-725 (merge=False).  Returns a list of (k, 6) tensors
@@ -85,47 +147,13 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
     batch overflows it (its true count comes back in the same read) the call reruns once at the exact capacity, so
     the top-`max_nms` cut always sees every candidate (utils/general.py:702-703).
     """
-    assert 0 <= conf_thres <= 1 and 0 <= iou_thres <= 1
-    if labels is not None and len(labels) and any(len(l) for l in labels):
-        raise NotImplementedError('autolabel (labels=...) is outside the DMA-YOLO hot path')
-    pred = prediction.detach()
-    if pred.dtype != torch.float32:
-        pred = pred.float()
-    pred = pred.contiguous()
-    nimg, A, no = pred.shape
-    nc = no - 5
-    multi = bool(multi_label and nc > 1)
-    dev = pred.device
-    max_nms = 30000
-    cls_ok = None
-    if classes is not None:
-        cls_ok = torch.zeros(nc, dtype=torch.uint8, device=dev)
-        cls_ok[torch.tensor([c for c in classes if 0 <= c < nc], dtype=torch.long, device=dev)] = 1
-    if nimg == 0:
+    pred, plan = nms_prepare(prediction, conf_thres, iou_thres, classes, agnostic, multi_label, labels, max_det)
+    if pred.shape[0] == 0:
         return []
-    cap0 = _pow2(A * (nc if multi else 1))
-    key = (A, nc, multi)
-    cap = min(_CAP_HINT.get(key, 2048), cap0)
+    cap = plan['cap']
     while True:
-        cnt = torch.zeros(2 * nimg, dtype=torch.int32, device=dev)  # [candidate counts | keep counts]
-        keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
-        call('dmy_nms_candidates', ptr(pred), nimg, A, no, float(conf_thres), int(multi), ptr(cls_ok), ptr(keys), cap,
-             ptr(cnt), stream())
-        call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), nimg, stream())
-        boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
-        out = torch.empty((nimg, max_det, 6), dtype=torch.float32, device=dev)
-        if cap <= _mask_cap():  # IoU bitmask + one-wave scan (same keep set and order as the lazy greedy kernel)
-            mask = torch.empty(nimg * cap * (cap // 64), dtype=torch.int64, device=dev)
-            call('dmy_nms_greedy_mask', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det),
-                 max_nms, ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(mask), ptr(out), ptr(cnt[nimg:]), stream())
-        else:
-            call('dmy_nms_greedy', ptr(pred), nimg, A, no, float(iou_thres), int(bool(agnostic)), int(max_det), max_nms,
-                 ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
-        h = cnt.tolist()  # the one host synchronisation
-        need = max(h[:nimg])
-        if need <= cap:
-            break
-        cap = _pow2(need)  # overflow: every candidate must enter the sort; rerun once at the exact capacity
-        _CAP_HINT[key] = cap
-    nk = h[nimg:]
-    return [out[b, :nk[b]] for b in range(nimg)]
+        cnt, out = nms_launch(pred, plan, cap)
+        res = nms_finish(plan, cap, cnt, out)
+        if res is not None:
+            return res
+        cap = _CAP_HINT[plan['key']]

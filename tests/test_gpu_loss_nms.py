@@ -162,3 +162,23 @@ def test_nms_bitmask_path_vs_oracle(case):
         res.append([o[b, :int(nk[b])].cpu() for b in range(2)])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('cap', [2048, 4096, 8192])
+def test_nms_sort_any_count(cap):
+    """dmy_nms_sort (pad + bitonic network) leaves each image's first count keys ascending and pad keys after, for
+    counts from 0 to cap: the first tile-local pass skips pad-only tiles and, at cap 2048, sorts only the pow2 prefix
+    holding the candidates (round 5); later passes must not skip (a descending merge moves real keys to a block end)"""
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(cap)
+    counts = [0, 1, 5, 100, 1000, 2047, 2048, min(3000, cap), min(5000, cap), cap]
+    nimg = len(counts)
+    keys = torch.randint(0, 2 ** 62, (nimg, cap), generator=g, dtype=torch.int64)
+    ref = [torch.sort(keys[b, :n])[0] for b, n in enumerate(counts)]
+    kd = keys.cuda()
+    cnt = torch.tensor(counts + [0] * nimg, dtype=torch.int32, device='cuda')
+    call('dmy_nms_sort', ptr(kd), cap, ptr(cnt), nimg, stream())
+    out = kd.cpu()
+    for b, n in enumerate(counts):
+        assert torch.equal(out[b, :n], ref[b]), (cap, n)
+        assert bool((out[b, n:] == -1).all()), (cap, n)  # PADKEY = all ones

@@ -159,6 +159,30 @@ def test_graphed_detector_replays_eager_forward():
         torch.testing.assert_close(gd(xs[1])[0], m(xs[1])[0], rtol=0, atol=0)
 
 
+def test_graphed_detect_equals_eager_forward_and_nms():
+    """infer.GraphedDetector.detect (eval forward + the NMS kernels recorded in ONE graph, one host read) == the eager
+    forward + utils.general.non_max_suppression, bit for bit, at conf 0.25 and at conf 0.001 -- the latter leaves
+    thousands of candidates, more than the first recorded sort capacity: that call falls back to the eager NMS at the
+    exact capacity and the next one re-records at it"""
+    from dmayolo.models.yolo import Model
+    from dmayolo.infer import GraphedDetector
+    from dmayolo.utils.general import non_max_suppression
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5s.yaml'), nc=10, act_dtype=torch.bfloat16).cuda().eval()
+    gd = GraphedDetector(m)
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randint(0, 256, (1, 3, 256, 320), generator=g, dtype=torch.uint8).cuda() for _ in range(3)]
+    with torch.no_grad():
+        for conf in (0.25, 0.001):
+            for x in xs:
+                dets, (z, _) = gd.detect(x, conf, 0.45, max_det=300)
+                ze = m(x)[0]
+                de = non_max_suppression(ze, conf, 0.45, max_det=300)
+                assert torch.equal(z, ze)
+                assert len(dets) == len(de) and all(torch.equal(a, b) for a, b in zip(dets, de)), conf
+        assert sum(d.shape[0] for d in dets) > 0  # conf 0.001 keeps boxes
+
+
 def test_graphed_train_step_matches_eager():
     """train_graph.GraphedTrainStep (fwd + loss + bwd replayed as one HIP graph, optimizer / EMA eager) against
     the eager step on an identical model copy over batches with different target counts (zero-row padding,
