@@ -23,8 +23,10 @@ SHAPES = [(32, 512, 192, 192, 128), (32, 256, 96, 96, 256), (32, 128, 192, 192, 
 
 def main():
     acc = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    only = os.environ.get('B1_ONLY') == '1'  # profiling: the fused kernel alone (PMC passes)
+    shapes = SHAPES if os.environ.get('B1_SET') != 'pmc' else [SHAPES[2], SHAPES[1], SHAPES[3], SHAPES[0]]
     print(f'accumulate={acc}: shape (N C H W K) | apply dgrad wgrad = 3-pass us | fused us | speedup | fused GB/s')
-    for N, C, H, W, K in SHAPES:
+    for N, C, H, W, K in shapes:
         M = N * H * W
         g = torch.Generator(device='cuda').manual_seed(0)
         dy = (torch.randn(M, K, device='cuda', generator=g) * 0.1).bfloat16()
@@ -54,7 +56,7 @@ def main():
             call('dmy_conv1x1_bwd_bn', ptr(dy), K, ptr(z), ptr(x), C, ptr(wt), sc, sh, mu, inv, 1, ca, cb, cc,
                  ptr(dx), C, acc, ptr(dw), None, 0, M, K, C, stream())
 
-        ta, td, tw = bench_cold(apply), bench_cold(dgrad), bench_cold(wgrad)
+        ta, td, tw = (bench_cold(apply), bench_cold(dgrad), bench_cold(wgrad)) if not only else (0.0, 0.0, 0.0)
         tf = bench_cold(fused)
         nb = 2 * (2 * M * K + (2 + acc) * M * C + K * C) + 4 * K * C
         print(f'{N:3d} {C:4d} {H:4d} {W:4d} {K:4d} | {ta:7.1f} {td:7.1f} {tw:7.1f} = {ta + td + tw:7.1f} | '
