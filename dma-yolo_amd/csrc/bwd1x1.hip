@@ -324,6 +324,10 @@ int num_cus() {
 // 49 / 106 spilled VGPRs (profiles/r05/bwd1x1_ab_v1.log).  K = 512 x C = 128 split over 2 blocks (CB 64, TP 32, no
 // spills) measured 0.86x (1733 vs 1491 us @192^2 bs32, profiles/r05/bwd1x1_ab_v3.log): its dz transform, ~20 VALU
 // issue cycles per element run twice for 512 channels, is worth ~0.6 ms of VALU on its own, so it is not built
+// A second register set of prefetched (dy, z, x) chunks (tile t + 2 in flight while t computes; the sets rotated at
+// the prefetch point) measured 1-11 % SLOWER on every shape (profiles/r05/bwd1x1_depth2_ab.log): the PMC passes show
+// these launches issue-bound (~50 % of wave cycles issuing, 25-39 % waiting, profiles/r05/pmc_bwd1x1.txt), not
+// starved for loads in flight
 struct Plan {
   int cb, tp, px;
 };

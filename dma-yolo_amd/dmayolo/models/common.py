@@ -9,6 +9,7 @@ Activation tensors are NHWC (torch.channels_last) in the model's storage dtype.
 """
 import math
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -97,6 +98,23 @@ class Bottleneck(nn.Module):
 _INPLACE_CAT = int(os.environ.get('DMY_INPLACE_CAT', '2'))
 
 
+# inference: C3's cv1 and cv2 (both 1x1 over x) as ONE conv with their weights / BN stacked; DMY_C3_PAIR (default on)
+_C3_PAIR = os.environ.get('DMY_C3_PAIR', '1') == '1'
+_PAIRS = weakref.WeakKeyDictionary()  # C3 module -> (source key, weight, bias, bn, act); not module state, so no
+# state_dict / checkpoint entry
+
+
+class _PairBN:
+    """two eval-mode BatchNorm2d side by side (the stacked cv1 | cv2 of C3._pair), as conv_bn_act reads one"""
+    training, track_running_stats, momentum = False, True, None
+
+    def __init__(self, a, b):
+        self.eps = a.eps
+        self.weight, self.bias, self.running_mean, self.running_var = (
+            torch.cat([getattr(a, n).detach(), getattr(b, n).detach()])
+            for n in ('weight', 'bias', 'running_mean', 'running_var'))
+
+
 class C3(nn.Module):
     """models/common.py:159-182."""
 
@@ -108,12 +126,48 @@ class C3(nn.Module):
         self.cv3 = Conv(2 * c_, c2, 1)
         self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, e=1.0) for _ in range(n)))
 
+    def _pair(self):
+        """(weight, bias, bn, act) of cv1 | cv2 stacked along the output channels, rebuilt when a source parameter or
+        BN buffer changes (torch _version / Fn.PARAM_GEN); None when the two layers cannot share a launch"""
+        c1, c2 = self.cv1, self.cv2
+        b1, b2 = getattr(c1, 'bn', None), getattr(c2, 'bn', None)
+        w1, w2 = c1.conv.weight, c2.conv.weight
+        if (b1 is None) != (b2 is None) or type(c1.act) is not type(c2.act) or w1.shape[1:] != w2.shape[1:] or \
+                tuple(w1.shape[2:]) != (1, 1) or tuple(c1.conv.stride) != (1, 1) or tuple(c2.conv.stride) != (1, 1) or \
+                (b1 is not None and (b1.eps != b2.eps or b1.training or b2.training)) or \
+                (c1.conv.bias is None) != (c2.conv.bias is None):
+            return None
+        srcs = [w1, w2, c1.conv.bias, c2.conv.bias] + ([b1.weight, b1.bias, b1.running_mean, b1.running_var, b2.weight,
+                                                        b2.bias, b2.running_mean, b2.running_var] if b1 is not None else [])
+        key = (Fn.PARAM_GEN[0],) + tuple((t.data_ptr(), t._version) if t is not None else None for t in srcs)
+        ent = _PAIRS.get(self)
+        if ent is None or ent[0] != key:
+            w = torch.cat([w1.detach(), w2.detach()])
+            b = torch.cat([c1.conv.bias.detach(), c2.conv.bias.detach()]) if c1.conv.bias is not None else None
+            ent = _PAIRS[self] = (key, w, b, _PairBN(b1, b2) if b1 is not None else None, act_code(c1.act))
+        return ent[1:]
+
     def forward(self, x, out=None):
         """out: a concat_buffer slice cv3 writes the block's output into (Model's concat plan)"""
-        sk = Fn.GradSink(2)  # x -> cv1 and cv2
-        a = self.cv1(x, xsink=sk)
         blocks = list(self.m) if isinstance(self.m, nn.Sequential) else []
         seq = bool(blocks) and type(blocks[-1]) is Bottleneck and _INPLACE_CAT >= 1
+        pair = self._pair() if seq and _C3_PAIR and not self.training and not torch.is_grad_enabled() else None
+        if pair is not None:
+            # inference: one 1x1 launch writes cv1's and cv2's activations into the two halves of the concat buffer;
+            # the Bottleneck stack starts from the first half and its last block writes its output back over it (for
+            # one block that is its own residual input: each output element is read as the residual, then written, by
+            # the epilogue that owns it), so cv3 reads the buffer as the concat
+            w, b, bn, act = pair
+            c_ = w.shape[0] // 2
+            cat = Fn.concat_buffer(x.shape[0], 2 * c_, x.shape[2], x.shape[3], x)
+            Fn.conv_bn_act(x, w, b, bn, 1, 0, act, out=cat)
+            a = cat[:, :c_]
+            for blk in blocks[:-1]:
+                a = blk(a)
+            a = blocks[-1](a, out=cat[:, :c_])
+            return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, a, cat[:, c_:]), out=out)
+        sk = Fn.GradSink(2)  # x -> cv1 and cv2
+        a = self.cv1(x, xsink=sk)
         if not seq and not (getattr(self.m, 'dmy_out', False) and _INPLACE_CAT >= 2):
             return self.cv3(Fn.ConcatFn.apply(None, 0.0, None, self.m(a), self.cv2(x, xsink=sk)), out=out)
         # the last Bottleneck (or the Swin block) and cv2 write their activations straight into the two halves of the

@@ -113,3 +113,42 @@ def test_winattn_mfma_vs_fp32_kernel(B, H, W, nh, shift):
         outs[dt] = (o.float().cpu(), dq.float().cpu(), dtab.cpu())
     for a, b in zip(outs[1], outs[0]):
         assert rel_err(a, b) < 2e-2, rel_err(a, b)
+
+
+@pytest.mark.parametrize('n,shortcut,fused', [(1, True, False), (3, True, False), (1, False, False), (2, True, True)])
+def test_c3_pair_inference_equals_separate_layers(n, shortcut, fused):
+    """inference C3 with cv1 | cv2 as one stacked launch (C3._pair, DMY_C3_PAIR) vs the two separate layers, bf16
+    storage at a batch-1 detect shape; the stacked weights follow an in-place parameter update"""
+    import dmayolo.models.common as cm
+    from dmayolo.utils.torch_utils import fuse_conv_and_bn
+    torch.manual_seed(0)
+    m = cm.C3(64, 128, n=n, shortcut=shortcut)
+    for bn in (mm for mm in m.modules() if isinstance(mm, torch.nn.BatchNorm2d)):
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.uniform_(-0.2, 0.2)
+    if fused:
+        for cv in (m.cv1, m.cv2):
+            cv.conv = fuse_conv_and_bn(cv.conv, cv.bn)
+            delattr(cv, 'bn')
+            cv.forward = cv.forward_fuse
+    m = m.cuda().eval()  # fp32 parameters, bf16 activations (Model(act_dtype=bf16))
+    x = torch.randn(1, 64, 40, 56, device='cuda').to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(pair):
+        old, cm._C3_PAIR = cm._C3_PAIR, pair
+        try:
+            with torch.no_grad():
+                return m(x).float()
+        finally:
+            cm._C3_PAIR = old
+
+    assert m._pair() is not None
+    a, b = run(True), run(False)
+    assert rel_err(a, b) < 1e-2, rel_err(a, b)
+    with torch.no_grad():
+        m.cv2.conv.weight.mul_(-1.0)
+    a2, b2 = run(True), run(False)
+    assert rel_err(a2, b2) < 1e-2, rel_err(a2, b2)
+    assert rel_err(a2, a) > 1e-2  # the stacked weight was rebuilt

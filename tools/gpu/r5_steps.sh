@@ -1,11 +1,12 @@
 #!/bin/bash
 # Round 5: run named steps, each under its own limit, logs under gpurun_out/r5/<TAG>_<name>.log; a failing step ends
-# the script.  STEPS="name:limit:command;;name:limit:command" (commands run by bash from the repo root).
+# the script.  STEPS="name:limit:command;;name:limit:command" (commands run by bash from the repo root), or STEPS_FILE=<file>.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/r5
 mkdir -p $OUT
 TAG=${TAG:-s}
+[ -n "$STEPS_FILE" ] && STEPS="$(cat $STEPS_FILE)"
 ( while sleep 50; do echo "[hb] $(date +%T)"; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
