@@ -49,6 +49,54 @@ __global__ void decode_kernel(const T* __restrict__ y, long sb, long sh, long sw
   }
 }
 
+// all levels of one Detect forward in one launch: the level of a flat element index from the cumulative element
+// counts, then decode_kernel's arithmetic (the same bits)
+constexpr int kDecLevels = 4;
+struct DecTab {
+  const void* y[kDecLevels];
+  long sb[kDecLevels], sh[kDecLevels], sw[kDecLevels], zoff[kDecLevels], cum[kDecLevels + 1];
+  int H[kDecLevels], W[kDecLevels];
+  float stride[kDecLevels];
+  int nl;
+};
+
+template <typename T>
+__global__ void decode_levels_kernel(DecTab tab, int N, int na, int no, const float* __restrict__ anchors,
+                                     float* __restrict__ z, long ztotal) {
+  for (long g = blockIdx.x * (long)blockDim.x + threadIdx.x; g < tab.cum[tab.nl]; g += (long)gridDim.x * blockDim.x) {
+    int L = 0;
+#pragma unroll
+    for (int l = 1; l < kDecLevels; ++l)
+      if (l < tab.nl && g >= tab.cum[l]) L = l;
+    const long i = g - tab.cum[L];
+    const int H = tab.H[L], W = tab.W[L];
+    const int c = (int)(i % no);
+    long t = i / no;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    t /= H;
+    const int a = (int)(t % na);
+    const int b = (int)(t / na);
+    const T* y = static_cast<const T*>(tab.y[L]);
+    const float v = to_f(y[b * tab.sb[L] + h * tab.sh[L] + w * tab.sw[L] + a * no + c]);
+    const float stride = tab.stride[L];
+    float s = 1.0f / (1.0f + expf(-v));
+    float o;
+    if (c < 2) {
+      const float gg = (float)(c == 0 ? w : h);
+      o = (s * 2.0f - 0.5f + gg) * stride;
+    } else if (c < 4) {
+      const float ag = anchors[(L * na + a) * 2 + (c - 2)] * stride;
+      const float q = s * 2.0f;
+      o = (q * q) * ag;
+    } else {
+      o = s;
+    }
+    z[((long)b * ztotal + tab.zoff[L] + ((long)a * H + h) * W + w) * no + c] = o;
+  }
+}
+
 // ---------------------------------------------------------------- build_targets
 struct TgtOut {
   int* b; int* a; int* gj; int* gi; int* tcls; float* tbox; float* anch; int* count;
@@ -365,6 +413,33 @@ DMY_API int dmy_detect_decode(int dtype, const void* y, long sb, long sh, long s
   const int g = grid_cap(ceil_div(total, 256), 8192);
   if (dtype) decode_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>((const bf16*)y, sb, sh, sw, N, H, W, na, no, stride, anchors, z, zoff, ztotal);
   else decode_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)y, sb, sh, sw, N, H, W, na, no, stride, anchors, z, zoff, ztotal);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_detect_decode_levels(int dtype, int nl, const void* const* ys, const long* strides, const int* hw,
+                                     const float* lvl_stride, int N, int na, int no, const float* anchors, float* z,
+                                     long ztotal, void* stream) {
+  if (nl < 1 || nl > kDecLevels) return (int)hipErrorInvalidValue;
+  DecTab tab{};
+  tab.nl = nl;
+  long zoff = 0;
+  tab.cum[0] = 0;
+  for (int l = 0; l < nl; ++l) {
+    tab.y[l] = ys[l];
+    tab.sb[l] = strides[3 * l];
+    tab.sh[l] = strides[3 * l + 1];
+    tab.sw[l] = strides[3 * l + 2];
+    tab.H[l] = hw[2 * l];
+    tab.W[l] = hw[2 * l + 1];
+    tab.stride[l] = lvl_stride[l];
+    tab.zoff[l] = zoff;
+    zoff += (long)na * tab.H[l] * tab.W[l];
+    tab.cum[l + 1] = tab.cum[l] + (long)N * na * tab.H[l] * tab.W[l] * no;
+  }
+  if (zoff != ztotal) return (int)hipErrorInvalidValue;
+  const int g = grid_cap(ceil_div(tab.cum[nl], 256), 8192);
+  if (dtype) decode_levels_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>(tab, N, na, no, anchors, z, ztotal);
+  else decode_levels_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>(tab, N, na, no, anchors, z, ztotal);
   return (int)hipGetLastError();
 }
 

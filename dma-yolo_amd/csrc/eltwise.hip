@@ -1137,6 +1137,107 @@ inline int egrid(long n) { return grid_cap(ceil_div(n, 256), 8192); }
 
 namespace {
 // all channel counts / pixel strides multiples of the 16-B vector and all bases 16-B aligned
+// Inference SPPF / SPPFCSPC pyramid (models/common.py:243-258, :1257-1276 under torch.no_grad): y1 = pool(x),
+// y2 = pool(y1), y3 = pool(y2) with the same k x k stride-1 window, in ONE launch instead of three.  The tile is loaded
+// with a 3P halo and the three pools run back to back in LDS, each over the region the next one needs, with
+// out-of-image positions -inf at every stage, the row pass before the column pass, taps in increasing order and
+// maxpool_fwd_lds's update rule (greater, or NaN): the bits of the three chained launches.  No argmax (no backward).
+template <typename T, int K>
+DEV void mp_stage(const uint4* src, int SW, uint4* rowb, uint4* dst, int DH, int DW, int gh0, int gw0, int H, int W) {
+  // src: (DH + K - 1) x SW, SW = DW + K - 1, origin image (gh0 - P, gw0 - P); dst: DH x DW, origin (gh0, gw0)
+  constexpr int NV = Traits<T>::VW, P = K / 2;
+  const int SH = DH + K - 1;
+  for (int e = threadIdx.x; e < SH * DW; e += 256) {
+    const int r = e / DW, w = e % DW;
+    float best[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) best[j] = -INFINITY;
+#pragma unroll
+    for (int dw = 0; dw < K; ++dw) {
+      float v[NV];
+      unpack<T>(src[r * SW + w + dw], v);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const unsigned up = (unsigned)(v[j] > best[j]) | (unsigned)__builtin_isnan(v[j]);
+        best[j] = up ? v[j] : best[j];
+      }
+    }
+    rowb[e] = pack<T>(best);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < DH * DW; e += 256) {
+    const int h = e / DW, w = e % DW;
+    float best[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) best[j] = -INFINITY;
+    const int gh = gh0 + h, gw = gw0 + w;
+    if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
+#pragma unroll
+      for (int dh = 0; dh < K; ++dh) {
+        float v[NV];
+        unpack<T>(rowb[(h + dh) * DW + w], v);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const unsigned up = (unsigned)(v[j] > best[j]) | (unsigned)__builtin_isnan(v[j]);
+          best[j] = up ? v[j] : best[j];
+        }
+      }
+    }
+    dst[e] = pack<T>(best);  // -inf off the image: the next pool's padding
+  }
+  __syncthreads();
+}
+
+template <typename T, int K, int TH, int TW>
+__global__ void __launch_bounds__(256) maxpool_chain3_lds(const T* __restrict__ x, long xps, T* __restrict__ y1,
+                                                          T* __restrict__ y2, T* __restrict__ y3, long yps, int H, int W,
+                                                          int C) {
+  constexpr int NV = Traits<T>::VW, P = K / 2;
+  constexpr int XH = TH + 6 * P, XW = TW + 6 * P;  // x with the 3P halo
+  constexpr int AH = TH + 4 * P, AW = TW + 4 * P;  // y1 region (2P halo)
+  __shared__ uint4 bufx[XH * XW];       // x, later y2
+  __shared__ uint4 bufr[XH * AW];       // row-pass scratch (largest: stage 1)
+  __shared__ uint4 bufa[AH * AW];       // y1
+  // block -> (image, tile, channel vector), channel vector fastest (mp_tile's order, without its XCD grouping: these
+  // grids are small)
+  const int CV = C / NV, twn = (W + TW - 1) / TW, thn = (H + TH - 1) / TH;
+  int L = (int)blockIdx.x;
+  const int c = (L % CV) * NV;
+  L /= CV;
+  const int w0 = (L % twn) * TW;
+  L /= twn;
+  const int h0 = (L % thn) * TH, b = L / thn;
+  const T* xb = x + (long)b * H * W * xps + c;
+  float ninf[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) ninf[j] = -INFINITY;
+  const uint4 pad = pack<T>(ninf);
+  for (int e = threadIdx.x; e < XH * XW; e += 256) {
+    const int hh = h0 - 3 * P + e / XW, ww = w0 - 3 * P + e % XW;
+    bufx[e] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                  ? *reinterpret_cast<const uint4*>(xb + ((long)hh * W + ww) * xps) : pad;
+  }
+  __syncthreads();
+  mp_stage<T, K>(bufx, XW, bufr, bufa, AH, AW, h0 - 2 * P, w0 - 2 * P, H, W);   // y1 over the 2P halo
+  constexpr int BH = TH + 2 * P, BW = TW + 2 * P;
+  mp_stage<T, K>(bufa, AW, bufr, bufx, BH, BW, h0 - P, w0 - P, H, W);           // y2 over the P halo (into bufx)
+  // y3 over the tile: into bufa (y1 is still needed for its store: stored first)
+  for (int e = threadIdx.x; e < TH * TW; e += 256) {
+    const int h = e / TW, w = e % TW, oh = h0 + h, ow = w0 + w;
+    if (oh >= H || ow >= W) continue;
+    const long pix = ((long)b * H + oh) * W + ow;
+    *reinterpret_cast<uint4*>(y1 + pix * yps + c) = bufa[(h + 2 * P) * AW + w + 2 * P];
+    *reinterpret_cast<uint4*>(y2 + pix * yps + c) = bufx[(h + P) * BW + w + P];
+  }
+  __syncthreads();
+  mp_stage<T, K>(bufx, BW, bufr, bufa, TH, TW, h0, w0, H, W);
+  for (int e = threadIdx.x; e < TH * TW; e += 256) {
+    const int h = e / TW, w = e % TW, oh = h0 + h, ow = w0 + w;
+    if (oh >= H || ow >= W) continue;
+    *reinterpret_cast<uint4*>(y3 + (((long)b * H + oh) * W + ow) * yps + c) = bufa[e];
+  }
+}
+
 inline bool vec_ok(int dtype, std::initializer_list<long> ns, std::initializer_list<const void*> ps) {
   const long VW = dtype ? 8 : 4;
   for (long n : ns)
@@ -1180,6 +1281,29 @@ DMY_API int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yp
     default: MP_FWD(0); break;
   }
 #undef MP_FWD
+  return (int)hipGetLastError();
+}
+// y1 = pool(x), y2 = pool(y1), y3 = pool(y2) (k x k, stride 1, pad k / 2) in one launch, no argmax (inference); the
+// three outputs share the pixel stride yps (three channel slices of one concat buffer, or three tensors)
+DMY_API int dmy_maxpool_chain3_fwd(int dtype, const void* x, long xps, void* y1, void* y2, void* y3, long yps, int N,
+                                   int H, int W, int C, int k, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!vec_ok(dtype, {C, xps, yps}, {x, y1, y2, y3}) || (k != 3 && k != 5) || N * (C / (dtype ? 8 : 4)) >= 65536)
+    return (int)hipErrorInvalidValue;
+  // 16 x 32 tiles, or 8 x 16 when those leave most CUs idle (the 20^2 / 40^2 maps of batch-1 detect)
+  const long cv = N * (C / (dtype ? 8 : 4));
+  const bool small = cv * ceil_div(W, 32) * ceil_div(H, 16) < 256;
+  const unsigned gl = (unsigned)(cv * (small ? ceil_div(W, 16) * ceil_div(H, 8) : ceil_div(W, 32) * ceil_div(H, 16)));
+#define MP3(KS, TH, TW) if (dtype) maxpool_chain3_lds<bf16, KS, TH, TW><<<gl, 256, 0, st>>>((const bf16*)x, xps, (bf16*)y1, (bf16*)y2, (bf16*)y3, yps, H, W, C); \
+                        else maxpool_chain3_lds<float, KS, TH, TW><<<gl, 256, 0, st>>>((const float*)x, xps, (float*)y1, (float*)y2, (float*)y3, yps, H, W, C)
+  if (k == 5) {
+    if (small) MP3(5, 8, 16);
+    else MP3(5, 16, 32);
+  } else {
+    if (small) MP3(3, 8, 16);
+    else MP3(3, 16, 32);
+  }
+#undef MP3
   return (int)hipGetLastError();
 }
 DMY_API int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned char* arg, void* dx, long dxps,

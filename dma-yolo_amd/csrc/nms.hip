@@ -90,7 +90,7 @@ __global__ void bitonic_global_kernel(unsigned long long* keys, long cap, long k
 // between tiles yet) a tile wholly past the image's candidate count holds only pad keys (pad_keys_kernel), sorted in
 // either direction: it is skipped -- later calls may not skip, a descending merge carries real keys to a block's end.
 // When the whole segment is one tile (cap 2048), only the first P = pow2 >= count keys are sorted: the rest are pad
-// keys, already in place, so the network over the prefix leaves the segment ascending (batch-1 detect at random init:
+// keys (written here as the tile is loaded), so the network over the prefix leaves the segment ascending (batch-1 detect at random init:
 // ~0 candidates, 27 us -> a few)
 __global__ void __launch_bounds__(1024) bitonic_local_kernel(unsigned long long* keys, long cap, long k_begin, long k_end,
                                                              const int* counts) {
@@ -99,15 +99,17 @@ __global__ void __launch_bounds__(1024) bitonic_local_kernel(unsigned long long*
   unsigned long long* K = keys + (long)b * cap + (long)blockIdx.x * 2048;
   const long g0 = (long)blockIdx.x * 2048;
   const long n = min((long)counts[b], cap);
-  if (k_begin == 2 && g0 >= n) return;
+  if (k_begin == 2 && g0 >= n && cap > 2048) return;  // (one tile: still writes its pads)
   int P = 2048;
-  if (cap == 2048 && k_begin == 2) {
+  const bool one = cap == 2048 && k_begin == 2;
+  if (one) {
     P = 2;
     while (P < n) P <<= 1;
     k_end = P;
   }
-  s[threadIdx.x] = K[threadIdx.x];
-  s[threadIdx.x + 1024] = K[threadIdx.x + 1024];
+  // one tile: the pad keys past the count are made here (dmy_nms_sort launches no pad_keys_kernel for cap 2048)
+  s[threadIdx.x] = one && threadIdx.x >= n ? PADKEY : K[threadIdx.x];
+  s[threadIdx.x + 1024] = one && threadIdx.x + 1024 >= n ? PADKEY : K[threadIdx.x + 1024];
   __syncthreads();
   for (long k = k_begin; k <= k_end; k <<= 1) {
     for (long j = (k >> 1) < 1024 ? (k >> 1) : 1024; j > 0; j >>= 1) {
@@ -145,8 +147,9 @@ DEV void cand_box(const float* pred, const NmsCfg& cfg, int b, unsigned long lon
 
 __global__ void __launch_bounds__(1024) nms_greedy_kernel(const float* __restrict__ pred, NmsCfg cfg,
                                                          const unsigned long long* __restrict__ keys, long cap,
-                                                         const int* __restrict__ counts, float* __restrict__ boxes,
-                                                         float* __restrict__ out, int* __restrict__ nkeep) {
+                                                         int* __restrict__ counts, float* __restrict__ boxes,
+                                                         float* __restrict__ out, int* __restrict__ nkeep,
+                                                         int* __restrict__ ncand) {
   extern __shared__ unsigned long long dead[];  // ceil(n/64) words
   const int b = blockIdx.x;
   const int n = min(min(counts[b], (int)cap), cfg.max_nms);
@@ -192,7 +195,13 @@ __global__ void __launch_bounds__(1024) nms_greedy_kernel(const float* __restric
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) nkeep[b] = kept;
+  if (threadIdx.x == 0) {
+    nkeep[b] = kept;
+    if (ncand != nullptr) {  // the count leaves through ncand; the counter is zero again for the next call
+      ncand[b] = counts[b];
+      counts[b] = 0;
+    }
+  }
 }
 
 
@@ -204,36 +213,34 @@ __global__ void __launch_bounds__(1024) nms_greedy_kernel(const float* __restric
 // mask words ORed into the later blocks' removed words in parallel (one word per lane). Same keep set and order.
 constexpr int kMaskCap = 4096;
 
-__global__ void nms_boxes_kernel(const float* __restrict__ pred, NmsCfg cfg, const unsigned long long* __restrict__ keys,
-                                 long cap, const int* __restrict__ counts, float* __restrict__ boxes) {
-  const int b = blockIdx.y;
-  const int n = min(min(counts[b], (int)cap), cfg.max_nms);
-  float* B = boxes + (long)b * cfg.max_nms * 5;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    float bx[4], sc, cl;
-    cand_box(pred, cfg, b, keys[(long)b * cap + i], bx, &sc, &cl);
-    const float off = cfg.agnostic ? 0.f : __fmul_rn(cl, 4096.f);
-    for (int q = 0; q < 4; ++q) B[i * 5 + q] = __fadd_rn(bx[q], off);
-    B[i * 5 + 4] = __fmul_rn(__fsub_rn(B[i * 5 + 2], B[i * 5 + 0]), __fsub_rn(B[i * 5 + 3], B[i * 5 + 1]));
-  }
+// the offset box + area of sorted candidate i (nms_boxes_kernel's arithmetic)
+DEV void offset_box(const float* pred, const NmsCfg& cfg, int b, unsigned long long key, float* o) {
+  float bx[4], sc, cl;
+  cand_box(pred, cfg, b, key, bx, &sc, &cl);
+  const float off = cfg.agnostic ? 0.f : __fmul_rn(cl, 4096.f);
+  for (int q = 0; q < 4; ++q) o[q] = __fadd_rn(bx[q], off);
+  o[4] = __fmul_rn(__fsub_rn(o[2], o[0]), __fsub_rn(o[3], o[1]));
 }
 
-// grid (cap/64 row blocks, cap/64 column blocks, nimg), 64 threads: mask[b][i][cb] bit c = IoU(i, 64 cb + c) > thr, j > i
-__global__ void __launch_bounds__(64) nms_mask_kernel(NmsCfg cfg, long cap, const int* __restrict__ counts,
-                                                      const float* __restrict__ boxes, unsigned long long* __restrict__ mask) {
+// grid (cap/64 row blocks, cap/64 column blocks, nimg), 64 threads: mask[b][i][cb] bit c = IoU(i, 64 cb + c) > thr, j > i.
+// The boxes come straight from the sorted keys (offset_box): no separate boxes launch
+__global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ pred, NmsCfg cfg,
+                                                      const unsigned long long* __restrict__ keys, long cap,
+                                                      const int* __restrict__ counts,
+                                                      unsigned long long* __restrict__ mask) {
   const int rb = blockIdx.x, cb = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
   if (cb < rb) return;
   const int n = min(min(counts[b], (int)cap), cfg.max_nms);
   if (rb * 64 >= n) return;
-  const float* B = boxes + (long)b * cfg.max_nms * 5;
   __shared__ float cbx[64][5];
   const int j0 = cb * 64;
-  if (j0 + t < n)
-    for (int q = 0; q < 5; ++q) cbx[t][q] = B[(j0 + t) * 5 + q];
+  if (j0 + t < n) offset_box(pred, cfg, b, keys[(long)b * cap + j0 + t], cbx[t]);
   __syncthreads();
   const int i = rb * 64 + t;
   if (i >= n) return;
-  const float x1 = B[i * 5], y1 = B[i * 5 + 1], x2 = B[i * 5 + 2], y2 = B[i * 5 + 3], ai = B[i * 5 + 4];
+  float rbx[5];
+  offset_box(pred, cfg, b, keys[(long)b * cap + i], rbx);
+  const float x1 = rbx[0], y1 = rbx[1], x2 = rbx[2], y2 = rbx[3], ai = rbx[4];
   unsigned long long bits = 0ull;
   const int cend = min(64, n - j0);
   for (int c = 0; c < cend; ++c) {
@@ -256,9 +263,10 @@ DEV unsigned long long readlane64(unsigned long long v, int l) {
 // one wave per image; lane w holds the removed-bits word of candidates [64 w, 64 w + 64)
 __global__ void __launch_bounds__(64) nms_scan_kernel(const float* __restrict__ pred, NmsCfg cfg,
                                                       const unsigned long long* __restrict__ keys, long cap,
-                                                      const int* __restrict__ counts,
+                                                      int* __restrict__ counts,
                                                       const unsigned long long* __restrict__ mask,
-                                                      float* __restrict__ out, int* __restrict__ nkeep) {
+                                                      float* __restrict__ out, int* __restrict__ nkeep,
+                                                      int* __restrict__ ncand) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int n = min(min(counts[b], (int)cap), cfg.max_nms);
   const int nw = (n + 63) / 64, W = (int)(cap / 64);
@@ -294,7 +302,13 @@ __global__ void __launch_bounds__(64) nms_scan_kernel(const float* __restrict__ 
       }
     }
   }
-  if (lane == 0) nkeep[b] = kept;
+  if (lane == 0) {
+    nkeep[b] = kept;
+    if (ncand != nullptr) {  // the count leaves through ncand; the counter is zero again for the next call
+      ncand[b] = counts[b];
+      counts[b] = 0;
+    }
+  }
 }
 
 }  // namespace
@@ -312,7 +326,7 @@ DMY_API int dmy_nms_candidates(const float* pred, int nimg, int A, int no, float
 DMY_API int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, int nimg, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   dim3 gp(grid_cap(ceil_div(cap, 256), 1024), nimg);
-  pad_keys_kernel<<<gp, 256, 0, st>>>(keys, cap, counts, nimg);
+  if (cap > 2048) pad_keys_kernel<<<gp, 256, 0, st>>>(keys, cap, counts, nimg);  // cap 2048: bitonic_local pads
   dim3 gl((unsigned)(cap / 2048), nimg);
   bitonic_local_kernel<<<gl, 1024, 0, st>>>(keys, cap, 2, 2048, counts);
   for (long k = 4096; k <= cap; k <<= 1) {
@@ -323,11 +337,12 @@ DMY_API int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, 
 }
 
 DMY_API int dmy_nms_greedy(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det,
-                           int max_nms, const unsigned long long* keys, long cap, const int* counts, float* boxes,
-                           float* out, int* nkeep, void* stream) {
+                           int max_nms, const unsigned long long* keys, long cap, int* counts, float* boxes,
+                           float* out, int* nkeep, int* ncand, void* stream) {
   NmsCfg cfg{A, no, no - 5, 0.f, iou, 0, agnostic, max_det, max_nms, nullptr};
   const size_t lds = sizeof(unsigned long long) * (size_t)((max_nms + 63) / 64);
-  nms_greedy_kernel<<<nimg, 1024, lds, (hipStream_t)stream>>>(pred, cfg, keys, cap, counts, boxes, out, nkeep);
+  nms_greedy_kernel<<<nimg, 1024, lds, (hipStream_t)stream>>>(pred, cfg, keys, cap, counts, boxes, out, nkeep,
+                                                                ncand);
   return (int)hipGetLastError();
 }
 
@@ -335,13 +350,14 @@ DMY_API int dmy_nms_mask_rows() { return kMaskCap; }
 
 // the bitmask path: cap (the sort capacity) <= dmy_nms_mask_rows(); mask holds nimg * cap * cap / 64 words
 DMY_API int dmy_nms_greedy_mask(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det,
-                                int max_nms, const unsigned long long* keys, long cap, const int* counts, float* boxes,
-                                unsigned long long* mask, float* out, int* nkeep, void* stream) {
+                                int max_nms, const unsigned long long* keys, long cap, int* counts, float* boxes,
+                                unsigned long long* mask, float* out, int* nkeep, int* ncand, void* stream) {
   if (cap > kMaskCap || cap % 64 != 0) return (int)hipErrorInvalidValue;
   NmsCfg cfg{A, no, no - 5, 0.f, iou, 0, agnostic, max_det, max_nms, nullptr};
   hipStream_t st = (hipStream_t)stream;
-  nms_boxes_kernel<<<dim3(grid_cap(ceil_div(cap, 256), 64), nimg), 256, 0, st>>>(pred, cfg, keys, cap, counts, boxes);
-  nms_mask_kernel<<<dim3((unsigned)(cap / 64), (unsigned)(cap / 64), nimg), 64, 0, st>>>(cfg, cap, counts, boxes, mask);
-  nms_scan_kernel<<<nimg, 64, 0, st>>>(pred, cfg, keys, cap, counts, mask, out, nkeep);
+  (void)boxes;  // the mask kernel makes its boxes from the keys (the lazy path's scratch; kept in the ABI)
+  nms_mask_kernel<<<dim3((unsigned)(cap / 64), (unsigned)(cap / 64), nimg), 64, 0, st>>>(pred, cfg, keys, cap, counts,
+                                                                                          mask);
+  nms_scan_kernel<<<nimg, 64, 0, st>>>(pred, cfg, keys, cap, counts, mask, out, nkeep, ncand);
   return (int)hipGetLastError();
 }

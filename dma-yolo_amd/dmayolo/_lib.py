@@ -73,6 +73,7 @@ SIGNATURES = {
     'dmy_colsum2': [P, P, L, I, P, P, P],
     # eltwise.hip
     'dmy_maxpool_fwd': [I, P, L, P, L, P, I, I, I, I, I, P],
+    'dmy_maxpool_chain3_fwd': [I, P, L, P, P, P, L, I, I, I, I, I, P],
     'dmy_maxpool_bwd': [I, P, L, P, P, L, I, I, I, I, I, I, P],
     'dmy_avgpool_fwd': [I, P, L, P, I, I, I, I, I, P],
     'dmy_avgpool_bwd': [I, P, P, L, I, I, I, I, I, I, P],
@@ -97,6 +98,7 @@ SIGNATURES = {
     'dmy_cast': [I, I, P, P, L, F, P],
     # detect_loss.hip
     'dmy_detect_decode': [I, P, L, L, L, I, I, I, I, I, F, P, P, L, L, P],
+    'dmy_detect_decode_levels': [I, I, P, P, P, P, I, I, I, P, P, L, P],
     'dmy_build_targets': [P, I, P, I, I, I, F, P, P, P, P, P, P, P, P, P],
     'dmy_yolo_loss_part_rows': [],
     'dmy_yolo_loss_level': [I, P, L, L, L, L, I, I, I, I, I, I, F, F, F, F, F, F, F, F, F, P, P, P, P, P, P, P, P,
@@ -127,9 +129,9 @@ SIGNATURES = {
     # nms.hip
     'dmy_nms_candidates': [P, I, I, I, F, I, P, P, L, P, P],
     'dmy_nms_sort': [P, L, P, I, P],
-    'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P],
+    'dmy_nms_greedy': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P, P],
     'dmy_nms_mask_rows': [],
-    'dmy_nms_greedy_mask': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P, P],
+    'dmy_nms_greedy_mask': [P, I, I, I, F, I, I, I, P, L, P, P, P, P, P, P, P],
     # metrics.hip
     'dmy_process_batch': [P, P, P, P, I, P, I, P, P, P, P, P],
     # swin.hip

@@ -953,6 +953,36 @@ class MaxPoolFn(torch.autograd.Function):
         return sink_result(ctx.sink, buf), None, None, None
 
 
+POOL3 = [os.environ.get('DMY_POOL3', '1') == '1']  # the one-launch pyramid (DMY_POOL3=0: three MaxPoolFn launches)
+
+
+def maxpool_chain3(x, k, outs=(None, None, None)):
+    """inference SPPF / SPPFCSPC pyramid: (pool(x), pool(pool(x)), pool(pool(pool(x)))) with the k x k stride-1 pool in
+    ONE launch (dmy_maxpool_chain3_fwd, the bits of three MaxPoolFn launches), written into `outs` when they are three
+    NHWC views with one pixel stride (concat_buffer slices), else into fresh tensors.  None when autograd is recording
+    (the backward needs MaxPoolFn's argmax) or the kernel does not take the shape: the caller chains MaxPoolFn"""
+    if torch.is_grad_enabled() or k not in (3, 5) or x.dtype not in (torch.bfloat16, torch.float32) or not POOL3[0]:
+        return None
+    x, xps = pixel_stride(x)
+    N, C, H, W = x.shape
+    vw = 8 if x.dtype == torch.bfloat16 else 4
+    ys, yps = [], None
+    for o in outs:
+        if o is None or tuple(o.shape) != (N, C, H, W) or o.dtype != x.dtype or pixel_stride(o)[0] is not o or \
+                (yps is not None and pixel_stride(o)[1] != yps):
+            ys = None
+            break
+        yps = pixel_stride(o)[1]
+        ys.append(o)
+    if ys is None:
+        ys, yps = [new_act(N, C, H, W, x) for _ in range(3)], C
+    if C % vw or xps % vw or yps % vw or N * (C // vw) >= 65536 or any(t.data_ptr() % 16 for t in [x] + ys):
+        return None
+    call('dmy_maxpool_chain3_fwd', dcode(x), ptr(x), xps, ptr(ys[0]), ptr(ys[1]), ptr(ys[2]), yps, N, H, W, C, k,
+         stream())
+    return tuple(ys)
+
+
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, sink=None):

@@ -49,11 +49,16 @@ class GraphedDetector:
         self._capture(x)  # warm-up forwards fill every per-layer cache; the forward-only graph stays usable
         z = self.static_out[0]
         pred, plan = nms_prepare(z, **nms_args)  # NMS plan from the recorded output's shape (the cap hint)
-        for _ in range(self.warmup):  # the NMS path's own allocations, outside the capture
-            nms_launch(pred, plan)
+        # the NMS path's own allocations, outside the capture, on the capture stream itself (its self-resetting
+        # candidate counter is per stream: made here, the graph records no fill for it)
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            for _ in range(self.warmup):
+                nms_launch(pred, plan)
         torch.cuda.synchronize()
         self.dgraph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.dgraph), torch.no_grad():
+        with torch.cuda.graph(self.dgraph, stream=cs), torch.no_grad():
             out = self.model(self.static_in)
             dpred = out[0].detach().float().contiguous()  # nms_prepare's conversion (the plan, cls_ok included, is made)
             self.dstate = (out, plan, plan['cap']) + nms_launch(dpred, plan)

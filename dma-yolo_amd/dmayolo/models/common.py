@@ -202,6 +202,9 @@ class SPPF(nn.Module):
         else:
             sl = [None] * 4
         x = self.cv1(x, out=sl[0])
+        ys = Fn.maxpool_chain3(x, k, sl[1:])  # inference: the three pools in one launch
+        if ys is not None:
+            return self.cv2(Fn.ConcatFn.apply(None, 0.0, None, x, *ys))
         s0, s1, s2 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)  # each pool input -> next pool + concat
         y1 = Fn.MaxPoolFn.apply(x, k, s0, sl[1:2])
         y2 = Fn.MaxPoolFn.apply(y1, k, s1, sl[2:3])
@@ -237,11 +240,15 @@ class SPPFCSPC(nn.Module):
             sl, s2l = [None] * 4, [None] * 2
         sx = Fn.GradSink(2)  # x -> cv1 and cv2
         x1 = self.cv4(self.cv3(self.cv1(x, xsink=sx)), out=sl[0])
-        s1, s2, s3 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)
-        x2 = Fn.MaxPoolFn.apply(x1, k, s1, sl[1:2])
-        x3 = Fn.MaxPoolFn.apply(x2, k, s2, sl[2:3])
-        y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, (s1, s2, s3, None), x1, x2, x3,
-                                                 Fn.MaxPoolFn.apply(x3, k, s3, sl[3:4]))), out=s2l[0])
+        ys = Fn.maxpool_chain3(x1, k, sl[1:])  # inference: the three pools in one launch
+        if ys is not None:
+            y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, None, x1, *ys)), out=s2l[0])
+        else:
+            s1, s2, s3 = Fn.GradSink(2), Fn.GradSink(2), Fn.GradSink(2)
+            x2 = Fn.MaxPoolFn.apply(x1, k, s1, sl[1:2])
+            x3 = Fn.MaxPoolFn.apply(x2, k, s2, sl[2:3])
+            y1 = self.cv6(self.cv5(Fn.ConcatFn.apply(None, 0.0, (s1, s2, s3, None), x1, x2, x3,
+                                                     Fn.MaxPoolFn.apply(x3, k, s3, sl[3:4]))), out=s2l[0])
         y2 = self.cv2(x, xsink=sx, out=s2l[1])
         return self.cv7(Fn.ConcatFn.apply(None, 0.0, None, y1, y2))
 

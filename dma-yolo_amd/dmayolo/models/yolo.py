@@ -6,6 +6,7 @@ Differences from the reference that do not change results:
     (parity is anchored on state_dict transfer, SURVEY §0.6);
   * activations are NHWC in `Model.act_dtype` (float32 parity / bfloat16 throughput).
 """
+import ctypes
 import math
 import os
 import weakref
@@ -68,6 +69,15 @@ class Detect(nn.Module):
         sl = getattr(self, 'stride_list', None)
         if not sl or len(sl) != len(out):  # host copy of the strides: no device sync per forward (graph-capturable)
             sl = self.stride_list = [float(v) for v in self.stride.cpu()]
+        if len(out) <= 4 and len({p.dtype for p in out}) == 1:  # every level in one launch
+            nl, (_, na, _, _, no) = len(out), out[0].shape
+            ys = (ctypes.c_void_p * nl)(*[p.data_ptr() for p in out])
+            st = (ctypes.c_long * (3 * nl))(*[v for p in out for v in (p.stride(0), p.stride(2), p.stride(3))])
+            hw = (ctypes.c_int * (2 * nl))(*[v for p in out for v in (p.shape[2], p.shape[3])])
+            ls = (ctypes.c_float * nl)(*sl)
+            call('dmy_detect_decode_levels', dcode(out[0]), nl, ys, st, hw, ls, bs, na, no, ptr(anchors), ptr(z), total,
+                 stream())
+            return z
         for i, p in enumerate(out):
             _, na, ny, nx, no = p.shape
             s = p.stride()

@@ -106,21 +106,39 @@ def nms_launch(pred, plan, cap=None):
     dev = pred.device
     cap = plan['cap'] if cap is None else cap
     max_nms = 30000
-    cnt = torch.zeros(2 * nimg, dtype=torch.int32, device=dev)
+    ctr = _nms_counter(dev, nimg)  # zero on entry; the greedy launch hands the counts to cnt and re-zeroes it
+    cnt = torch.empty(2 * nimg, dtype=torch.int32, device=dev)
     keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
     call('dmy_nms_candidates', ptr(pred), nimg, A, no, plan['conf'], int(plan['multi']), ptr(plan['cls_ok']), ptr(keys),
-         cap, ptr(cnt), stream())
-    call('dmy_nms_sort', ptr(keys), cap, ptr(cnt), nimg, stream())
-    boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
+         cap, ptr(ctr), stream())
+    call('dmy_nms_sort', ptr(keys), cap, ptr(ctr), nimg, stream())
     out = torch.empty((nimg, plan['max_det'], 6), dtype=torch.float32, device=dev)
     if cap <= _mask_cap():  # IoU bitmask + one-wave scan (same keep set and order as the lazy greedy kernel)
         mask = torch.empty(nimg * cap * (cap // 64), dtype=torch.int64, device=dev)
         call('dmy_nms_greedy_mask', ptr(pred), nimg, A, no, plan['iou'], int(plan['agnostic']), plan['max_det'],
-             max_nms, ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(mask), ptr(out), ptr(cnt[nimg:]), stream())
+             max_nms, ptr(keys), cap, ptr(ctr), None, ptr(mask), ptr(out), ptr(cnt[nimg:]), ptr(cnt), stream())
     else:
+        boxes = torch.empty((nimg, max_nms, 5), dtype=torch.float32, device=dev)
         call('dmy_nms_greedy', ptr(pred), nimg, A, no, plan['iou'], int(plan['agnostic']), plan['max_det'], max_nms,
-             ptr(keys), cap, ptr(cnt), ptr(boxes), ptr(out), ptr(cnt[nimg:]), stream())
+             ptr(keys), cap, ptr(ctr), ptr(boxes), ptr(out), ptr(cnt[nimg:]), ptr(cnt), stream())
     return cnt, out
+
+
+_NMS_CTR = {}
+
+
+def _nms_counter(dev, nimg):
+    """the candidate counter of the current stream: int32 [>= nimg], zero between calls (the greedy launch of each call
+    copies the counts out and re-zeroes it), so a call needs no fill launch.  One per (device, stream): calls on two
+    streams never share it.  Created (zeroed) outside graph capture when possible; one created during a capture is
+    zeroed by a fill recorded in that graph"""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    t = _NMS_CTR.get(key)
+    if t is None or t.numel() < nimg:
+        t = torch.zeros(max(nimg, 64), dtype=torch.int32, device=dev)
+        if not torch.cuda.is_current_stream_capturing():
+            _NMS_CTR[key] = t
+    return t
 
 
 def nms_finish(plan, cap, cnt, out):

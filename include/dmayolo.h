@@ -163,6 +163,10 @@ int dmy_maxpool_fwd(int dtype, const void* x, long xps, void* y, long yps, unsig
                     int C, int k, void* stream);
 int dmy_maxpool_bwd(int dtype, const void* dy, long dps, const unsigned char* argmax, void* dx, long dxps,
                     int accumulate, int N, int H, int W, int C, int k, void* stream);
+/* inference SPPF / SPPFCSPC pyramid (common.py:250-258, :1266-1274 under no_grad): y1 = pool(x), y2 = pool(y1),
+   y3 = pool(y2) in one launch, bit-identical to three dmy_maxpool_fwd calls; k 3 or 5, 16-B vectors, no argmax */
+int dmy_maxpool_chain3_fwd(int dtype, const void* x, long xps, void* y1, void* y2, void* y3, long yps, int N, int H,
+                           int W, int C, int k, void* stream);
 /* nn.AvgPool2d(r, r): SCConv.k2[0] common.py:1282 */
 int dmy_avgpool_fwd(int dtype, const void* x, long xps, void* y, int N, int H, int W, int C, int r, void* stream);
 int dmy_avgpool_bwd(int dtype, const void* dy, void* dx, long dxps, int accumulate, int N, int H, int W, int C, int r,
@@ -216,6 +220,13 @@ int dmy_cast(int src_kind, int dst_kind, const void* x, void* y, long n, float s
 /* ---- Detect decode (models/yolo.py:78-101) and ComputeLoss (utils/loss.py:167-276, metrics.py:192-235) */
 int dmy_detect_decode(int dtype, const void* y, long sb, long sh, long sw, int N, int H, int W, int na, int no,
                       float stride, const float* anchors, float* z, long zoff, long ztotal, void* stream);
+/* every level of one Detect forward in one launch (yolo.py:63-76 under eval): level l's NHWC head output ys[l] with
+   element strides strides[3l .. 3l+2] = (batch, row, col), hw[2l], hw[2l+1] = its H, W, lvl_stride[l] its stride,
+   anchors [nl][na][2] (device); z rows of level l start at the sum of the earlier levels' na*H*W.  The bits of one
+   dmy_detect_decode per level */
+int dmy_detect_decode_levels(int dtype, int nl, const void* const* ys, const long* strides, const int* hw,
+                             const float* lvl_stride, int N, int na, int no, const float* anchors, float* z, long ztotal,
+                             void* stream);
 int dmy_build_targets(const float* targets, int nt, const float* anchors, int na, int H, int W, float anchor_t,
                       int* b, int* a, int* gj, int* gi, int* tcls, float* tbox, float* anch, int* count,
                       void* stream);
@@ -238,14 +249,17 @@ int dmy_siou_eval(const float* b1, const float* b2, float* iou, float* grad_b1, 
 int dmy_nms_candidates(const float* pred, int nimg, int A, int no, float conf, int multi_label,
                        const unsigned char* class_ok, unsigned long long* keys, long cap, int* counts, void* stream);
 int dmy_nms_sort(unsigned long long* keys, long cap, const int* counts, int nimg, void* stream);
+/* ncand (nullable): the greedy launch also writes each image's candidate count there and re-zeroes counts[b], so a
+   persistent counts buffer is zero for the next dmy_nms_candidates without a fill launch */
 int dmy_nms_greedy(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det, int max_nms,
-                   const unsigned long long* keys, long cap, const int* counts, float* boxes, float* out, int* nkeep,
-                   void* stream);
-/* the same greedy keep set / order through an IoU bitmask (cap <= dmy_nms_mask_rows(); mask: nimg * cap * cap / 64 words) */
+                   const unsigned long long* keys, long cap, int* counts, float* boxes, float* out, int* nkeep,
+                   int* ncand, void* stream);
+/* the same greedy keep set / order through an IoU bitmask (cap <= dmy_nms_mask_rows(); mask: nimg * cap * cap / 64 words;
+   boxes is not used: the mask kernel makes each box from its key) */
 int dmy_nms_mask_rows(void);
 int dmy_nms_greedy_mask(const float* pred, int nimg, int A, int no, float iou, int agnostic, int max_det, int max_nms,
-                        const unsigned long long* keys, long cap, const int* counts, float* boxes,
-                        unsigned long long* mask, float* out, int* nkeep, void* stream);
+                        const unsigned long long* keys, long cap, int* counts, float* boxes,
+                        unsigned long long* mask, float* out, int* nkeep, int* ncand, void* stream);
 
 /* ---- Swin / C3STR (models/common.py:452-654): LayerNorm, shifted-window attention core with the
  *      reference's mask semantics, per-sample DropPath scale (common.py:386-403) */

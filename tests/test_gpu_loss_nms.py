@@ -157,9 +157,17 @@ def test_nms_bitmask_path_vs_oracle(case):
                 ptr(keys), cap, ptr(cnt), ptr(boxes)]
         if fn.endswith('mask'):
             args.append(ptr(torch.empty(2 * cap * (cap // 64), dtype=torch.int64, device='cuda')))
-        call(fn, *args, ptr(o), ptr(nk), stream())
+        call(fn, *args, ptr(o), ptr(nk), None, stream())
         torch.cuda.synchronize()
         res.append([o[b, :int(nk[b])].cpu() for b in range(2)])
+        # the self-resetting counter form (ncand): the counts leave through ncand and the counter is zero afterwards
+        ctr, nc_out = cnt[:2].clone(), torch.full((2,), -1, dtype=torch.int32, device='cuda')
+        o2 = torch.full_like(o, float('nan'))
+        args2 = args[:10] + [ptr(ctr)] + args[11:]
+        call(fn, *args2, ptr(o2), ptr(nk), ptr(nc_out), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(nc_out, cnt[:2]) and not bool(ctr.any())
+        assert all(torch.equal(o2[b, :int(nk[b])].cpu(), res[-1][b]) for b in range(2))
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
@@ -168,7 +176,8 @@ def test_nms_bitmask_path_vs_oracle(case):
 def test_nms_sort_any_count(cap):
     """dmy_nms_sort (pad + bitonic network) leaves each image's first count keys ascending and pad keys after, for
     counts from 0 to cap: the first tile-local pass skips pad-only tiles and, at cap 2048, sorts only the pow2 prefix
-    holding the candidates (round 5); later passes must not skip (a descending merge moves real keys to a block end)"""
+    holding the candidates (round 5) and writes the pad keys itself (no pad launch); later passes must not skip (a
+    descending merge moves real keys to a block end)"""
     from dmayolo.functional import call, ptr, stream
     g = torch.Generator().manual_seed(cap)
     counts = [0, 1, 5, 100, 1000, 2047, 2048, min(3000, cap), min(5000, cap), cap]

@@ -269,6 +269,34 @@ def test_detect_module_vs_reference_golden(dtype):
         assert float((z.cpu() - ref).abs().max()) < 2e-2 * float(ref.abs().max())
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_detect_decode_one_launch_equals_per_level(dtype):
+    """Detect.decode's one launch over every level (dmy_detect_decode_levels) gives the bits of one dmy_detect_decode
+    per level, for strided (permuted NHWC head) level views and a batch of 2"""
+    from dmayolo.functional import call, ptr, stream, dcode
+    from dmayolo.models.yolo import Detect
+    torch.manual_seed(3)
+    d = Detect(7, [[10, 13, 16, 30, 33, 23], [30, 61, 62, 45, 59, 119], [116, 90, 156, 198, 373, 326]], (32, 64, 128))
+    d.stride = torch.tensor([8., 16., 32.])
+    d = d.cuda().eval()
+    xs = [torch.randn(2, c, 80 // s, 72 // s, device='cuda').to(dtype).contiguous(memory_format=torch.channels_last)
+          for c, s in ((32, 1), (64, 2), (128, 4))]
+    with torch.no_grad():
+        z, out = d(xs)
+    total = sum(d.na * p.shape[2] * p.shape[3] for p in out)
+    ref = torch.empty_like(z)
+    anchors = d.anchors.float().contiguous()
+    off = 0
+    for i, p in enumerate(out):
+        _, na, ny, nx, no = p.shape
+        sd = p.stride()
+        call('dmy_detect_decode', dcode(p), ptr(p), sd[0], sd[2], sd[3], 2, ny, nx, na, no, float(d.stride[i]),
+             ptr(anchors[i]), ptr(ref), off, total, stream())
+        off += na * ny * nx
+    torch.cuda.synchronize()
+    assert torch.equal(z.view(torch.int32), ref.view(torch.int32))
+
+
 def test_jit_trace_like_reference_logger():
     """Missing-item #7 of round 1: the reference's train.py logs the graph at the first batch with
     torch.jit.trace(de_parallel(model), imgs[0:1], strict=False) (utils/loggers/__init__.py:86, plots on by default).

@@ -63,6 +63,37 @@ def test_maxpool_vs_aten(dtype, k, N, C, H, W, extra):
 
 
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('k', [3, 5])
+@pytest.mark.parametrize('N,C,H,W', [(1, 256, 20, 20), (2, 16, 37, 53), (1, 64, 48, 48), (2, 8, 5, 70), (2, 256, 45, 70)])
+def test_maxpool_chain3_equals_three_launches(dtype, k, N, C, H, W):
+    """the inference SPPF pyramid in one launch (dmy_maxpool_chain3_fwd) gives the bits of three chained
+    dmy_maxpool_fwd launches, into three channel slices of one concat buffer, with signed zeros and NaNs among the
+    ties (the update rule's order decides which zero survives)"""
+    call, ptr, stream = _lib()
+    gen = torch.Generator().manual_seed(k * 10 + C + H)
+    dt = 1 if dtype == torch.bfloat16 else 0
+    xs = _grid_values((N, H, W, C), gen)
+    xs[xs == 0.25] = -0.0
+    xs.view(-1)[torch.randint(0, xs.numel(), (3,), generator=gen)] = float('nan')
+    x = xs.to(dtype).cuda()
+    cat = torch.full((N, H, W, 4 * C), 7.0, dtype=dtype, device='cuda')
+    call('dmy_maxpool_chain3_fwd', dt, ptr(x), C, ptr(cat[..., C:]), ptr(cat[..., 2 * C:]), ptr(cat[..., 3 * C:]),
+         4 * C, N, H, W, C, k, stream())
+    ref, cur = [], x
+    arg = torch.empty(N, H, W, C, dtype=torch.uint8, device='cuda')
+    for _ in range(3):
+        y = torch.empty(N, H, W, C, dtype=dtype, device='cuda')
+        call('dmy_maxpool_fwd', dt, ptr(cur), C, ptr(y), C, ptr(arg), N, H, W, C, k, stream())
+        ref.append(y)
+        cur = y
+    torch.cuda.synchronize()
+    iv = torch.int16 if dtype == torch.bfloat16 else torch.int32
+    for i in range(3):
+        assert torch.equal(cat[..., (i + 1) * C:(i + 2) * C].contiguous().view(iv), ref[i].view(iv)), i
+    assert bool((cat[..., :C] == 7.0).all())  # the first slice is not touched
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize('N,C,H,W', [(2, 16, 120, 97), (3, 40, 9, 7), (1, 6, 64, 300), (2, 512, 30, 30)])
 def test_gpool_vs_aten(dtype, N, C, H, W):
     call, ptr, stream = _lib()
