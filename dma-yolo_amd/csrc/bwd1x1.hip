@@ -328,6 +328,9 @@ int num_cus() {
 // the prefetch point) measured 1-11 % SLOWER on every shape (profiles/r05/bwd1x1_depth2_ab.log): the PMC passes show
 // these launches issue-bound (~50 % of wave cycles issuing, 25-39 % waiting, profiles/r05/pmc_bwd1x1.txt), not
 // starved for loads in flight
+// An 8-wave single block per tile for the K = 256 layers (no column split, the transform once; 4 x 2 or 2 x 4 wave grid)
+// does not fit: 2 waves per SIMD leave 256 registers per wave, and the kernel's working set besides the weight-grad
+// accumulators is ~290 (63-80 VGPRs spilled at 256 x 256 / 256 x 128), so it was not built
 struct Plan {
   int cb, tp, px;
 };
