@@ -517,6 +517,20 @@ inline int vec_grid(long M, int C, int VW) {
   const int RB = 256 / (C / VW);
   return grid_cap(ceil_div(M, (long)RB * 8), cap);
 }
+// the grid caps of the streaming passes, measured per kind (tools/gpu/bw_micro.py, profiles/r05/bn_grid_ab.log, M x C =
+// 1.18M x 128 and 295k x 512 bf16): the reduce passes (bn_stats, bn_bwd_reduce: per-block partial rows) are fastest at
+// 2048 blocks (5.0 -> 5.5 TB/s: fewer partial rows to write and sum), the elementwise ones (bn_act_fwd, bn_bwd_apply)
+// at 16384 (apply 4.7 -> 5.2 TB/s, act 5.3 -> 5.5: more rows in flight per CU).  DMY_BN_GRID_RED / DMY_BN_GRID_EW
+inline int vec_grid_red(long M, int C, int VW) {
+  static const int cap = env_knob("DMY_BN_GRID_RED", 2048);
+  const int RB = 256 / (C / VW);
+  return grid_cap(ceil_div(M, (long)RB * 8), cap);
+}
+inline int vec_grid_ew(long M, int C, int VW) {
+  static const int cap = env_knob("DMY_BN_GRID_EW", 16384);
+  const int RB = 256 / (C / VW);
+  return grid_cap(ceil_div(M, (long)RB * 8), cap);
+}
 // row order of the streaming passes, as a bit mask (DMY_BN_ORDER): 1 = bn_act_fwd, 2 = bn_bwd_reduce, 4 = bn_bwd_apply
 // walk M from the END.  A pass that reads a tensor in the reverse of the order its producer (or the previous pass)
 // touched it starts on the lines still resident in the 256 MiB Infinity Cache instead of the ones evicted first:
@@ -544,7 +558,7 @@ DMY_API int dmy_bn_partial_rows(long M) {
 DMY_API int dmy_bn_stats(int dtype, const void* z, long zps, long M, int C, float* psum, float* psq, void* stream) {
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, 0, 0, z, nullptr, nullptr) && C / VW <= 256) {
-    const int g = vec_grid(M, C, VW);
+    const int g = vec_grid_red(M, C, VW);
     hipStream_t st = (hipStream_t)stream;
     if (dtype) bn_bwd_reduce_vec<bf16, true><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq, 0);
     else bn_bwd_reduce_vec<float, true><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)z, zps, nullptr, nullptr, nullptr, nullptr, 0, M, C, psum, psq, 0);
@@ -579,7 +593,7 @@ DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scal
   const int VW = dtype ? 8 : 4;
   const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res) && C / VW <= 256;
   if (vec) {
-    const int g = vec_grid(M, C, VW);
+    const int g = vec_grid_ew(M, C, VW);
 #define ACT_GO(U_, ...) bn_act_fwd_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C, bn_order() & 1)
     if (dtype) { BN_UNROLL(ACT_GO, 0) }
 #undef ACT_GO
@@ -610,7 +624,7 @@ DMY_API int dmy_bn_act_fwd_f8(const void* z, long zps, const float* scale, const
 // Partial rows written by dmy_bn_bwd_reduce / dmy_bn_stats for these exact arguments.
 DMY_API int dmy_bn_reduce_rows(int dtype, const void* z, long zps, const void* dy, long dps, long M, int C) {
   const int VW = dtype ? 8 : 4;
-  if (vec_ok(VW, C, zps, dy ? dps : 0, 0, z, dy, nullptr) && C / VW <= 256) return vec_grid(M, C, VW);
+  if (vec_ok(VW, C, zps, dy ? dps : 0, 0, z, dy, nullptr) && C / VW <= 256) return vec_grid_red(M, C, VW);
   return dmy_bn_partial_rows(M);
 }
 
@@ -620,7 +634,7 @@ DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy
   hipStream_t st = (hipStream_t)stream;
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, 0, z, dy, nullptr) && C / VW <= 256) {
-    const int g = vec_grid(M, C, VW);
+    const int g = vec_grid_red(M, C, VW);
 #define RED_GO(U_, ...) bn_bwd_reduce_vec<bf16, false, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, (bn_order() >> 1) & 1)
     if (dtype) { BN_UNROLL(RED_GO, 0) }
 #undef RED_GO
@@ -661,7 +675,7 @@ DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy,
   hipStream_t st = (hipStream_t)stream;
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, dzps, z, dy, dz) && C / VW <= 256) {
-    const int g = vec_grid(M, C, VW);
+    const int g = vec_grid_ew(M, C, VW);
 #define APP_GO(U_, ...) bn_bwd_apply_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C, (bn_order() >> 2) & 1)
     if (dtype) { BN_UNROLL(APP_GO, 0) }
 #undef APP_GO
