@@ -21,6 +21,8 @@ for cfg in ${CFGS:-dma-1536 v5s-640}; do
     rc=$?; echo "stats $cfg rc=$rc"; [ $rc -ne 0 ] && exit $rc
   fi
   [ -n "$NOPMC" ] && continue
+  # the counter passes run 1 + 1 steps: the profiler's packet callback reads past its ring on longer runs
+  PARGS="--config $cfg --also none --steps ${PSTEPS:-1} --warmup ${PWARM:-1} --no-cpu-baseline --no-detect"
   for pass in ${PASSES:-fetch write mfma}; do
     case $pass in
       fetch) ctr="FETCH_SIZE";;
@@ -28,7 +30,8 @@ for cfg in ${CFGS:-dma-1536 v5s-640}; do
       mfma) ctr="SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES";;
     esac
     out=$GRAFT_REPO_ROOT/$OUT/pmc_${cfg}_$pass
-    (cd /tmp && export DMY_SEGV_REPORT=1 HIP_FORCE_DEV_KERNARG=${KARG:-1} && timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $ctr -d $out -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py $ARGS > $out.log 2>&1)
+    SEGV=""; [ -f tools/segv/libsegv_report.so ] && SEGV=1
+    (cd /tmp && export DMY_SEGV_REPORT=$SEGV HIP_FORCE_DEV_KERNARG=${KARG:-1} && timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $ctr -d $out -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py $PARGS > $out.log 2>&1)
     rc=$?; echo "pmc $cfg $pass rc=$rc"; [ $rc -ne 0 ] && { grep -A12 "\[segv\]" $out.log | head -30; tail -5 $out.log; exit $rc; }
   done
 done
