@@ -100,14 +100,17 @@ def nms_prepare(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnos
 
 def nms_launch(pred, plan, cap=None):
     """the NMS kernels of one call at sort capacity `cap`, no host synchronisation (so it can be recorded into a HIP
-    graph, infer.GraphedDetector.detect): returns (cnt, out) -- cnt = [candidate counts | keep counts] (int32, device),
+    graph, infer.GraphedDetector.detect): returns (cnt, out) -- cnt = [candidate counts | keep counts] (int32, in the
+    stream's pinned host buffer; a device tensor inside a capture that has none),
     out = (nimg, max_det, 6) rows; nms_finish reads them"""
     nimg, A, no = pred.shape
     dev = pred.device
     cap = plan['cap'] if cap is None else cap
     max_nms = 30000
     ctr = _nms_counter(dev, nimg)  # zero on entry; the greedy launch hands the counts to cnt and re-zeroes it
-    cnt = torch.empty(2 * nimg, dtype=torch.int32, device=dev)
+    cnt = _nms_host_counts(dev, nimg)  # pinned host memory the scan writes directly: no read-back copy
+    if cnt is None:
+        cnt = torch.empty(2 * nimg, dtype=torch.int32, device=dev)
     keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
     call('dmy_nms_candidates', ptr(pred), nimg, A, no, plan['conf'], int(plan['multi']), ptr(plan['cls_ok']), ptr(keys),
          cap, ptr(ctr), stream())
@@ -125,6 +128,20 @@ def nms_launch(pred, plan, cap=None):
 
 
 _NMS_CTR = {}
+_NMS_HOST = {}
+
+
+def _nms_host_counts(dev, nimg):
+    """[candidate counts | keep counts] of the current stream's calls in pinned host memory (int32, 2 * nimg): the
+    greedy / scan kernels store them there, so nms_finish reads them after a stream synchronize instead of a device ->
+    host copy.  None during a graph capture that has no buffer yet (the device tensor is used then)"""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    t = _NMS_HOST.get(key)
+    if t is None or t.numel() < 2 * nimg:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = _NMS_HOST[key] = torch.zeros(max(2 * nimg, 64), dtype=torch.int32, pin_memory=True)
+    return t[:2 * nimg]
 
 
 def _nms_counter(dev, nimg):
@@ -145,6 +162,8 @@ def nms_finish(plan, cap, cnt, out):
     """the one host read of a launch: the per-image detections, or None when some image had more candidates than the
     sort capacity held (the caller reruns at the capacity this records as the new hint)"""
     nimg = out.shape[0]
+    if not cnt.is_cuda:  # pinned host counts written by the kernels: wait for them, read them in place
+        torch.cuda.current_stream(out.device).synchronize()
     h = cnt.tolist()  # the one host synchronisation
     need = max(h[:nimg])
     if need > cap:
