@@ -847,6 +847,46 @@ __global__ void dot_partial_kernel(const T* __restrict__ a, long aps, const T* _
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// BiFPN weighted-concat backward of one input in one pass over its dy slice: g (+)= scale * dy (slice_copy_kernel's
+// arithmetic) and the block partial of sum(dy * x) (dot_partial_kernel's, same grid-stride element order per thread),
+// reading dy once instead of once per kernel
+template <typename T>
+__global__ void slice_copy_dot_kernel(const T* __restrict__ dy, long dps, T* __restrict__ g, long gps,
+                                      const T* __restrict__ x, long xps, long M, int C, const float* __restrict__ wv,
+                                      int idx, int nw, float eps, int accumulate, float* __restrict__ part) {
+  constexpr int VW = Traits<T>::VW;
+  const float sc = bifpn_scale(wv, idx, nw, eps);
+  const int cv = C / VW;
+  const long total = M * cv;
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long m;
+    int c;
+    divmod(i, cv, m, c);
+    c *= VW;
+    float f[VW], xv[VW];
+    unpack<T>(*reinterpret_cast<const uint4*>(dy + m * dps + c), f);
+    unpack<T>(*reinterpret_cast<const uint4*>(x + m * xps + c), xv);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s += f[j] * xv[j];
+    if (accumulate) {
+      float o[VW];
+      unpack<T>(*reinterpret_cast<const uint4*>(g + m * gps + c), o);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] = f[j] * sc + o[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) f[j] *= sc;
+    }
+    *reinterpret_cast<uint4*>(g + m * gps + c) = pack<T>(f);
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 // dw_j = sum_i g_i * d(scale_i)/d(w_j),  scale_i = w_i / S, S = sum(w) + eps
 __global__ void bifpn_wgrad_kernel(const float* __restrict__ part, int nblk, int nw, const float* __restrict__ wv,
                                    float eps, float* __restrict__ dw) {
@@ -1469,6 +1509,18 @@ DMY_API int dmy_dot_partial(int dtype, const void* a, long aps, const void* b, l
   const int nb = dmy_dot_partial_blocks(M, C);
   const bool v = vec_ok(dtype, {C, aps, bps}, {a, b});
   DISPATCH_TV(dtype, v, dot_partial_kernel<T, NV><<<nb, 256, 0, st>>>((const T*)a, aps, (const T*)b, bps, M, C, part));
+  return (int)hipGetLastError();
+}
+// dmy_slice_copy (accumulate as given) + dmy_dot_partial(dy, x) in one launch; part gets dmy_dot_partial_blocks(M, C)
+// partials.  16-B vectors only (returns hipErrorInvalidValue otherwise: use the two calls)
+DMY_API int dmy_slice_copy_dot(int dtype, const void* dy, long dps, void* g, long gps, const void* x, long xps, long M,
+                               int C, const float* wv, int idx, int nw, float eps, int accumulate, float* part,
+                               void* stream) {
+  if (!vec_ok(dtype, {C, dps, gps, xps}, {dy, g, x})) return (int)hipErrorInvalidValue;
+  const int nb = dmy_dot_partial_blocks(M, C);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, slice_copy_dot_kernel<T><<<nb, 256, 0, st>>>((const T*)dy, dps, (T*)g, gps, (const T*)x, xps, M, C,
+                                                                  wv, idx, nw, eps, accumulate, part));
   return (int)hipGetLastError();
 }
 DMY_API int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* wv, float eps, float* dw, void* stream) {

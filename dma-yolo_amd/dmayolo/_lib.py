@@ -80,6 +80,7 @@ SIGNATURES = {
     'dmy_resize_fwd': [I, P, L, P, L, F, I, I, I, I, I, I, P],
     'dmy_resize_bwd': [I, P, L, P, L, I, I, I, I, I, I, P],
     'dmy_slice_copy': [I, P, L, P, L, L, I, P, I, I, F, I, P],
+    'dmy_slice_copy_dot': [I, P, L, P, L, P, L, L, I, P, I, I, F, I, P, P],
     'dmy_dot_partial_blocks': [L, I],
     'dmy_dot_partial': [I, P, L, P, L, L, I, P, P],
     'dmy_bifpn_wgrad': [P, I, I, P, F, P, P],

@@ -1027,6 +1027,9 @@ class ResizeFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+CAT_DOT = [os.environ.get('DMY_CAT_DOT', '1') == '1']  # weighted-concat backward in one pass per input
+
+
 class ConcatFn(torch.autograd.Function):
     """cat(w_i/(sum w + eps) * x_i) along channels (w=None: plain Concat)."""
 
@@ -1077,11 +1080,17 @@ class ConcatFn(torch.autograd.Function):
             x, xps = pixel_stride(x)
             g, gps, acc = sink_target(sinks[i], N, C, H, W, dy)
             sl = dy[:, c0:c0 + C]
-            call('dmy_slice_copy', dcode(dy), ptr(sl), dps, ptr(g), gps, M, C, ptr(w), i, len(xs), float(ctx.eps), acc,
-                 stream())
+            vw = 8 if dy.dtype == torch.bfloat16 else 4
+            if CAT_DOT[0] and C % vw == 0 and dps % vw == 0 and gps % vw == 0 and xps % vw == 0 and \
+                    all(t.data_ptr() % 16 == 0 for t in (sl, g, x)):  # one pass over the dy slice
+                call('dmy_slice_copy_dot', dcode(dy), ptr(sl), dps, ptr(g), gps, ptr(x), xps, M, C, ptr(w), i, len(xs),
+                     float(ctx.eps), acc, ptr(part[i]), stream())
+            else:
+                call('dmy_slice_copy', dcode(dy), ptr(sl), dps, ptr(g), gps, M, C, ptr(w), i, len(xs), float(ctx.eps),
+                     acc, stream())
+                call('dmy_dot_partial', dcode(dy), ptr(sl), dps, ptr(x), xps, M, C, ptr(part[i]), stream())
             g = sink_result(sinks[i], g)
             nbi = call('dmy_dot_partial_blocks', M, C)
-            call('dmy_dot_partial', dcode(dy), ptr(sl), dps, ptr(x), xps, M, C, ptr(part[i]), stream())
             if nbi < nb:
                 part[i, nbi:].zero_()
             grads.append(g)

@@ -182,6 +182,10 @@ int dmy_slice_copy(int dtype, const void* src, long sps, void* dst, long dps, lo
 int dmy_dot_partial_blocks(long M, int C);
 int dmy_dot_partial(int dtype, const void* a, long aps, const void* b, long bps, long M, int C, float* part,
                     void* stream);
+/* BiFPN weighted-concat backward of one input in one pass: dmy_slice_copy(dy -> g, scale, accumulate) and
+   dmy_dot_partial(dy, x -> part) reading dy once (16-B vectors; else hipErrorInvalidValue) */
+int dmy_slice_copy_dot(int dtype, const void* dy, long dps, void* g, long gps, const void* x, long xps, long M, int C,
+                       const float* wv, int idx, int nw, float eps, int accumulate, float* part, void* stream);
 int dmy_bifpn_wgrad(const float* part, int nblk, int nw, const float* w, float eps, float* dw, void* stream);
 /* SCConv gate k3(x) * sigmoid(x + up(k2(x))): common.py:1311-1314 */
 int dmy_scgate_fwd(int dtype, const void* x, long xps, const void* u3, const void* g, void* out, int N, int H, int W,

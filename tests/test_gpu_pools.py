@@ -122,3 +122,33 @@ def test_gpool_vs_aten(dtype, N, C, H, W):
     tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
     torch.testing.assert_close(o[:N], mean.detach().to(dtype).float(), rtol=tol, atol=tol)
     torch.testing.assert_close(dx.float().cpu(), xr.grad.permute(0, 2, 3, 1).to(dtype).float(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('M,C,acc', [(32 * 48 * 48, 256, 0), (3 * 37 * 41, 64, 1), (7, 16, 0)])
+def test_slice_copy_dot_equals_two_launches(dtype, M, C, acc):
+    """the BiFPN weighted-concat backward of one input in one pass (dmy_slice_copy_dot) gives the bits of
+    dmy_slice_copy + dmy_dot_partial: the scaled (accumulated) gradient slice and (bf16 operands) every block partial
+    of sum(dy * x)"""
+    call, ptr, stream = _lib()
+    gen = torch.Generator().manual_seed(M + C)
+    dt = 1 if dtype == torch.bfloat16 else 0
+    dyb = torch.randn(M, 3 * C, generator=gen).to(dtype).cuda()
+    dy = dyb[:, C:2 * C]
+    x = torch.randn(M, C, generator=gen).to(dtype).cuda()
+    g0 = torch.randn(M, C, generator=gen).to(dtype).cuda()
+    w = (torch.rand(3, generator=gen) + 0.5).cuda()
+    nb = call('dmy_dot_partial_blocks', M, C)
+    ga, gb = g0.clone(), g0.clone()
+    pa, pb = torch.zeros(nb, device='cuda'), torch.zeros(nb, device='cuda')
+    call('dmy_slice_copy_dot', dt, ptr(dy), 3 * C, ptr(ga), C, ptr(x), C, M, C, ptr(w), 1, 3, 1e-4, acc, ptr(pa), stream())
+    call('dmy_slice_copy', dt, ptr(dy), 3 * C, ptr(gb), C, M, C, ptr(w), 1, 3, 1e-4, acc, stream())
+    call('dmy_dot_partial', dt, ptr(dy), 3 * C, ptr(x), C, M, C, ptr(pb), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ga, gb)
+    if dtype == torch.bfloat16:
+        assert torch.equal(pa, pb)
+    else:  # fp32: the two kernels' products may contract into FMAs differently (last-ulp partials)
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-4)
+    ref = float((dy.double() * x.double()).sum())
+    assert abs(float(pa.double().sum()) - ref) <= 1e-3 * max(1.0, abs(ref))
