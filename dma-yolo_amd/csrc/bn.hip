@@ -719,6 +719,21 @@ DMY_API int dmy_reduce_rows(const float* part, int P, int C, float* out, int acc
 // bf16), one row per block, so k3's ConvBNActFn backward skips bn_bwd_reduce (functional.BnLink).  Thread layout of the
 // BN streaming kernels (RowMap: a thread owns one 8-channel vector and walks rows), rows in order: deterministic.
 namespace {
+// (w, h, image) of NHWC pixel m: 32-bit divisions whenever the pixel count fits (the gate kernels' per-row index math
+// was three 64-bit divisions per 8-channel vector)
+DEV void pix_hwb(long m, int W, int H, bool small, int& w, int& h, int& b) {
+  if (small) {
+    const unsigned u = (unsigned)m, q = u / (unsigned)W;
+    w = (int)(u - q * (unsigned)W);
+    b = (int)(q / (unsigned)H);
+    h = (int)(q - (unsigned)b * (unsigned)H);
+  } else {
+    w = (int)(m % W);
+    h = (int)((m / W) % H);
+    b = (int)(m / ((long)W * H));
+  }
+}
+
 DEV int nearest_src_bn(int d, int in, int out) {  // ATen nearest index rule (= eltwise.hip nearest_src)
   if (out == in) return d;
   if (out == 2 * in) return d >> 1;
@@ -740,8 +755,10 @@ __global__ void __launch_bounds__(256) scgate_bn_fwd_kernel(const bf16* __restri
   ldf<VW>(scale + c0, sc);
   ldf<VW>(shift + c0, sh);
   const long M = (long)N * H * W, S = (long)gridDim.x * rm.RB;
+  const bool small = M < (1L << 31);
   for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S) {
-    const int w = (int)(m % W), h = (int)((m / W) % H), b = (int)(m / ((long)W * H));
+    int w, h, b;
+    pix_hwb(m, W, H, small, w, h, b);
     const long gp = ((long)b * GH + nearest_src_bn(h, GH, H)) * GW + nearest_src_bn(w, GW, W);
     const uint4 xv = *reinterpret_cast<const uint4*>(x + m * xps + c0);
     const uint4 zv = *reinterpret_cast<const uint4*>(z + m * C + c0);
@@ -779,8 +796,10 @@ __global__ void __launch_bounds__(256) scgate_bn_bwd_kernel(
     ldf<VW>(mean + c0, mu);
     ldf<VW>(invstd + c0, is);
     const long M = (long)N * H * W, S = (long)gridDim.x * rm.RB;
+    const bool small = M < (1L << 31);
     for (long m = (long)blockIdx.x * rm.RB + rm.rr; m < M; m += S) {
-      const int w = (int)(m % W), h = (int)((m / W) % H), b = (int)(m / ((long)W * H));
+      int w, h, b;
+      pix_hwb(m, W, H, small, w, h, b);
       const long gp = ((long)b * GH + nearest_src_bn(h, GH, H)) * GW + nearest_src_bn(w, GW, W);
       const uint4 xv = *reinterpret_cast<const uint4*>(x + m * xps + c0);
       const uint4 zv = *reinterpret_cast<const uint4*>(z + m * C + c0);
