@@ -3460,10 +3460,10 @@ __global__ void __launch_bounds__(512) conv_wgrad_w(const bf16* __restrict__ x, 
 //   stage in flight across each barrier.  4 waves = 2 (m) x 2 (n), wave tile BM/2 x 144 (BM/32 x 9 MFMA frags).
 // Valid for KH = KW = 3, S = 1, P = 1, OH = H, OW = W, C % 32 == 0 (host-checked).  Split-K over patches; the
 // (tile, split) -> linear id mapping keeps a split's tiles on one XCD (they read the same patches).
-template <int BM>
+template <int BM, int NP = 1>  // NP halo planes of 32 input channels each (2: a block owns 64 input channels)
 struct WgradTapLds {
   static constexpr int BC = 32, PH = 8, PW = 8, HP = 12;  // halo pitch 12 (10 used)
-  static constexpr int A_BYTES = 64 * BM * 2, B_BYTES = 8 * 1024, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_BYTES = 64 * BM * 2, B_BYTES = NP * 8 * 1024, STAGE = A_BYTES + B_BYTES;
   static constexpr int APW = A_BYTES / 1024 / 4;           // dy pieces per wave (4 waves)
   static constexpr int SLOTS = BM / 8, RPP = 64 / SLOTS;   // 16-B slots per pixel row, pixel rows per piece
   __amdgpu_buffer_rsrc_t rx, rdy;
@@ -3527,7 +3527,10 @@ struct WgradTapLds {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const bool ok = bok[j] && (unsigned)(oy0 - 1 + by[j]) < (unsigned)H && (unsigned)(ox0 - 1 + bx[j]) < (unsigned)W;
-      blds16(rx, ok ? (unsigned)(xbase + brel[j] + bcol[j]) * 2u : kBufOob, stage + A_BYTES + (wid * 2 + j) * 1024);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        blds16(rx, ok ? (unsigned)(xbase + brel[j] + bcol[j] + 32 * pl) * 2u : kBufOob,
+               stage + A_BYTES + pl * 8192 + (wid * 2 + j) * 1024);
     }
     if (++px == npw) {
       px = 0;
@@ -3553,22 +3556,27 @@ DEV bf16x8 frag_halo(const bf16* Bs, int kh, int kw, int ch0, int k0, int lane) 
   return r;
 }
 
-template <int BM>
+// NP = 2 (layers with <= 64 output channels, BM = 64): a block owns 64 input channels (two halo planes) and its 4
+// waves are 1 (m) x 4 (n), wave tile BM x 144 (4 A + 9 B fragments per 36 MFMAs instead of 2 + 9 per 18): the
+// halo fragment reads, which bound the 64-channel layers on the LDS port, are amortised over twice the rows
+template <int BM, int NP = 1>
 __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                          float* __restrict__ dw, int kt_per_split, Geom g, int gm,
                                                          int gn, int nk_all, unsigned xbytes, unsigned dybytes,
                                                          int ff) {
-  using LD = WgradTapLds<BM>;
-  constexpr int NS = 3, STAGE = LD::STAGE, TM = BM / 32;  // 4 waves = 2 (m) x 2 (n); wave tile BM/2 x 144
-  constexpr int CTR = BM / 2, CTS = 288 + 4;               // epilogue: half the tile staged at a time
+  using LD = WgradTapLds<BM, NP>;
+  constexpr int NS = 3, STAGE = LD::STAGE;
+  constexpr int TM = NP == 2 ? BM / 16 : BM / 32;           // NP 1: 2 (m) x 2 (n) waves; NP 2: 1 x 4
+  constexpr int NCOL = 288 * NP;                            // tile columns: NP planes x 9 taps x 32 channels
+  constexpr int CTR = BM / 2, CTS = NCOL + 4;               // epilogue: half the tile staged at a time
   constexpr int LDSB = NS * STAGE > CTR * CTS * 4 ? NS * STAGE : CTR * CTS * 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDSB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = NP == 2 ? 0 : wid >> 1, wn = NP == 2 ? (wid & 1) : wid & 1, wpl = NP == 2 ? wid >> 1 : 0;
   const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int tile = lin % (gm * gn), split = lin / (gm * gn);
   const int tm = tile % gm, tc = tile / gm;  // out-channel tiles of one channel group adjacent (share the x halo)
-  const int m0 = tm * BM, c0 = tc * LD::BC;
+  const int m0 = tm * BM, c0 = tc * LD::BC * NP;
   const int kt0 = split * kt_per_split;
   const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
   f32x4 acc[TM][9];
@@ -3581,12 +3589,12 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
     ld.issue(smem, wid);
     if (nk > 1) ld.issue(smem + STAGE, wid);
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) vm_wait<LD::APW + 2>();
+      if (kt + 1 < nk) vm_wait<LD::APW + 2 * NP>();
       else vm_wait<0>();
       __builtin_amdgcn_s_barrier();
       if (!ff && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
-      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
+      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES + wpl * 8192);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         bf16x8 a[TM];
@@ -3613,19 +3621,23 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     __syncthreads();
-    if (wm == half) {
+    if (NP == 2 || wm == half) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        const int row = NP == 2 ? i * 16 - half * CTR : i * 16;  // row of the staged half
+        if (NP == 2 && (row < 0 || row >= CTR)) continue;
 #pragma unroll
         for (int j = 0; j < 9; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            ct[(i * 16 + 4 * (lane >> 4) + r) * CTS + (wn * 9 + j) * 16 + (lane & 15)] = acc[i][j][r];
+            ct[(row + 4 * (lane >> 4) + r) * CTS + wpl * 288 + (wn * 9 + j) * 16 + (lane & 15)] = acc[i][j][r];
+      }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < CTR * 288; e += 256) {
-      const int row = e / 288, col = e % 288, m = m0 + half * CTR + row;
-      const int n = (col >> 5) * g.C + c0 + (col & 31);  // col = tap * 32 + ci
+    for (int e = threadIdx.x; e < CTR * NCOL; e += 256) {
+      const int row = e / NCOL, col = e % NCOL, m = m0 + half * CTR + row;
+      const int pl = col / 288, cc = col % 288;
+      const int n = (cc >> 5) * g.C + c0 + pl * 32 + (cc & 31);  // cc = tap * 32 + ci
       if (m < g.K) wgrad_out(g, dw, split, (long)m * Ntot + wgrad_col(g, n), ct[row * CTS + col]);
     }
   }
@@ -4859,9 +4871,16 @@ inline bool wgrad_tap_ok(const Geom& g, const void* x, const void* dy) {
   static const long min_units = env_int("DMY_WGRAD_TAP_UNITS", 10000);
   return units >= min_units;
 }
-template <int BM>
+// DMY_WGRAD_TAP_NP: 2 (default) the <= 64-output-channel layers with C % 64 == 0 run the two-plane tile, 1 the one-plane
+// tile (read per launch: the tests compare both in one process)
+inline int wgrad_tap_np(const Geom& g) {
+  const char* e = getenv("DMY_WGRAD_TAP_NP");
+  const int np = e ? atoi(e) : 2;
+  return (np == 2 && g.K <= 64 && g.C % 64 == 0) ? 2 : 1;
+}
+template <int BM, int NP = 1>
 int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
-  const int gm = ceil_div(g.K, BM), gn = g.C / 32;
+  const int gm = ceil_div(g.K, BM), gn = g.C / (32 * NP);
   const int nk = g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8);  // 8 x 8 patches
   const int tiles = gm * gn;
   int maxs = nk / 8;
@@ -4874,7 +4893,7 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
     // two resident blocks per CU; ~1.1 us per patch step of the 128-row tile (288 MFMA per wave pair at ~45 %
     // of peak) and its 147 KiB fp32 tile of atomics per block at 1.3 TB/s (MI355X_MICROARCH.md §Global float
     // atomics); the 64-row tile halves both
-    const double R = 2.0 * num_cus(), f = BM / 128.0;
+    const double R = 2.0 * num_cus(), f = BM / 128.0 * NP;
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
       const double blocks = (double)tiles * sp;
@@ -4890,7 +4909,7 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * 9 * g.C, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
   static const int ff = env_int("DMY_TAP_FF", 0);
-  v3::conv_wgrad_tap<BM><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db, ff);
+  v3::conv_wgrad_tap<BM, NP><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db, ff);
   wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
@@ -4963,7 +4982,8 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const int v4 = wgrad_v4_mode();
     const double xb4 = 2.0 * ((double)g.N * g.H * g.W * g.xps), db4 = 2.0 * ((double)NP * g.yps);
     if (wgrad_tap_ok(g, x, dy))
-      return g.K <= 64 ? launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st)
+      return g.K <= 64 ? (wgrad_tap_np(g) == 2 ? launch_wgrad_tap<64, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                                               : launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st))
                        : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
         db4 < (double)v3::kBufOob) {

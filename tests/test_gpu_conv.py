@@ -158,6 +158,31 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
         assert torch.equal(y, first), i
 
 
+@pytest.mark.parametrize('N,C,H,W,K', [(16, 64, 160, 160, 64), (16, 64, 150, 146, 48), (10, 128, 128, 136, 32)])
+def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K, monkeypatch):
+    """3x3 s1 weight-grad of <= 64-output-channel layers on the tap-fused kernel, two halo planes (64 input channels per
+    block, DMY_WGRAD_TAP_NP=2, default) and one (=1): both against torch's fp32 conv2d_weight, and against each other"""
+    import os
+    from dmayolo.functional import call, ptr, stream
+    g = torch.Generator().manual_seed(N + C + K + H)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    dy = torch.randn(N, K, H, W, generator=g).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float().cuda(), (K, C, 3, 3), dy.float().cuda(), stride=1, padding=1)
+    xd = x.cuda().contiguous(memory_format=torch.channels_last)
+    dyd = dy.cuda().contiguous(memory_format=torch.channels_last)
+    out = {}
+    for np_ in ('2', '1'):
+        monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP', np_)
+        dwo = torch.empty(K * C * 9, device='cuda')
+        dw = torch.empty(K, C, 3, 3, device='cuda')
+        assert call('dmy_conv_wgrad', 1, ptr(xd), ptr(dyd), ptr(dwo), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K, stream()) == 0
+        call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, C, 3, 3, stream())
+        torch.cuda.synchronize()
+        out[np_] = dw
+        assert _rel(dw, ref) < 2e-3, (np_, _rel(dw, ref))
+    assert _rel(out['2'], out['1']) < 1e-4
+
+
 def test_conv_fwd_1x1_small_m_unsplit():
     from dmayolo.functional import call, ptr
     x = torch.empty(1, 256, 96, 96, dtype=torch.bfloat16, device='cuda', memory_format=torch.channels_last)
