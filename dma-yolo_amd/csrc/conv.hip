@@ -3560,7 +3560,7 @@ DEV bf16x8 frag_halo(const bf16* Bs, int kh, int kw, int ch0, int k0, int lane) 
 // waves are 1 (m) x 4 (n), wave tile BM x 144 (4 A + 9 B fragments per 36 MFMAs instead of 2 + 9 per 18): the
 // halo fragment reads, which bound the 64-channel layers on the LDS port, are amortised over twice the rows
 template <int BM, int NP = 1>
-__global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+__global__ void __launch_bounds__(256, (BM == 128 && NP == 2) ? 1 : 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                          float* __restrict__ dw, int kt_per_split, Geom g, int gm,
                                                          int gn, int nk_all, unsigned xbytes, unsigned dybytes,
                                                          int ff) {
@@ -3568,7 +3568,8 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
   constexpr int NS = 3, STAGE = LD::STAGE;
   constexpr int TM = NP == 2 ? BM / 16 : BM / 32;           // NP 1: 2 (m) x 2 (n) waves; NP 2: 1 x 4
   constexpr int NCOL = 288 * NP;                            // tile columns: NP planes x 9 taps x 32 channels
-  constexpr int CTR = BM / 2, CTS = NCOL + 4;               // epilogue: half the tile staged at a time
+  constexpr int NPASS = (BM == 128 && NP == 2) ? 4 : 2;    // epilogue: the tile staged in NPASS row slices
+  constexpr int CTR = BM / NPASS, CTS = NCOL + 4;
   constexpr int LDSB = NS * STAGE > CTR * CTS * 4 ? NS * STAGE : CTR * CTS * 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDSB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3595,7 +3596,8 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
       if (!ff && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
       const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES + wpl * 8192);
-#pragma unroll
+      constexpr int HU = (BM == 128 && NP == 2) ? 1 : 2;  // the 288-accumulator tile: one k half live at a time
+#pragma unroll HU
       for (int h = 0; h < 2; ++h) {
         bf16x8 a[TM];
 #pragma unroll
@@ -3619,7 +3621,7 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict_
   const int Ntot = 9 * g.C;
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < NPASS; ++half) {
     __syncthreads();
     if (NP == 2 || wm == half) {
 #pragma unroll
@@ -4878,6 +4880,14 @@ inline int wgrad_tap_np(const Geom& g) {
   const int np = e ? atoi(e) : 2;
   return (np == 2 && g.K <= 64 && g.C % 64 == 0) ? 2 : 1;
 }
+// DMY_WGRAD_TAP_NP128: 1 the > 64-output-channel layers with C % 64 == 0 run the two-plane 128-row tile (one block per
+// CU: 288 accumulator registers per lane), 0 (default) the one-plane tile.  Measured SLOWER: DMA-1536 158.25 ->
+// 154.9 img/s on one box (profiles/r05/wgrad_tap_np128_ab.log): one 4-wave block per CU hides too little latency
+inline int wgrad_tap_np128(const Geom& g) {
+  const char* e = getenv("DMY_WGRAD_TAP_NP128");
+  const int on = e ? atoi(e) : 0;
+  return (on == 1 && g.K > 64 && g.C % 64 == 0) ? 2 : 1;
+}
 template <int BM, int NP = 1>
 int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const int gm = ceil_div(g.K, BM), gn = g.C / (32 * NP);
@@ -4893,7 +4903,7 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
     // two resident blocks per CU; ~1.1 us per patch step of the 128-row tile (288 MFMA per wave pair at ~45 %
     // of peak) and its 147 KiB fp32 tile of atomics per block at 1.3 TB/s (MI355X_MICROARCH.md §Global float
     // atomics); the 64-row tile halves both
-    const double R = 2.0 * num_cus(), f = BM / 128.0 * NP;
+    const double R = ((BM == 128 && NP == 2) ? 1.0 : 2.0) * num_cus(), f = BM / 128.0 * NP;
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
       const double blocks = (double)tiles * sp;
@@ -4984,7 +4994,8 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     if (wgrad_tap_ok(g, x, dy))
       return g.K <= 64 ? (wgrad_tap_np(g) == 2 ? launch_wgrad_tap<64, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
                                                : launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st))
-                       : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st);
+                       : (wgrad_tap_np128(g) == 2 ? launch_wgrad_tap<128, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                                                  : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st));
     if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
         db4 < (double)v3::kBufOob) {
       if (wgrad_w_mode() && g.K >= 256 && Ntot >= 256)

@@ -158,12 +158,15 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
         assert torch.equal(y, first), i
 
 
-@pytest.mark.parametrize('N,C,H,W,K', [(16, 64, 160, 160, 64), (16, 64, 150, 146, 48), (10, 128, 128, 136, 32)])
+@pytest.mark.parametrize('N,C,H,W,K', [(16, 64, 160, 160, 64), (16, 64, 150, 146, 48), (10, 128, 128, 136, 32),
+                                       (16, 128, 100, 104, 128), (8, 256, 96, 96, 256), (10, 128, 96, 96, 192)])
 def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K, monkeypatch):
-    """3x3 s1 weight-grad of <= 64-output-channel layers on the tap-fused kernel, two halo planes (64 input channels per
-    block, DMY_WGRAD_TAP_NP=2, default) and one (=1): both against torch's fp32 conv2d_weight, and against each other"""
+    """3x3 s1 weight-grad on the tap-fused kernel, two halo planes (64 input channels per block: DMY_WGRAD_TAP_NP=2 for
+    <= 64 output channels, DMY_WGRAD_TAP_NP128=1 for more) and one: both against torch's fp32 conv2d_weight, and
+    against each other"""
     import os
     from dmayolo.functional import call, ptr, stream
+    monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP128', '1')
     g = torch.Generator().manual_seed(N + C + K + H)
     x = torch.randn(N, C, H, W, generator=g).bfloat16()
     dy = torch.randn(N, K, H, W, generator=g).bfloat16()
@@ -173,6 +176,7 @@ def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K, monkeypatch):
     out = {}
     for np_ in ('2', '1'):
         monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP', np_)
+        monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP128', '1' if np_ == '2' else '0')
         dwo = torch.empty(K * C * 9, device='cuda')
         dw = torch.empty(K, C, 3, 3, device='cuda')
         assert call('dmy_conv_wgrad', 1, ptr(xd), ptr(dyd), ptr(dwo), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K, stream()) == 0
