@@ -3458,7 +3458,8 @@ __global__ void __launch_bounds__(512) conv_wgrad_w(const bf16* __restrict__ x, 
 //   ds_read_b64_tr_b16 group touches ((y, x .. x + 3), (y + 1, x .. x + 3)) then hit 64 distinct banks.
 //   Stages: BM/8 KiB A + 8 KiB B (120 of 128 halo rows used), 3-stage LDS-DMA ring, a counted vmcnt keeps one
 //   stage in flight across each barrier.  4 waves = 2 (m) x 2 (n), wave tile BM/2 x 144 (BM/32 x 9 MFMA frags).
-// Valid for KH = KW = 3, S = 1, P = 1, OH = H, OW = W, C % 32 == 0 (host-checked).  Split-K over patches; the
+// Valid for KH = KW = 3, S = 1, P = 1, OH = H, OW = W, C % 16 == 0 (host-checked; a
+// 16-channel plane half loads zeros).  Split-K over patches; the
 // (tile, split) -> linear id mapping keeps a split's tiles on one XCD (they read the same patches).
 template <int BM, int NP = 1>  // NP halo planes of 32 input channels each (2: a block owns 64 input channels)
 struct WgradTapLds {
@@ -3475,10 +3476,11 @@ struct WgradTapLds {
   int brel[2], by[2], bx[2];         // x halo: per piece halo (y, x) and element offset rel. to the halo origin
   int bcol[2];
   bool bok[2];
-  int yps, xps;
+  int yps, xps, cmax;
   DEV WgradTapLds(const bf16* x, const bf16* dy, const Geom& g, int m0, int c0, int kt0, int wid, int lane,
                   unsigned xbytes, unsigned dybytes)
       : OH(g.OH), OW(g.OW), H(g.H), W(g.W) {
+    cmax = g.C;  // C % 32 == 16 (the 16-channel space-to-depth stem): the plane's chunks past C load zeros
     rx = make_rsrc(x, xbytes);
     rdy = make_rsrc(dy, dybytes);
     yps = (int)g.yps;
@@ -3529,7 +3531,7 @@ struct WgradTapLds {
       const bool ok = bok[j] && (unsigned)(oy0 - 1 + by[j]) < (unsigned)H && (unsigned)(ox0 - 1 + bx[j]) < (unsigned)W;
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl)
-        blds16(rx, ok ? (unsigned)(xbase + brel[j] + bcol[j] + 32 * pl) * 2u : kBufOob,
+        blds16(rx, ok && bcol[j] + 32 * pl < cmax ? (unsigned)(xbase + brel[j] + bcol[j] + 32 * pl) * 2u : kBufOob,
                stage + A_BYTES + pl * 8192 + (wid * 2 + j) * 1024);
     }
     if (++px == npw) {
@@ -3639,8 +3641,8 @@ __global__ void __launch_bounds__(256, (BM == 128 && NP == 2) ? 1 : 2) conv_wgra
     for (int e = threadIdx.x; e < CTR * NCOL; e += 256) {
       const int row = e / NCOL, col = e % NCOL, m = m0 + half * CTR + row;
       const int pl = col / 288, cc = col % 288;
-      const int n = (cc >> 5) * g.C + c0 + pl * 32 + (cc & 31);  // cc = tap * 32 + ci
-      if (m < g.K) wgrad_out(g, dw, split, (long)m * Ntot + wgrad_col(g, n), ct[row * CTS + col]);
+      const int ci = c0 + pl * 32 + (cc & 31), n = (cc >> 5) * g.C + ci;  // cc = tap * 32 + ci
+      if (m < g.K && ci < g.C) wgrad_out(g, dw, split, (long)m * Ntot + wgrad_col(g, n), ct[row * CTS + col]);
     }
   }
 }
@@ -4862,12 +4864,15 @@ inline int wgrad_tap_mode() {
 }
 inline bool wgrad_tap_ok(const Geom& g, const void* x, const void* dy) {
   if (!wgrad_tap_mode() || g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.OH != g.H || g.OW != g.W) return false;
-  if (g.C % 32 != 0 || g.xps % 8 != 0 || g.yps % 8 != 0 || g.K % 8 != 0 || !aligned16(x) || !aligned16(dy)) return false;
+  if (g.C % 16 != 0 || g.xps % 8 != 0 || g.yps % 8 != 0 || g.K % 8 != 0 || !aligned16(x) || !aligned16(dy)) return false;
+  // C % 32 == 16 (the space-to-depth stem, 16 channels): DMY_WGRAD_TAP16 = 0 keeps it on the v3n column tiles
+  static const int t16 = env_int("DMY_WGRAD_TAP16", 1);
+  if (g.C % 32 != 0 && !t16) return false;
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
   if (xb >= (double)v3::kBufOob || db >= (double)v3::kBufOob) return false;
   // enough (patch, tile) work units that the per-block fp32 atomics of the 288-column tile stay a small share
   // (tools/gpu/tune_conv.py: 20^2 / 40^2 / 80^2 yolov5s layers are faster on the v3 / v4 column tiles)
-  const long units = (long)g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8) * ceil_div(g.K, 128) * (g.C / 32);
+  const long units = (long)g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8) * ceil_div(g.K, 128) * ceil_div(g.C, 32);
   // 10000: the yolov5s 64-channel @80^2 layers (12800 units) measured 96 -> 79 us on the tap kernel, the 256-channel
   // @20^2 ones (9216) 70 -> 106 us (profiles/r02/ab_wgrad_v5s.log)
   static const long min_units = env_int("DMY_WGRAD_TAP_UNITS", 10000);
@@ -4890,7 +4895,7 @@ inline int wgrad_tap_np128(const Geom& g) {
 }
 template <int BM, int NP = 1>
 int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
-  const int gm = ceil_div(g.K, BM), gn = g.C / (32 * NP);
+  const int gm = ceil_div(g.K, BM), gn = ceil_div(g.C, 32 * NP);
   const int nk = g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8);  // 8 x 8 patches
   const int tiles = gm * gn;
   int maxs = nk / 8;

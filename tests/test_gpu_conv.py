@@ -159,11 +159,12 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
 
 
 @pytest.mark.parametrize('N,C,H,W,K', [(16, 64, 160, 160, 64), (16, 64, 150, 146, 48), (10, 128, 128, 136, 32),
-                                       (16, 128, 100, 104, 128), (8, 256, 96, 96, 256), (10, 128, 96, 96, 192)])
+                                       (16, 128, 100, 104, 128), (8, 256, 96, 96, 256), (10, 128, 96, 96, 192),
+                                       (8, 16, 288, 288, 64), (8, 16, 290, 282, 32)])
 def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K, monkeypatch):
     """3x3 s1 weight-grad on the tap-fused kernel, two halo planes (64 input channels per block: DMY_WGRAD_TAP_NP=2 for
     <= 64 output channels, DMY_WGRAD_TAP_NP128=1 for more) and one: both against torch's fp32 conv2d_weight, and
-    against each other"""
+    against each other.  C = 16 is the space-to-depth stem's view (half a plane, the rest loads zeros)"""
     import os
     from dmayolo.functional import call, ptr, stream
     monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP128', '1')
