@@ -232,13 +232,25 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
     else:
         pk = PEAK_FLOPS['fp8'] if dom.endswith('_f8') else PEAK_FLOPS[dtype]
         achieved, peak, unit = d['flops'] / d['seconds'] / 1e12, pk / 1e12, 'TFLOP/s'
-    traffic, tsrc = None, None
+    # PMC traffic of the same call population (tools/pmc_traffic.py: every dispatch assigned to the dmy_conv_* call
+    # family that launches it, bytes divided by the calls the profiled bench command made); used only when the
+    # profiled command made as many calls per step of this family as this run does
+    traffic, tsrc, tnote, per_step = None, None, None, None
     tpath = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tpath):
         with open(tpath) as f:
-            tr = json.load(f).get(cfg_name, {}).get(dom)
-        if tr:
-            traffic, tsrc = round(tr['bytes_per_launch']), 'profiles/pmc_traffic.json: ' + tr['source']
+            tj = json.load(f).get(cfg_name, {})
+        tr = tj.get(dom)
+        if tr and 'bytes_per_call' in tr:
+            if abs(tr['calls_per_step'] - d['launches'] / steps) < 0.5:
+                traffic, tsrc = round(tr['bytes_per_call']), 'profiles/pmc_traffic.json: ' + tr['source']
+            else:
+                tnote = ('PMC record made %.1f calls per step of %s, this run %.1f: populations differ, not used'
+                         % (tr['calls_per_step'], dom, d['launches'] / steps))
+        if '_per_step' in tj:
+            ps_ = tj['_per_step']
+            per_step = dict(pmc_gb=round(ps_['pmc_bytes'] / 1e9, 2), algorithmic_gb=round(ps_['algorithmic_bytes'] / 1e9, 2),
+                            ratio=round(ps_['pmc_over_algorithmic'], 3), families=ps_['families'])
     mfma, msrc = {}, None  # MFMA-busy per family from the PMC pass of the same bench command (tools/pmc_mfma.py)
     mpath = os.path.join(ROOT, 'profiles', 'pmc_mfma.json')
     if os.path.exists(mpath):
@@ -251,7 +263,10 @@ def roofline(ks, steps, el_events, dtype, cfg_name):
                 'time-weighted per family; conv_3x3 = the k > 1 kernels', mfma_busy_source=msrc,
                 achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(troof / d['seconds'], 4),
                 achieved_over_peak=round(achieved / peak, 4),
-                traffic=traffic, traffic_unit='bytes/launch (HBM, PMC)', traffic_source=tsrc,
+                traffic=traffic, traffic_unit='bytes/launch (HBM, PMC, same call population)', traffic_source=tsrc,
+                traffic_note=tnote,
+                traffic_over_algorithmic=round(traffic / (d['bytes'] / d['launches']), 3) if traffic else None,
+                conv_traffic_per_step=per_step,
                 algorithmic_bytes_per_launch=round(d['bytes'] / d['launches']),
                 algorithmic_flops_per_launch=round(d['flops'] / d['launches']),
                 launches=d['launches'], avg_launch_us=round(d['seconds'] / d['launches'] * 1e6, 2),
@@ -282,11 +297,13 @@ def run_config(name, a, world, rank, dev_idx, device, dtype, batch=0, cpu_second
     torch.cuda.reset_peak_memory_stats(device)
     model = build(cfg, dtype, device, fp8=fp8)
     net = model
+    # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
+    fu = any(isinstance(m, torch.nn.MultiheadAttention) for m in model.modules())
     if world > 1 and a.ddp == 'arena':  # buckets = slices of the gradient arena (dmayolo/ddp.py)
         from dmayolo.ddp import ArenaDDP
-        net = ArenaDDP(model, bucket_cap_mb=a.bucket_mb, compress=None if a.grad_compress == 'none' else a.grad_compress)
-    elif world > 1:  # train.py:326 (find_unused_parameters when the model holds nn.MultiheadAttention)
-        fu = any(isinstance(m, torch.nn.MultiheadAttention) for m in model.modules())
+        net = ArenaDDP(model, bucket_cap_mb=a.bucket_mb, compress=None if a.grad_compress == 'none' else a.grad_compress,
+                       find_unused_parameters=fu)
+    elif world > 1:
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev_idx], output_device=dev_idx,
                                                         find_unused_parameters=fu)
     total_bs = bs * world

@@ -22,10 +22,16 @@ parameter order), so here the buckets ARE contiguous slices of that buffer and n
     construction, as DDP's defaults (broadcast_buffers=True).
 
 A parameter that gets no gradient on this rank still has its (zeroed) slice reduced with the rest, and after backward
-its .grad is that slice -- the rank average, zero when no rank used it -- as torch DDP writes the reduced gradient into
-locally unused parameters, so replicas cannot diverge.  The hooks act only for a backward this wrapper armed (a
-training forward through it); `close()` removes them, and a model may be wrapped again after that.  The loss * WORLD_SIZE of train.py:440 stays in the backward seed (GradScaler.upstream), so
-the averaged gradient is the sum over ranks, exactly as with DDP.
+its .grad is that slice -- the rank average -- as torch DDP writes the reduced gradient into locally unused
+parameters, so replicas cannot diverge.  A parameter that NO rank used is told apart only with
+`find_unused_parameters=True` (train.py:326 sets it when the model holds nn.MultiheadAttention): every rank then
+all-reduces a used-flag vector after the buckets and reads it back (one host synchronisation per backward, as DDP's own
+find-unused mode), and a globally unused parameter keeps the .grad it had (None after zero_grad), so SGD's weight decay
+and momentum, and Adam's step count, do not advance for it.  Without the flag the graph is assumed static, as DDP does
+without it, and such a parameter gets a zero gradient.  The hooks act only for a backward this wrapper armed (a
+training forward through it); `close()` removes them, and a model may be wrapped again after that.  The loss *
+WORLD_SIZE of train.py:440 stays in the backward seed (GradScaler.upstream), so the averaged gradient is the sum over
+ranks, exactly as with DDP.
 """
 import torch
 import torch.distributed as dist
@@ -53,10 +59,11 @@ class _Backward:
 
 class ArenaDDP(torch.nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=32.0, first_bucket_mb=4.0, compress=None,
-                 broadcast_buffers=True):
+                 broadcast_buffers=True, find_unused_parameters=False):
         super().__init__()
         assert compress in (None, 'bf16'), compress
         self.module, self.pg, self.compress, self.broadcast_buffers = module, process_group, compress, broadcast_buffers
+        self.find_unused = bool(find_unused_parameters)
         self.world = dist.get_world_size(process_group)
         self.params = [p for p in module.parameters() if p.requires_grad]
         all_params = list(module.parameters())
@@ -86,19 +93,24 @@ class ArenaDDP(torch.nn.Module):
             state = [t for t in module.state_dict().values() if torch.is_tensor(t)]
             if state:
                 dist._broadcast_coalesced(self._group(), state, 250 * 2 ** 20, 0)
+        self._owner = object()  # identity token: a flag on a parameter names the wrapper that set it
         for p in self.reduced:
             if getattr(p, '_dmy_arena_ddp', None) is not None:
+                self.close()  # release only the flags this wrapper set so far
                 raise RuntimeError('ArenaDDP: a parameter is already hooked by another live wrapper; close() it first')
-            p._dmy_arena_ddp = True
+            p._dmy_arena_ddp = self._owner
             self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
     def close(self):
-        """remove the gradient hooks (the model can then be used unwrapped, or wrapped again)"""
+        """remove the gradient hooks (the model can then be used unwrapped, or wrapped again); a flag another live
+        wrapper set on a parameter is left alone, e.g. when an old wrapper is garbage-collected after a new one"""
         for h in self._handles:
             h.remove()
         self._handles = []
-        for p in self.reduced:
-            p._dmy_arena_ddp = None
+        owner = getattr(self, '_owner', None)
+        for p in getattr(self, 'reduced', ()):
+            if owner is not None and getattr(p, '_dmy_arena_ddp', None) is owner:
+                p._dmy_arena_ddp = None
         self._bw = self._buf = None
 
     def __del__(self):
@@ -167,9 +179,9 @@ class ArenaDDP(torch.nn.Module):
             view = bw.buf[lo:hi]
             if self.trace is not None:
                 self.trace.append(('launch' if upto is None else 'launch_final', bw.next))
-            if self.world == 1:
-                bw.works.append((None, None, view))
-            elif self.compress == 'bf16':
+            # no world-size-1 shortcut: a one-rank group issues its collectives as well, so the RCCL stream
+            # semantics (async all_reduce, work.wait() making the current stream wait) run on one GPU too
+            if self.compress == 'bf16':
                 c = (view / self.world).to(torch.bfloat16)
                 bw.works.append((dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), c, view))
             else:
@@ -186,6 +198,18 @@ class ArenaDDP(torch.nn.Module):
                 work.wait()  # RCCL: the current stream waits on the collective's stream (no host sync)
             if c is not None:
                 view.copy_(c)
-        for p in self.reduced:
-            if id(p) not in bw.seen:  # no gradient on this rank: it still gets the rank average (DDP semantics)
-                p.grad = self._slice(bw.buf, p)
+        unused = [i for i, p in enumerate(self.reduced) if id(p) not in bw.seen]
+        if self.find_unused and self.world > 1:
+            # which parameters some rank used: a MAX over the ranks' used flags, read on the host (DDP's find-unused
+            # mode synchronises the same way); every rank issues it, whether or not it has locally unused parameters
+            flags = torch.ones(len(self.reduced), dtype=torch.int32)
+            flags[unused] = 0
+            flags = flags.to(bw.buf.device)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.pg)
+            used = flags.cpu()
+            unused = [i for i in unused if used[i] != 0]
+        elif self.find_unused:
+            unused = []  # one rank: what it did not use, nobody used
+        for i in unused:  # no gradient on this rank but on some other: it gets the rank average (DDP semantics)
+            p = self.reduced[i]
+            p.grad = self._slice(bw.buf, p)

@@ -45,24 +45,27 @@ class GraphedDetector:
         self.key = self._state_key(x)
 
     def _capture_detect(self, x, nms_args):
-        from .utils.general import nms_prepare, nms_launch
+        from .utils.general import nms_prepare, nms_launch, nms_buffers
         self._capture(x)  # warm-up forwards fill every per-layer cache; the forward-only graph stays usable
         z = self.static_out[0]
         pred, plan = nms_prepare(z, **nms_args)  # NMS plan from the recorded output's shape (the cap hint)
-        # the NMS path's own allocations, outside the capture, on the capture stream itself (its self-resetting
-        # candidate counter is per stream: made here, the graph records no fill for it)
+        # the detect graph owns its input buffer, its state key and its NMS counter / pinned counts: __call__ may
+        # re-record the forward-only graph (and replace static_in) without this graph noticing otherwise
+        self.dstatic_in = x.clone()
+        bufs = nms_buffers(x.device, x.shape[0])
         cs = torch.cuda.Stream()
         cs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cs):
             for _ in range(self.warmup):
-                nms_launch(pred, plan)
+                nms_launch(pred, plan, bufs=bufs)
         torch.cuda.synchronize()
         self.dgraph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.dgraph, stream=cs), torch.no_grad():
-            out = self.model(self.static_in)
+            out = self.model(self.dstatic_in)
             dpred = out[0].detach().float().contiguous()  # nms_prepare's conversion (the plan, cls_ok included, is made)
-            self.dstate = (out, plan, plan['cap']) + nms_launch(dpred, plan)
-        self.dkey = (self.key, tuple(sorted((k, str(v)) for k, v in nms_args.items())), plan['cap'])
+            self.dstate = (out, plan, plan['cap']) + nms_launch(dpred, plan, bufs=bufs)
+        self.dbufs = bufs
+        self.dkey = (self._state_key(x), tuple(sorted((k, str(v)) for k, v in nms_args.items())), plan['cap'])
 
     @torch.no_grad()
     def detect(self, x, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False, multi_label=False,
@@ -77,10 +80,10 @@ class GraphedDetector:
                     multi_label=multi_label, max_det=max_det)
         key = tuple(sorted((k, str(v)) for k, v in args.items()))
         cur = getattr(self, 'dkey', None)
-        if (self.graph is None or self._state_key(x) != self.key or cur is None or cur[1] != key or
+        if (cur is None or self._state_key(x) != cur[0] or cur[1] != key or
                 _CAP_HINT.get(self.dstate[1]['key'], cur[2]) != cur[2]):
             self._capture_detect(x, args)
-        self.static_in.copy_(x)
+        self.dstatic_in.copy_(x)
         self.dgraph.replay()
         out, plan, cap, cnt, dets = self.dstate
         res = nms_finish(plan, cap, cnt, dets)

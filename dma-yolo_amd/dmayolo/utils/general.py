@@ -98,17 +98,27 @@ def nms_prepare(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnos
     return pred, plan
 
 
-def nms_launch(pred, plan, cap=None):
+def nms_buffers(dev, nimg):
+    """a private (candidate counter, pinned host counts) pair for a caller that owns them, e.g. a recorded graph
+    (infer.GraphedDetector): the counter starts zeroed and every call re-zeroes it, so no other stream can share it"""
+    return (torch.zeros(max(nimg, 64), dtype=torch.int32, device=dev),
+            torch.zeros(max(2 * nimg, 64), dtype=torch.int32, pin_memory=True))
+
+
+def nms_launch(pred, plan, cap=None, bufs=None):
     """the NMS kernels of one call at sort capacity `cap`, no host synchronisation (so it can be recorded into a HIP
     graph, infer.GraphedDetector.detect): returns (cnt, out) -- cnt = [candidate counts | keep counts] (int32, in the
-    stream's pinned host buffer; a device tensor inside a capture that has none),
-    out = (nimg, max_det, 6) rows; nms_finish reads them"""
+    stream's pinned host buffer, or the caller's own `bufs` = nms_buffers(); a device tensor inside a capture that has
+    neither), out = (nimg, max_det, 6) rows; nms_finish reads them"""
     nimg, A, no = pred.shape
     dev = pred.device
     cap = plan['cap'] if cap is None else cap
     max_nms = 30000
-    ctr = _nms_counter(dev, nimg)  # zero on entry; the greedy launch hands the counts to cnt and re-zeroes it
-    cnt = _nms_host_counts(dev, nimg)  # pinned host memory the scan writes directly: no read-back copy
+    if bufs is not None:
+        ctr, cnt = bufs[0], bufs[1][:2 * nimg]
+    else:
+        ctr = _nms_counter(dev, nimg)  # zero on entry; the greedy launch hands the counts to cnt and re-zeroes it
+        cnt = _nms_host_counts(dev, nimg)  # pinned host memory the scan writes directly: no read-back copy
     if cnt is None:
         cnt = torch.empty(2 * nimg, dtype=torch.int32, device=dev)
     keys = torch.empty((nimg, cap), dtype=torch.int64, device=dev)
@@ -146,8 +156,8 @@ def _nms_host_counts(dev, nimg):
 
 def _nms_counter(dev, nimg):
     """the candidate counter of the current stream: int32 [>= nimg], zero between calls (the greedy launch of each call
-    copies the counts out and re-zeroes it), so a call needs no fill launch.  One per (device, stream): calls on two
-    streams never share it.  Created (zeroed) outside graph capture when possible; one created during a capture is
+    copies the counts out and re-zeroes it), so a call needs no fill launch.  One per (device, stream handle) for eager
+    calls, which run in issue order on that stream; a recorded graph owns its own pair (nms_buffers).  Created (zeroed) outside graph capture when possible; one created during a capture is
     zeroed by a fill recorded in that graph"""
     key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
     t = _NMS_CTR.get(key)

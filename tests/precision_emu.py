@@ -19,6 +19,7 @@ run again with the roundings a reduced-precision run performs, and the product i
   mode 'fp16'     the reference's own training precision, CUDA autocast (train.py:434): the same roundings to fp16
                    (conv / linear / activation outputs and weights fp16, BatchNorm statistics and the loss fp32),
                    backward seeded with a 2^16 loss scale as GradScaler does, so that fp16 gradients do not underflow;
+  mode 'fp8_sink' 'fp8' with 'bf16_sink's input-gradient roundings (the per-layer comparison of the fp8 product);
   mode 'fp8'      config 5's storage: 'bf16', and every conv the product runs on the e4m3 kernel (functional.set_fp8:
                    k >= 3, C % 128 == 0, K % 8 == 0, K >= 32) computes its FORWARD from e4m3 operands -- the input
                    scaled per tensor by 448 / max|x|, the fp32 weight per output channel by 448 / max|w_k| -- while its
@@ -29,8 +30,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 DTYPES = {'bf16_act': torch.bfloat16, 'bf16': torch.bfloat16, 'bf16_sink': torch.bfloat16, 'fp16': torch.float16,
-          'fp8': torch.bfloat16}
-LOSS_SCALE = {'bf16_act': 1.0, 'bf16': 1.0, 'bf16_sink': 1.0, 'fp16': 2.0 ** 16, 'fp8': 1.0}
+          'fp8': torch.bfloat16, 'fp8_sink': torch.bfloat16}
+LOSS_SCALE = {'bf16_act': 1.0, 'bf16': 1.0, 'bf16_sink': 1.0, 'fp16': 2.0 ** 16, 'fp8': 1.0, 'fp8_sink': 1.0}
 
 LEAVES = (nn.Conv2d, nn.BatchNorm2d, nn.SiLU, nn.Upsample, nn.MaxPool2d, nn.Linear, nn.LayerNorm, nn.GELU, nn.Hardswish,
           nn.Sigmoid, nn.AvgPool2d, nn.AdaptiveAvgPool2d, nn.AdaptiveMaxPool2d, nn.ReLU)
@@ -126,7 +127,7 @@ def emulate(model, mode):
             mod.register_forward_hook(hook)
     if mode == 'bf16_act':
         return model
-    if mode == 'bf16_sink':
+    if mode in ('bf16_sink', 'fp8_sink'):
         pre = lambda m, i: tuple(RoundGrad.apply(a, dt) if torch.is_tensor(a) and a.requires_grad else a  # noqa: E731
                                  for a in i)
         for mod in model.modules():
@@ -135,7 +136,7 @@ def emulate(model, mode):
     for mod in model.modules():
         if isinstance(mod, _stored_types()):
             mod.register_forward_hook(hook)
-        if mode == 'fp8' and type(mod) is nn.Conv2d and fp8_eligible(mod):
+        if mode in ('fp8', 'fp8_sink') and type(mod) is nn.Conv2d and fp8_eligible(mod):
             mod.forward = (lambda m: lambda x: F8Conv.apply(x, m.weight, m.stride, m.padding))(mod)
         elif type(mod) is nn.Conv2d:
             mod.forward = (lambda m: lambda x: F.conv2d(x, RoundWeight.apply(m.weight, dt), m.bias, m.stride, m.padding,

@@ -202,13 +202,14 @@ def test_arena_reducer_overlaps_backward():
 
 
 class _Branchy(torch.nn.Module):
-    """a parameter (`b`) that only rank 0 uses"""
+    """a parameter (`b`) that only rank 0 uses, and one (`c`) that no rank uses"""
 
     def __init__(self):
         super().__init__()
         torch.manual_seed(0)
         self.a = torch.nn.Linear(8, 8)
         self.b = torch.nn.Linear(8, 8)
+        self.c = torch.nn.Linear(8, 8)
 
     def forward(self, x, use_b):
         y = self.a(x)
@@ -222,10 +223,10 @@ def _unused_worker(rank, world, port, out):
     torch.set_num_threads(1)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     m = _Branchy()
-    net = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4)
+    net = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4, find_unused_parameters=True)
     x = torch.randn(4, 8, generator=torch.Generator().manual_seed(rank))
     net(x, use_b=rank == 0).square().sum().backward()
-    g = {k: p.grad.clone() for k, p in m.named_parameters()}
+    g = {k: (None if p.grad is None else p.grad.clone()) for k, p in m.named_parameters()}
     # the wrapper's hooks act only for backward passes it armed; close() removes them and the model can be wrapped
     # again: a backward through the bare model, then a second wrapper
     m.zero_grad(set_to_none=True)
@@ -235,14 +236,28 @@ def _unused_worker(rank, world, port, out):
     net2 = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4)
     net2(x, use_b=rank == 0).square().sum().backward()
     g2 = {k: p.grad.clone() for k, p in m.named_parameters()}
-    torch.save(dict(g=g, g2=g2), out + f'.{rank}')
+    # a wrapper garbage-collected after a new one wraps the model must not clear the live wrapper's flags
+    net2.close()
+    net3 = ArenaDDP(m, first_bucket_mb=1e-4, bucket_cap_mb=1e-4)
+    del net2
+    import gc
+    gc.collect()
+    try:
+        ArenaDDP(m)
+        double = True
+    except RuntimeError:
+        double = False
+    net3.close()
+    torch.save(dict(g=g, g2=g2, double=double), out + f'.{rank}')
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_arena_reducer_unused_parameter_and_rewrap():
     """a parameter with a gradient on rank 0 only gets the rank average on BOTH ranks (torch DDP writes the reduced
-    gradient into locally unused parameters); wrapping a model twice works after close()"""
+    gradient into locally unused parameters); with find_unused_parameters=True a parameter NO rank used keeps
+    .grad None (so the optimizer leaves it alone), without it (static graph) it gets zeros; wrapping a model twice
+    works after close(), and an old wrapper's garbage collection leaves a live wrapper's guard in place"""
     _setup()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, 'r.pt')
@@ -258,5 +273,9 @@ def test_arena_reducer_unused_parameter_and_rewrap():
             exp[k] = exp.get(k, 0) + g / 2
     for key in ('g', 'g2'):
         for k in exp:
+            if key == 'g' and k.startswith('c.'):  # globally unused, find_unused_parameters=True: untouched
+                assert r[0][key][k] is None and r[1][key][k] is None, k
+                continue
             torch.testing.assert_close(r[0][key][k], exp[k], rtol=1e-5, atol=1e-7)
             assert torch.equal(r[0][key][k], r[1][key][k]), (key, k)
+    assert not r[0]['double'] and not r[1]['double']

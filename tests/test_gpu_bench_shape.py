@@ -1,26 +1,23 @@
 """The bench's own configuration end to end: full-width models at the bench resolutions, bf16 HIP product (v3 LDS-DMA
 convs at these M, split-K weight-grads into the gradient arena, s2d stem, one-launch weight prep, GradSinks) against
-the fp32 CPU oracle on the same state_dict, images and targets.
+the fp32 oracle on the same state_dict, images and targets.
 
 Compared: the three Detect outputs, the loss and its items (ComputeLoss, utils/loss.py:167-218), the vector of
 per-parameter gradient norms and the direction of the whole gradient.  At random init these BN networks lose a large
 part of the gradient direction to 8-bit-mantissa storage alone, so fixed fp32-style bounds do not apply; the oracle is
 run again under tests/precision_emu.py's emulation of the product's storage ('bf16': every stored activation and its
-gradient, the conv / linear weight copies and the stored composite outputs rounded to bf16) in TWO realizations -- on
-the CPU, and with the same torch ops on the GPU (whose fp32 sums run in another order) three times, two of them with the
-weights moved by one fp32 ulp -- and the product is held to the envelope of the four:
+gradient, the conv / linear weight copies and the stored composite outputs rounded to bf16) in several realizations --
+the state_dict as is, and with the weights moved by one fp32 ulp -- and the product is held to their envelope:
   outputs relative L2 per level <= 1.1 * env + 2e-3 ; loss <= 1.5 * env + 5e-3 ; items <= 1.5 * env + 1e-2
   grads  relative L2 of the whole gradient <= 1.1 * env + 1e-2; median over the top-level layers of (product layer
          error / emulation layer error) <= 1.1; per-parameter grad-norm vector <= 1.5 * env + 2e-3;
          cosine(product, fp32) >= min(emulation cosines) - 0.05   (round 2's strictness)
-Round 4 measured (gpurun_out r4 diag logs): realizations of the one emulation alone differ by up to 3x
-on the gradient metrics (DMA-YOLO-l grad-norm vector 1.80e-2 on the CPU, 2.2e-2 and 5.5e-2 on the GPU of two boxes),
-so those metrics measure the rounding-noise realization at random init; the product sits inside the spread.  A kernel bias is caught instead by
-test_gpu_conv_bench_shapes.py (every conv shape of both bench configs exact to one bf16 rounding) and by
-test_gpu_trajectory.py (120-step training runs).  The reference itself trains under CUDA autocast (fp16 activations,
-train.py:434); its emulation ('fp16') is run and printed too, about 7x closer to fp32 than bf16 storage -- asserted as
-a documented property of the two formats, not of the product.  'bf16_sink' (bf16 + per-contribution rounding of input
-gradients, the product's GradSink accumulation) is printed: it moves the metrics by < 6 %."""
+The fp32 oracle and the emulations run their torch ops on the GPU (TF32 off): the same algorithm as the CPU oracle
+(pinned to it in float64 by test_gpu_trajectory.py), another fp32 summation order.  A kernel bias is caught by
+test_gpu_conv_bench_shapes.py (every conv shape of both bench configs exact to one bf16 rounding), by the per-layer tests
+below and by test_gpu_trajectory.py (120-step training runs).  The reference itself trains under CUDA autocast (fp16
+activations, train.py:434); its emulation ('fp16') is run and printed too, closer to fp32 than bf16 storage -- asserted
+as a documented property of the two formats, not of the product."""
 import os
 
 import pytest
@@ -87,22 +84,22 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
                 {k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
 
     chaotic = yml in CHAOTIC
-    # product realizations: the state_dict as is, and (chaotic configs) ulp-perturbed copies, seeds 1..4 -- the product
+    # product realizations: the state_dict as is, and (chaotic configs) ulp-perturbed copies, seeds 1, 2 -- the product
     # decides its bf16 roundings on slightly different fp32 values, exactly as the emulation realizations below do.  An
-    # odd count, so the median is one realization (round 5: with 4 the upper median of [2.8e-2 .. 8.4e-2] failed against
-    # the max of 5 emulation realizations in one run, 6.5e-2, and passed in another, 1.4e-1)
-    prods = [product_run(sd)] + ([product_run(perturbed(s_)) for s_ in (1, 2, 3, 4)] if chaotic else [])
+    # odd count, so the median is one realization
+    prods = [product_run(sd)] + ([product_run(perturbed(s_)) for s_ in (1, 2)] if chaotic else [])
     p, loss, items, pgrads = prods[0]
-    ref, pr, lr_, ir_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, None)
-    emu, pe_, le_, ie_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16')
-    h16, ph_, lh_, ih_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'fp16')
-    snk, ps_, ls_, is_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16_sink')
-    # more realizations of the bf16 emulation: the same roundings after fp32 sums in another order (GPU torch ops), and
-    # with the weights moved by one fp32 ulp (relative 2^-24 noise, seeds 1 / 2 / 3) -- each decides its bf16 roundings
-    # on slightly different fp32 values, as the product's kernels do
-    reals = [_oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16', 'cuda')]
-    for seed in ((1, 2, 3, 4, 5, 6) if chaotic else (1, 2)):
-        reals.append(_oracle_grads(yml, nc, perturbed(seed), x, t, anchors, hyp, 'bf16', 'cuda'))
+    # the fp32 oracle and its emulations run their torch ops on the GPU (TF32 off; DropPath / dropout off): the CPU runs
+    # of round 5 took most of this test's time, and the fp32 order is one more realization of the same sums
+    ref, pr, lr_, ir_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, None, 'cuda')
+    emu, pe_, le_, ie_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16', 'cuda')
+    h16, ph_, lh_, ih_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'fp16', 'cuda')
+    snk, ps_, ls_, is_ = _oracle_grads(yml, nc, sd, x, t, anchors, hyp, 'bf16_sink', 'cuda')
+    # more realizations of the emulation, with the weights moved by one fp32 ulp (relative 2^-24 noise, seeds 1..):
+    # each decides its bf16 roundings on slightly different fp32 values, as the product's kernels do.  Chaotic configs:
+    # 'bf16_sink', the product's own storage model (GradSink roundings), for the distribution comparison
+    reals = [_oracle_grads(yml, nc, perturbed(seed), x, t, anchors, hyp, 'bf16_sink' if chaotic else 'bf16', 'cuda')
+             for seed in ((1, 2, 3, 4) if chaotic else (1, 2, 3))]
 
     def errs(po, lo, io, pg):
         """pg: parameter name -> its gradient tensor"""
@@ -145,7 +142,7 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
           f'{h_gn[0]:.2e} whole gradient {h_gn[1]:.2e} cos {h_cos:.4f}\n'
           f'  bf16 storage + per-contribution gradient rounding (bf16_sink): outputs {f(s_out)} loss {s_loss:.2e} '
           f'grad-norm vector {s_gn[0]:.2e} whole gradient {s_gn[1]:.2e} cos {s_cos:.4f}\n'
-          + ''.join(f'\n  bf16 emulation, realization {i + 2} (GPU fp32 order{", ulp-perturbed weights" if i else ""}): '
+          + ''.join(f'\n  emulation realization {i + 2} (ulp-perturbed weights): '
                     f'outputs {f(r[0])} loss {r[1]:.2e} grad-norm vector {r[3][0]:.2e} whole gradient {r[3][1]:.2e} cos '
                     f'{r[4]:.4f}' for i, r in enumerate(rerr)))
     sr = sorted(gn_err[2][i] / max(s_gn[2][i], 1e-12) for i in gn_err[2])
@@ -187,22 +184,23 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
     if chaotic:
         # see CHAOTIC: the whole-model single-step gradient of this config is a noise realization, so one product
         # realization against one emulation realization says nothing.  Compared as DISTRIBUTIONS instead (VERDICT r4
-        # item 2b): 5 product realizations (ulp-perturbed weights) against 8 emulation realizations (CPU order, GPU
-        # order, 6 ulp-perturbed) -- the product's MEDIAN grad-norm-vector error, whole-gradient error and cosine must lie
-        # inside the emulation realizations' range (median cosine >= their minimum)
+        # item 2b, r5 item 8): 3 product realizations (ulp-perturbed weights) against 5 realizations of the product's
+        # storage model ('bf16_sink': the unperturbed one and 4 ulp-perturbed) -- the product's MEDIAN grad-norm-vector
+        # error and whole-gradient error must be within 1.25x the emulation's MEDIAN, and its median cosine within
+        # 0.05 of theirs
         med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
         p_gn = [r[3][0] for r in perr]
         p_wg = [r[3][1] for r in perr]
-        p_cos = sorted(r[4] for r in perr)
-        e_all = rerr + [(e_out, e_loss, e_item, e_gn, e_cos)]
+        p_cos = [r[4] for r in perr]
+        e_all = rerr + [(s_out, s_loss, s_item, s_gn, s_cos)]
         e_gnv = [r[3][0] for r in e_all]
         e_wg = [r[3][1] for r in e_all]
         e_cs = [r[4] for r in e_all]
         print(f'  distribution: product grad-norm vector {f(p_gn)} whole {f(p_wg)} cos {f(p_cos)}\n'
               f'                emulation    grad-norm vector {f(e_gnv)} whole {f(e_wg)} cos {f(e_cs)}')
-        assert med(p_gn) <= max(e_gnv), (p_gn, e_gnv)
-        assert med(p_wg) <= max(e_wg), (p_wg, e_wg)
-        assert p_cos[(len(p_cos) - 1) // 2] >= min(e_cs), (p_cos, e_cs)
+        assert med(p_gn) <= 1.25 * med(e_gnv), (p_gn, e_gnv)
+        assert med(p_wg) <= 1.25 * med(e_wg), (p_wg, e_wg)
+        assert med(p_cos) >= med(e_cs) - 0.05, (p_cos, e_cs)
         for r in perr:  # every product realization's outputs / loss inside the per-realization bounds too
             for a, e in zip(r[0], env_out):
                 assert a <= 1.1 * e + 2e-3, (r[0], env_out)
@@ -260,34 +258,104 @@ def test_bench_shape_fp32_product_vs_oracle():
     assert all(abs(v - 1) < 1e-3 for v in lr.values()), lr
 
 
-@pytest.mark.parametrize('yml,img,bs', [('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 1536, 2),
-                                        ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2)])
-def test_bench_shape_layers_bf16_vs_emulation(yml, img, bs):
-    """Every top-level layer of a bench model alone at its bench resolution on the inputs the fp32 oracle sees there
-    (tests/module_parity.py): the bf16 product module and the bf16-storage emulation of the oracle module against the
-    fp32 oracle module, for one seeded upstream gradient.  DMA-YOLO-l @1536 (config 3) and config 5 @1920 -- there
-    C3TR's global attention runs over 60 x 60 = 3,600 tokens per image, as in the bench.  The emulation is 'bf16_sink'
-    with the layer's input gradient rounded as the product stores it (module_parity): round 4's 1.13x excess on every
-    plain Conv was exactly that one rounding.  Bounds per layer (round 5 measured, profiles/r05/layers_*.log: product /
-    emulation input-gradient error 0.89-1.21x, parameter-gradient error 0.78-1.21x, CoorAttention the highest at
-    1.21x, norms within 2e-4 of fp32 for both): input and parameter gradient relative L2 <= 1.25 x the emulation's + 5e-4,
-    norm ratios within 1e-3 of 1 or of 1.5 x the emulation's own deviation + 2e-3 (config 5's C3TR over 3,600 tokens
-    loses 42-51 % of its gradient to bf16 storage in product and emulation alike, norms 0.9962 vs 0.9978)."""
-    from module_parity import layer_parity, fmt
+def _layer_bounds(rows, k=1.25, floor=5e-4, outputs=True):
+    """per layer: output, input- and parameter-gradient relative L2 <= k x the emulation's + floor; norm ratios within
+    1e-3 of 1 or of 1.5 x the emulation's own deviation + 2e-3.  Returns the violations."""
     bad = []
-    n = 0
-    for i, name, row in layer_parity(yml, img, bs):
-        print(fmt(i, name, row), flush=True)
-        n += 1
+    for i, name, row in rows:
         if isinstance(row, Exception):
             if i != 0:  # the stem's product module takes the space-to-depth image input, not the oracle's
                 bad.append((i, name, repr(row)))
             continue
-        checks = [('dx', row['dx']), ('w', row.get('w'))]
-        for kd, v in checks:
-            if v is not None and v[0] > 1.25 * v[1] + 5e-4:
+        for kd in (('y', 'dx', 'w') if outputs else ('dx', 'w')):
+            v = row.get(kd)
+            if v is not None and v[0] > k * v[1] + floor:
                 bad.append((i, name, kd, v))
         for kd in ('dxn', 'wn'):
             if kd in row and abs(row[kd][0] - 1) > max(1e-3, 1.5 * abs(row[kd][1] - 1) + 2e-3):
                 bad.append((i, name, kd, row[kd]))
-    assert n >= 15 and not bad, bad
+    return bad
+
+
+def _collect(gen):
+    from module_parity import fmt
+    rows = []
+    for i, name, row in gen:
+        print(fmt(i, name, row), flush=True)
+        rows.append((i, name, row))
+    return rows
+
+
+@pytest.mark.parametrize('yml,img,bs', [('yolov5l-ca-sppfcspc-bifpn-scconv.yaml', 1536, 2),
+                                        ('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2)])
+def test_bench_shape_layers_bf16_vs_emulation(yml, img, bs, monkeypatch):
+    """Every top-level layer of a bench model alone at its bench resolution on the inputs the fp32 oracle sees there
+    (tests/module_parity.py): the bf16 product module and the bf16-storage emulation of the oracle module against the
+    fp32 oracle module, for one seeded upstream gradient.  DMA-YOLO-l @1536 (config 3) and config 5 @1920 -- there
+    C3TR's global attention runs over 60 x 60 = 3,600 tokens per image, as in the bench.  The emulation is 'bf16_sink'
+    with the layer's input gradient rounded as the product stores it (module_parity).  Bounds per layer: output, input
+    and parameter gradient relative L2 <= 1.25 x the emulation's + 5e-4, norm ratios within 1e-3 of 1 or of 1.5 x the
+    emulation's own deviation + 2e-3.
+    Round 5's C3TR rows (0.423 for product, bf16 AND fp16 emulation alike) compared three different dropout masks:
+    TransformerLayer's nn.Dropout(0.1) (common.py:328) was on in all three runs.  With dropout off (module_parity) the
+    row is a real check; config 5 then re-runs its C3TR layers with the product's attention output scaled by 1.1 (a
+    10 % kernel error) and requires the bound to FAIL there."""
+    from module_parity import layer_parity
+    rows = _collect(layer_parity(yml, img, bs))
+    assert len(rows) >= 15
+    bad = _layer_bounds(rows)
+    assert not bad, bad
+    c3tr = [i for i, name, row in rows if name == 'C3TR']
+    if 'xs-tr' in yml:
+        assert c3tr
+        import dmayolo.functional as Fn
+        real = Fn.MHAFn
+
+        class Off10:  # the attention core, 10 % off (forward and, through autograd, backward)
+            @staticmethod
+            def apply(q, k, v, nh):
+                return real.apply(q, k, v, nh) * 1.1
+
+        monkeypatch.setattr(Fn, 'MHAFn', Off10)
+        sab = _collect(layer_parity(yml, img, bs, only=c3tr))
+        monkeypatch.setattr(Fn, 'MHAFn', real)
+        for i, name, row in sab:
+            assert _layer_bounds([(i, name, row)]), (i, 'a 10 % attention error passed the per-layer bound')
+
+
+def test_c5_layers_fp32_product_vs_oracle():
+    """Config 5 @1920 bs2 per layer in fp32 storage (act_dtype float32: the fp32 kernels, fp32 generic attention over
+    3,600 tokens) against the fp32 oracle module on the same inputs and upstream gradient -- the config-5 counterpart of
+    test_bench_shape_fp32_product_vs_oracle, per layer so that CBAM / SPP argmax near-ties do not chain.  No storage
+    rounding on either side: outputs <= 1e-4, input and parameter gradients <= 1e-3 relative L2, norms within 1e-3."""
+    from module_parity import layer_parity
+    rows = _collect(layer_parity('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2, prod='fp32'))
+    assert len(rows) >= 15 and any(name == 'C3TR' for _, name, _ in rows)
+    bad = []
+    for i, name, row in rows:
+        if isinstance(row, Exception):
+            if i != 0:
+                bad.append((i, name, repr(row)))
+            continue
+        if row['y'][0] > 1e-4:
+            bad.append((i, name, 'y', row['y'][0]))
+        for kd in ('dx', 'w'):
+            if kd in row and row[kd][0] > 1e-3:
+                bad.append((i, name, kd, row[kd][0]))
+        for kd in ('dxn', 'wn'):
+            if kd in row and abs(row[kd][0] - 1) > 1e-3:
+                bad.append((i, name, kd, row[kd][0]))
+    assert not bad, bad
+
+
+def test_c5_layers_fp8_vs_emulation():
+    """Config 5's fp8 leg (functional.set_fp8: e4m3 forward of every 3x3 conv with C % 128 == 0, bf16 backward) per
+    layer at its bench resolution 1920 bs2 against the 'fp8_sink' emulation (precision_emu: the same e4m3 quantisation
+    of input and weights, per tensor / per output channel, on top of 'bf16_sink'), both against the fp32 oracle.  The
+    layers' first call quantises just in time with the current amax, as the emulation does.  Bounds as the bf16 layer
+    test: 1.25 x the emulation's error + 5e-4 on outputs and gradients."""
+    from module_parity import layer_parity
+    rows = _collect(layer_parity('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2, prod='fp8'))
+    assert len(rows) >= 15
+    bad = _layer_bounds(rows)
+    assert not bad, bad

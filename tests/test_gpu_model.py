@@ -183,6 +183,41 @@ def test_graphed_detect_equals_eager_forward_and_nms():
         assert sum(d.shape[0] for d in dets) > 0  # conf 0.001 keeps boxes
 
 
+def test_graphed_detect_after_call_recapture():
+    """detect(), then a weight change, then __call__ (which re-records the forward-only graph and its static input),
+    then detect() again: the detect graph keeps its own input buffer and state key, so the second detect re-records
+    with the new weights and reads the new input (it used to replay the old graph on a stale input)"""
+    from dmayolo.models.yolo import Model
+    from dmayolo.infer import GraphedDetector
+    from dmayolo.utils.general import non_max_suppression
+    torch.manual_seed(0)
+    m = Model(os.path.join(CFG, 'yolov5s.yaml'), nc=10, act_dtype=torch.bfloat16).cuda().eval()
+    gd = GraphedDetector(m)
+    g = torch.Generator().manual_seed(6)
+    xs = [torch.randint(0, 256, (1, 3, 256, 320), generator=g, dtype=torch.uint8).cuda() for _ in range(3)]
+
+    def check(dets, z, x):
+        ze = m(x)[0]
+        de = non_max_suppression(ze, 0.01, 0.45, max_det=300)
+        assert torch.equal(z, ze)
+        assert len(dets) == len(de) and all(torch.equal(a, b) for a, b in zip(dets, de))
+
+    with torch.no_grad():
+        dets, (z, _) = gd.detect(xs[0], 0.01, 0.45)
+        check(dets, z, xs[0])
+        det0 = z.clone()
+        for p in m.parameters():  # an in-place weight change torch sees (its _version moves)
+            p.mul_(1.01)
+            break
+        m.model[-1].m[0].bias.add_(0.5)
+        torch.testing.assert_close(gd(xs[1])[0], m(xs[1])[0], rtol=0, atol=0)  # __call__ re-records
+        dets, (z, _) = gd.detect(xs[2], 0.01, 0.45)
+        check(dets, z, xs[2])
+        dets, (z, _) = gd.detect(xs[0], 0.01, 0.45)  # same input as the first call, new weights
+        check(dets, z, xs[0])
+        assert not torch.equal(z, det0)
+
+
 def test_graphed_train_step_matches_eager():
     """train_graph.GraphedTrainStep (fwd + loss + bwd replayed as one HIP graph, optimizer / EMA eager) against
     the eager step on an identical model copy over batches with different target counts (zero-row padding,

@@ -1,7 +1,7 @@
 """Diagnostic: tests/module_parity.py's layer-by-layer parity at a bench shape, printed (product | emulation per
 column; see that module).
 
-python tools/gpu/diag_modules.py <yaml> <img> <bs> [layer ids, comma-separated | all] [emulation mode]
+python tools/gpu/diag_modules.py <yaml> <img> <bs> [layer ids, comma-separated | all] [product: bf16 | fp8 | fp32]
 (DIAG_FP16=1: also the fp16 autocast emulation per layer)
 """
 import os
@@ -14,9 +14,9 @@ from module_parity import layer_parity, fmt  # noqa: E402
 if __name__ == '__main__':
     yml, img, bs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     only = [int(v) for v in sys.argv[4].split(',')] if len(sys.argv) > 4 and sys.argv[4] != 'all' else None
-    mode = sys.argv[5] if len(sys.argv) > 5 else 'bf16_sink'
-    print(f'{yml} @{img} bs{bs}: layer type | dx rel prod emu | dx norm prod emu | params rel prod emu | params norm '
-          f'prod emu | worst param (rel prod / emu)', flush=True)
-    print(f'emulation: {mode}', flush=True)
-    for i, name, row in layer_parity(yml, img, bs, only, fp16=os.environ.get('DIAG_FP16') == '1', mode=mode):
+    prod = sys.argv[5] if len(sys.argv) > 5 else 'bf16'
+    print(f'{yml} @{img} bs{bs}: layer type | output rel prod emu | dx rel prod emu | dx norm prod emu | params rel '
+          f'prod emu | params norm prod emu | worst param (rel prod / emu)', flush=True)
+    print(f'product: {prod}', flush=True)
+    for i, name, row in layer_parity(yml, img, bs, only, fp16=os.environ.get('DIAG_FP16') == '1', prod=prod):
         print(fmt(i, name, row), flush=True)
