@@ -199,7 +199,7 @@ class ArenaDDP(torch.nn.Module):
             if c is not None:
                 view.copy_(c)
         unused = [i for i, p in enumerate(self.reduced) if id(p) not in bw.seen]
-        if self.find_unused and self.world > 1:
+        if self.find_unused:
             # which parameters some rank used: a MAX over the ranks' used flags, read on the host (DDP's find-unused
             # mode synchronises the same way); every rank issues it, whether or not it has locally unused parameters
             flags = torch.ones(len(self.reduced), dtype=torch.int32)
@@ -208,8 +208,6 @@ class ArenaDDP(torch.nn.Module):
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.pg)
             used = flags.cpu()
             unused = [i for i in unused if used[i] != 0]
-        elif self.find_unused:
-            unused = []  # one rank: what it did not use, nobody used
         for i in unused:  # no gradient on this rank but on some other: it gets the rank average (DDP semantics)
             p = self.reduced[i]
             p.grad = self._slice(bw.buf, p)

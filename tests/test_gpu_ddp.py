@@ -172,7 +172,7 @@ def _rccl1_worker(rank, world, port, out, topology):
         m1, nc, img = _model(topology)
         m2 = copy.deepcopy(m1)
         fup = any(isinstance(mm, torch.nn.MultiheadAttention) for mm in m1.modules())
-        net = ArenaDDP(m1, bucket_cap_mb=1.0, first_bucket_mb=0.25, find_unused_parameters=fup)
+        net = ArenaDDP(m1, bucket_cap_mb=0.25, first_bucket_mb=0.05, find_unused_parameters=fup)
         net.trace = []
         t1 = Trainer(m1, m1.hyp, BS, nb=100, world_size=1, rank=0, net=net, ema=False)
         t2 = Trainer(m2, copy.deepcopy(m2.hyp), BS, nb=100, world_size=1, rank=-1, ema=False)
