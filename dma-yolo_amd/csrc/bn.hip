@@ -502,53 +502,28 @@ inline bool vec_ok(int VW, int C, long s1, long s2, long s3, const void* p1, con
 
 }  // namespace
 
-inline int env_knob(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-// rows per thread and loop iteration of the bf16 streaming kernels (DMY_BN_UNROLL: 1, 2 or 4) and the grid cap
-// (DMY_BN_GRID blocks of 256 threads)
-inline int bn_unroll() {
-  static const int u = env_knob("DMY_BN_UNROLL", 1);
-  return u;
-}
-inline int vec_grid(long M, int C, int VW) {
-  static const int cap = env_knob("DMY_BN_GRID", 4096);
+// grid of the vectorised streaming passes (blocks of 256 threads, RB rows per block and loop step), capped per kind
+// (tools/gpu/bw_micro.py, profiles/r05/bn_grid_ab.log, M x C = 1.18M x 128 and 295k x 512 bf16): the reduce passes
+// (bn_stats, bn_bwd_reduce: per-block partial rows) are fastest at 2048 blocks (5.0 -> 5.5 TB/s: fewer partial rows to
+// write and sum), the elementwise ones (bn_act_fwd, bn_bwd_apply) at 16384 (apply 4.7 -> 5.2 TB/s, act 5.3 -> 5.5: more
+// rows in flight per CU); 4096 for the rest.  Round 6 fixed the caps and removed their switches, with the unroll
+// variants (DMY_BN_UNROLL 2 / 4, never faster than 1) and the row-order switch.
+inline int vec_grid_cap(long M, int C, int VW, int cap) {
   const int RB = 256 / (C / VW);
   return grid_cap(ceil_div(M, (long)RB * 8), cap);
 }
-// the grid caps of the streaming passes, measured per kind (tools/gpu/bw_micro.py, profiles/r05/bn_grid_ab.log, M x C =
-// 1.18M x 128 and 295k x 512 bf16): the reduce passes (bn_stats, bn_bwd_reduce: per-block partial rows) are fastest at
-// 2048 blocks (5.0 -> 5.5 TB/s: fewer partial rows to write and sum), the elementwise ones (bn_act_fwd, bn_bwd_apply)
-// at 16384 (apply 4.7 -> 5.2 TB/s, act 5.3 -> 5.5: more rows in flight per CU).  DMY_BN_GRID_RED / DMY_BN_GRID_EW
-inline int vec_grid_red(long M, int C, int VW) {
-  static const int cap = env_knob("DMY_BN_GRID_RED", 2048);
-  const int RB = 256 / (C / VW);
-  return grid_cap(ceil_div(M, (long)RB * 8), cap);
-}
-inline int vec_grid_ew(long M, int C, int VW) {
-  static const int cap = env_knob("DMY_BN_GRID_EW", 16384);
-  const int RB = 256 / (C / VW);
-  return grid_cap(ceil_div(M, (long)RB * 8), cap);
-}
-// row order of the streaming passes, as a bit mask (DMY_BN_ORDER): 1 = bn_act_fwd, 2 = bn_bwd_reduce, 4 = bn_bwd_apply
-// walk M from the END.  A pass that reads a tensor in the reverse of the order its producer (or the previous pass)
-// touched it starts on the lines still resident in the 256 MiB Infinity Cache instead of the ones evicted first:
-// conv writes z -> act reads z backwards (tail hot) and writes y backwards -> the next conv reads y forwards (head hot);
-// data-grad writes dy -> reduce reads dy, z forwards -> apply reads them backwards (tail hot) and writes dz backwards ->
-// the conv's data-grad reads dz forwards (head hot).  Default 5; same-box A/B on DMA-1536 (profiles/r03/ab_bnorder.log):
-// 0 -> 147.0 / 146.9, 3 -> 147.3 / 147.4, 5 -> 147.5 / 147.6 img/s (the tensors are 0.15-2.4 GB, so only their
-// Infinity-Cache-sized ends benefit)
-inline int bn_order() {
-  static const int o = env_knob("DMY_BN_ORDER", 5);
-  return o;
-}
-#define BN_UNROLL(KERNEL, ...)                                   \
-  switch (bn_unroll()) {                                         \
-    case 4: KERNEL(4, __VA_ARGS__); break;                       \
-    case 2: KERNEL(2, __VA_ARGS__); break;                       \
-    default: KERNEL(1, __VA_ARGS__); break;                      \
-  }
+inline int vec_grid(long M, int C, int VW) { return vec_grid_cap(M, C, VW, 4096); }
+inline int vec_grid_red(long M, int C, int VW) { return vec_grid_cap(M, C, VW, 2048); }
+inline int vec_grid_ew(long M, int C, int VW) { return vec_grid_cap(M, C, VW, 16384); }
+// row order of the streaming passes: bn_act_fwd and bn_bwd_apply walk M from the END.  A pass that reads a tensor in
+// the reverse of the order its producer (or the previous pass) touched it starts on the lines still resident in the
+// 256 MiB Infinity Cache instead of the ones evicted first: conv writes z -> act reads z backwards (tail hot) and writes
+// y backwards -> the next conv reads y forwards (head hot); data-grad writes dy -> reduce reads dy, z forwards -> apply
+// reads them backwards (tail hot) and writes dz backwards -> the conv's data-grad reads dz forwards (head hot).  Same-box
+// A/B on DMA-1536 (profiles/r03/ab_bnorder.log): all forwards 147.0 / 146.9, reduce + act reversed 147.3 / 147.4, act +
+// apply reversed (kept) 147.5 / 147.6 img/s (the tensors are 0.15-2.4 GB, so only their Infinity-Cache-sized ends
+// benefit)
+constexpr int kRevAct = 1, kRevReduce = 0, kRevApply = 1;
 
 DMY_API int dmy_bn_partial_rows(long M) {
   long p = (M + 255) / 256;
@@ -594,10 +569,8 @@ DMY_API int dmy_bn_act_fwd(int dtype, const void* z, long zps, const float* scal
   const bool vec = vec_ok(VW, C, zps, yps, res ? rps : 0, z, y, res) && C / VW <= 256;
   if (vec) {
     const int g = vec_grid_ew(M, C, VW);
-#define ACT_GO(U_, ...) bn_act_fwd_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C, bn_order() & 1)
-    if (dtype) { BN_UNROLL(ACT_GO, 0) }
-#undef ACT_GO
-    else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C, bn_order() & 1);
+    if (dtype) bn_act_fwd_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C, kRevAct);
+    else bn_act_fwd_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, scale, shift, act, (const float*)res, rps, (float*)y, yps, M, C, kRevAct);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);
     if (dtype) bn_act_fwd_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, scale, shift, act, (const bf16*)res, rps, (bf16*)y, yps, M, C);
@@ -635,10 +608,8 @@ DMY_API int dmy_bn_bwd_reduce(int dtype, const void* z, long zps, const void* dy
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, 0, z, dy, nullptr) && C / VW <= 256) {
     const int g = vec_grid_red(M, C, VW);
-#define RED_GO(U_, ...) bn_bwd_reduce_vec<bf16, false, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, (bn_order() >> 1) & 1)
-    if (dtype) { BN_UNROLL(RED_GO, 0) }
-#undef RED_GO
-    else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, (bn_order() >> 1) & 1);
+    if (dtype) bn_bwd_reduce_vec<bf16, false><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, kRevReduce);
+    else bn_bwd_reduce_vec<float, false><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, M, C, pdb, pdg, kRevReduce);
     return (int)hipGetLastError();
   }
   const int P = dmy_bn_partial_rows(M);
@@ -676,10 +647,8 @@ DMY_API int dmy_bn_bwd_apply(int dtype, const void* z, long zps, const void* dy,
   const int VW = dtype ? 8 : 4;
   if (vec_ok(VW, C, zps, dps, dzps, z, dy, dz) && C / VW <= 256) {
     const int g = vec_grid_ew(M, C, VW);
-#define APP_GO(U_, ...) bn_bwd_apply_vec<bf16, U_><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C, (bn_order() >> 2) & 1)
-    if (dtype) { BN_UNROLL(APP_GO, 0) }
-#undef APP_GO
-    else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C, (bn_order() >> 2) & 1);
+    if (dtype) bn_bwd_apply_vec<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C, kRevApply);
+    else bn_bwd_apply_vec<float><<<g, 256, 0, st>>>((const float*)z, zps, (const float*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (float*)dz, dzps, M, C, kRevApply);
   } else {
     const int g = grid_cap(ceil_div(M * C, 256), 8192);
     if (dtype) bn_bwd_apply_scalar<bf16><<<g, 256, 0, st>>>((const bf16*)z, zps, (const bf16*)dy, dps, scale, shift, mean, invstd, act, ca, cb, cc, (bf16*)dz, dzps, M, C);

@@ -25,12 +25,6 @@
 #include <atomic>
 #include <cmath>
 
-// s_setprio(1) around the MFMA cluster of the LDS-DMA main loops (cdna_hip_programming.md §5.5 T5);
-// compile-time A/B switch, off unless measured faster
-#ifndef DMY_SETPRIO
-#define DMY_SETPRIO 0
-#endif
-
 namespace {
 
 constexpr int NT = 256;  // 4 waves, 2x2 over the block tile
@@ -1121,7 +1115,7 @@ template <int N> DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N
 
 // Main loop with the whole K step's fragments read up front (64 VGPRs), the next stage's LDS-DMA
 // issued while those reads are in flight, then the step's 32 MFMAs back to back.
-template <int BM, int BN, int NS, bool IF, class LD>
+template <int BM, int BN, int NS, class LD>
 DEV void mainloop4(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int lane) {
   using C3_ = Cfg3<BM, BN, NS>;
   constexpr int PER = C3_::APW + C3_::BPW;
@@ -1132,7 +1126,6 @@ DEV void mainloop4(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
     if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (IF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
     const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
     const bf16* Bs = As + BM * BK;
     bf16x8 a[2][4], b[2][4];
@@ -1144,16 +1137,14 @@ DEV void mainloop4(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
       for (int j = 0; j < 4; ++j) b[h][j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!IF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
+    if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
-    if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -1186,127 +1177,13 @@ DEV void mainloop3(LD& ld, int nk, char* smem, f32x4 (&acc)[4][4], int wid, int 
   }
 }
 
-// The data-grad output's producer BatchNorm (+ activation): a stride-1 data-grad whose output is the complete
-// gradient of a train-mode BN layer's output writes that layer's backward-reduce partials itself (sum du and
-// sum du * xhat per 64-row block, du = dy * act'(z * scale + shift), xhat = (z - mean) * invstd -- bn.hip
-// bn_bwd_reduce_vec's arithmetic on the stored bf16 values), so bn_bwd_reduce's second read of dy disappears.
-// z == nullptr: off.
-struct BnB {
-  const bf16* z;
-  long zps;
-  const float* scale;
-  const float* shift;
-  const float* mean;
-  const float* invstd;
-  int act;
-  float* pdb;
-  float* pdg;
-};
-
-// store loop of the data-grad epilogue with the fused partials: ONE partial row per BM-row tile (the partial array
-// is 2 * 4 B * C per 256 rows of dx, 1/64 of dx's bytes).  Thread t keeps the 8 channels cv = t % CPR and rows
-// t / CPR + G * it; per-thread sums -> xor-shuffles over the lanes sharing cv -> per-wave rows in LDS (the ct region,
-// after a barrier) -> summed over waves in wave order.
-template <int BM, int BN, int NTH>
-DEV void store_dgrad_bn(bf16* ct, bf16* __restrict__ y, int accumulate, const Geom& g, int tm, long m0, int n0,
-                        const BnB& bb) {
-  constexpr int RS = BN + 8, CPR = BN / 8, G = NTH / CPR, IT = BM / G, NW = NTH / 64;
-  static_assert(NTH % CPR == 0 && BM % G == 0 && CPR < 64 && BN >= 128, "store_dgrad_bn tiling");
-  const long M = (long)g.N * g.OH * g.OW;
-  const int cv = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
-  const int n = n0 + cv * 8;
-  const bool colok = n < g.K;
-  float sc[8], sh[8], mu[8], is[8], sa[8], sb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) sc[j] = sh[j] = mu[j] = is[j] = sa[j] = sb[j] = 0.f;
-  if (colok) {  // K % 8 == 0 on this path: a live column vector has all 8 channels
-    ldf<8>(bb.scale + n, sc);
-    ldf<8>(bb.shift + n, sh);
-    ldf<8>(bb.mean + n, mu);
-    ldf<8>(bb.invstd + n, is);
-  }
-  // rows in groups of HALF iterations: every z (and accumulate) load of a group is issued before any is consumed,
-  // so a thread keeps HALF 16-B loads in flight instead of one dependent load per row
-  constexpr int HALF = IT >= 8 ? 8 : IT;
-#pragma unroll
-  for (int i0 = 0; i0 < IT; i0 += HALF) {
-    uint4 zv[HALF], ov[HALF];
-#pragma unroll
-    for (int q = 0; q < HALF; ++q) {
-      const long m = m0 + r0 + (i0 + q) * G;
-      const long mc = (m < M && colok) ? m : m0;  // in-range row for the masked lanes
-      zv[q] = *reinterpret_cast<const uint4*>(bb.z + mc * bb.zps + (colok ? n : n0));
-      if (accumulate) ov[q] = *reinterpret_cast<const uint4*>(y + mc * g.yps + (colok ? n : n0));
-    }
-#pragma unroll
-    for (int q = 0; q < HALF; ++q) {
-      const int row = r0 + (i0 + q) * G;
-      const long m = m0 + row;
-      if (m < M && colok) {
-        uint4 v = *reinterpret_cast<const uint4*>(ct + row * RS + cv * 8);
-        if (accumulate) {
-          float a[8], b[8];
-          unpack<bf16>(v, a);
-          unpack<bf16>(ov[q], b);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) a[j] += b[j];
-          v = pack<bf16>(a);
-        }
-        *reinterpret_cast<uint4*>(y + m * g.yps + n) = v;
-        float f[8], zf[8];
-        unpack<bf16>(v, f);
-        unpack<bf16>(zv[q], zf);
-        float ag[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ag[j] = zf[j] * sc[j] + sh[j];
-        act_grad_n<8>(bb.act, ag);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float du = f[j] * ag[j];
-          sa[j] += du;
-          sb[j] += du * (zf[j] - mu[j]) * is[j];
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int o = CPR; o < 64; o <<= 1)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sa[j] += __shfl_xor(sa[j], o, 64);
-      sb[j] += __shfl_xor(sb[j], o, 64);
-    }
-  __syncthreads();  // every read of ct is done: it becomes the [wave][2][BN] reduction buffer
-  float* red = reinterpret_cast<float*>(ct);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane < CPR) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[(wid * 2 + 0) * BN + cv * 8 + j] = sa[j];
-      red[(wid * 2 + 1) * BN + cv * 8 + j] = sb[j];
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < BN; c += NTH) {
-    float s1 = 0.f, s2 = 0.f;
-    for (int w = 0; w < NW; ++w) {
-      s1 += red[(w * 2 + 0) * BN + c];
-      s2 += red[(w * 2 + 1) * BN + c];
-    }
-    if (n0 + c < g.K) {
-      bb.pdb[(long)tm * g.K + n0 + c] = s1;
-      bb.pdg[(long)tm * g.K + n0 + c] = s2;
-    }
-  }
-}
-
 // Epilogue of the v3 GEMM kernels: (+bias) -> bf16 tile in LDS `ct` [BM][BN+8] + BN partials.  Partial rows
 // follow the v2 numbering of dmy_conv_fwd_partial_rows: one per 64 rows of M when K > 64, one per 32 otherwise.
 // Then 16-B stores (inference epilogue / accumulate / stride-2 class pixel mapping as configured).
 template <int BM, int BN, int NS, bool DG, int BUF, int WTR = 64>
 DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __restrict__ bias, bf16* __restrict__ y,
                      float* __restrict__ psum, float* __restrict__ psq, int accumulate, const Geom& g, int tm,
-                     long m0, int n0, const v3::S2Cls& cls, const Epi& ep, const BnB& bb = BnB{}) {
+                     long m0, int n0, const v3::S2Cls& cls, const Epi& ep) {
   using C3_ = Cfg3<BM, BN, NS, WTR>;
   constexpr int NI = WTR / 16, NQ = NI / 2;  // 16-row fragments and 32-row groups per wave
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1366,12 +1243,6 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
     }
   }
   __syncthreads();
-  if constexpr (DG && BUF != 3 && BN >= 128 && BM <= 256) {  // (the 512-row tile would spill its 8 partial rows)
-    if (bb.z != nullptr) {
-      store_dgrad_bn<BM, BN, C3_::NTH>(ct, y, accumulate, g, tm, m0, n0, bb);
-      return;
-    }
-  }
   constexpr int CPR = BN / 8;
   for (int e = threadIdx.x; e < BM * CPR; e += C3_::NTH) {
     const int row = e / CPR, cv = e % CPR;
@@ -1400,83 +1271,6 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
       v = pack<bf16>(a);
     }
     *dst = v;
-  }
-}
-
-// Persistent 1x1 (pure GEMM, stride 1) forward / data-grad for C % 64 == 0: gridDim.x blocks walk the tiles
-// t = blockIdx.x, + gridDim.x, ... through ONE continuous LDS-DMA ring of K steps, so the next tile's first
-// stages are in flight while this tile's epilogue runs (the epilogue stages through its own LDS region).  The
-// 1x1 layers have 1..8 K steps per tile, where a one-tile block spent its time in the prologue load latency and
-// the epilogue stores with nothing else in flight on the CU.
-template <int BM, int BN, bool DG>
-__global__ void __launch_bounds__(BM * BN / 64) conv_p1_persist(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                               const float* __restrict__ bias, bf16* __restrict__ y,
-                                                               float* __restrict__ psum, float* __restrict__ psq,
-                                                               int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                               unsigned wbytes, Epi ep) {
-  constexpr int NS = 3;
-  using C3_ = Cfg3<BM, BN, NS>;
-  constexpr int PER = C3_::APW + C3_::BPW;
-  constexpr int CTB = BM * (BN + 8) * 2;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * C3_::STAGE + CTB];
-  bf16* ct = reinterpret_cast<bf16*>(smem + NS * C3_::STAGE);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
-  const long M = (long)g.N * g.OH * g.OW;
-  const int ntiles = gm * gn, nk = g.C / BK, G = gridDim.x;
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
-  // issue cursor (tile, k step) and its loader
-  int lt = t, lk = 0;
-  using LD = FwdLdsB<BM, BN, NS, true, DG>;
-  LD ld(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
-  auto issue = [&](int s) {
-    if (lt >= ntiles) return;
-    ld.issue(smem + (s % NS) * C3_::STAGE, wid);
-    if (++lk == nk) {
-      lk = 0;
-      lt += G;
-      if (lt < ntiles) ld = LD(x, w, g, M, (long)(lt / gn) * BM, (lt % gn) * BN, wid, lane, xbytes, wbytes);
-    }
-  };
-  const int my_tiles = (ntiles - 1 - blockIdx.x) / G + 1, total = my_tiles * nk;
-  issue(0);
-  if (total > 1) issue(1);
-  int s = 0;
-  for (; t < ntiles; t += G) {
-    const int tm = t / gn, tn = t % gn;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt, ++s) {
-      if (s + 1 < total) vm_wait<PER>();
-      else vm_wait<0>();
-      __builtin_amdgcn_s_barrier();
-      const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
-      const bf16* Bs = As + BM * BK;
-      bf16x8 a[2][4], b[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[h][i] = frag_sw(As, wm * 64 + i * 16, h * 32, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[h][j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + NS - 1 < total) issue(s + NS - 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
-    }
-    v3_epilogue<BM, BN, NS, DG, 1>(acc, ct, bias, y, psum, psq, accumulate, g, tm, (long)tm * BM, tn * BN,
-                                   v3::S2Cls{0, 0, 0, 0}, ep);
-    vm_wait<0>();  // stores (and any accumulate loads) drained: the loop's counted waits see only stage loads
   }
 }
 
@@ -1523,7 +1317,7 @@ template <int BM, int BN, int NS, int WTR, bool DG, bool LANE = false>
 __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
     const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias, bf16* __restrict__ y,
     float* __restrict__ psum, float* __restrict__ psq, int /*accumulate: 0*/, Geom g, int gm, int gn, unsigned xbytes,
-    unsigned wbytes, unsigned ybytes, int nprow, Epi ep, unsigned rbytes, int ff) {
+    unsigned wbytes, unsigned ybytes, int nprow, Epi ep, unsigned rbytes) {
   using PP = P1P<BM, BN, NS, WTR>;
   using C3_ = typename PP::C3_;
   constexpr int PER = PP::PER, NI = PP::NI;
@@ -1618,7 +1412,7 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         vm_wait<0>();  // other epilogue shapes (accumulate, 32-pixel partial rows): wait for everything
       }
       __builtin_amdgcn_s_barrier();
-      if (!ff && s + NS - 1 < total) issue(s + NS - 1);
+      if (s + NS - 1 < total) issue(s + NS - 1);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
       const bf16* Bs = As + BM * BK;
 #pragma unroll
@@ -1628,11 +1422,6 @@ __global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_p1p(
         for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
 #pragma unroll
         for (int i = 0; i < NI; ++i) a[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
-        if (ff && h == 0) {  // fragments first (DMY_P1P_FF): the next stage's LDS-DMA after this half-step's reads
-          __builtin_amdgcn_sched_barrier(0);
-          if (s + NS - 1 < total) issue(s + NS - 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -1752,7 +1541,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
                                                             float* __restrict__ psum, float* __restrict__ psq,
                                                             int accumulate, Geom g, int gm, int gn, unsigned xbytes,
-                                                            unsigned wbytes, S2Cls cls, Epi ep, BnB bb) {
+                                                            unsigned wbytes, S2Cls cls, Epi ep) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1766,23 +1555,23 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_v3(const bf16* __restri
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // BUF: 0 = FwdLds, 1 = buffer loader (fragments first), 2 = buffer loader (DMA first), 3 = buffer loader,
-  // stride-2 data-grad parity class `cls` (only the class's taps: ceil((KH - kh0) / 2) x ceil((KW - kw0) / 2))
+  // BUF: 0 = FwdLds, 1 = buffer loader, 3 = buffer loader, stride-2 data-grad parity class `cls` (only the class's
+  // taps: ceil((KH - kh0) / 2) x ceil((KW - kw0) / 2))
   const int nk = BUF == 3 ? ((g.KH - ((cls.a + g.P) & 1) + 1) / 2) * ((g.KW - ((cls.b + g.P) & 1) + 1) / 2) * (g.C / BK)
                           : (g.KH * g.KW * g.C + BK - 1) / BK;
   if constexpr (BUF == 3) {
     FwdLdsB<BM, BN, NS, false, true, true> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes, cls);
-    mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+    mainloop4<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   } else if constexpr (BUF > 0) {
     FwdLdsB<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
-    mainloop4<BM, BN, NS, BUF == 2>(ld, nk, smem, acc, wid, lane);
+    mainloop4<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   } else {
     FwdLds<BM, BN, NS, P1, DG> ld(x, w, g, M, m0, n0, wid, lane);
     mainloop3<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   }
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, BUF>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
-                                    cls, ep, bb);
+                                    cls, ep);
 }
 
 // All four output-parity classes of a stride-2 data-grad in ONE launch. Block u (XCD-contiguous order, xcd_remap) takes
@@ -1814,177 +1603,21 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_dgrad_s2_v3(const bf16* __r
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = ((gv.KH - ((a + gv.P) & 1) + 1) / 2) * ((gv.KW - ((b + gv.P) & 1) + 1) / 2) * (gv.C / BK);
   FwdLdsB<BM, BN, NS, false, true, true> ld(dy, wt, gv, M, m0, n0, wid, lane, xbytes, wbytes, cls);
-  mainloop4<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+  mainloop4<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
   v3_epilogue<BM, BN, NS, true, 3>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr, accumulate, gv, tm,
-                                    m0, n0, cls, Epi{}, BnB{});
-}
-
-// ---------------------------------------------------------------- persistent stride-2 data-grad (conv_s2p, round 5)
-// The stride-2 data-grads (SCConv's k4 and the backbone's downsampling convs, models/common.py:1303, 50-77) as four
-// parity-class GEMMs of 1, 2, 2 and 4 taps: with 128-256 dy channels a class tile has only 2-16 K steps, and the
-// one-tile-per-block kernels above spent most of each tile in the load prologue and the LDS-staged epilogue with
-// nothing in flight (357-760 TF/s on the DMA-1536 shapes, round 4).  Here the (class, row tile, column tile) units of
-// all four classes run through conv_p1p's persistent structure: one continuous LDS-DMA ring of K steps across a
-// block's units (the next unit's first stages load under this unit's last MFMAs and its epilogue), transposed MFMAs
-// (D[channel][pixel]) so a lane ends with 8 consecutive channels of one pixel, and a register epilogue that maps the
-// class row straight to its dx pixel (2 i2 + a, 2 j2 + b) with one 16-B buffer store (accumulating data-grads load
-// the previous dx vector first).  Units are dispatched class-fastest in XCD-contiguous order, so the four classes over
-// the same dy rows run together on one XCD and share its L2.
-template <int BM, int BN, int NS, int WTR>
-__global__ void __launch_bounds__((BM / WTR) * (BN / 64) * 64) conv_s2p(const bf16* __restrict__ dy,
-                                                                      const bf16* __restrict__ wt, bf16* __restrict__ dx,
-                                                                      int accumulate, Geom g, int gmax, int gn,
-                                                                      unsigned xbytes, unsigned wbytes, unsigned ybytes) {
-  using PP = P1P<BM, BN, NS, WTR>;
-  using C3_ = typename PP::C3_;
-  constexpr int PER = PP::PER, NI = PP::NI;
-  static_assert(NS == 2 || NS == 3, "ring depth");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * C3_::STAGE];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid % C3_::WM, wn = wid / C3_::WM;
-  const int q = lane >> 4, pl = lane & 15;
-  const int nunits = 4 * gmax * gn, G = gridDim.x;
-  const int kpt = g.K / BK;  // K steps per tap
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dx, ybytes);
-  // unit L (dispatch order) -> class (a, b), row tile, column tile; returns its K steps (0: no rows in this class)
-  auto unit = [&](int L, int& a, int& b, int& tm, int& tn) -> int {
-    const int u = xcd_remap(L, nunits);
-    a = (u >> 1) & 1;
-    b = u & 1;
-    const int t = u >> 2;
-    tm = t / gn;
-    tn = t % gn;
-    const int oh = (g.H - a + 1) / 2, ow = (g.W - b + 1) / 2;
-    if (oh <= 0 || ow <= 0 || (long)tm * BM >= (long)g.N * oh * ow) return 0;
-    return ((g.KH - ((a + g.P) & 1) + 1) / 2) * ((g.KW - ((b + g.P) & 1) + 1) / 2) * kpt;
-  };
-  auto view = [&](int a, int b) {  // the class's GEMM view (conv_dgrad_s2_v3)
-    Geom gv = g;
-    gv.H = g.OH; gv.W = g.OW; gv.C = g.K; gv.xps = g.yps; gv.K = g.C; gv.S = 2;
-    gv.OH = (g.H - a + 1) / 2; gv.OW = (g.W - b + 1) / 2; gv.yps = g.xps;
-    return gv;
-  };
-  using LD = FwdLdsB<BM, BN, NS, false, true, true, 2, WTR>;
-  // issue cursor: unit lL (dispatch index), its K steps lnk, step lk
-  int lL = (int)blockIdx.x, la = 0, lb = 0, ltm = 0, ltn = 0, lnk = 0, lk = 0;
-  while (lL < nunits && (lnk = unit(lL, la, lb, ltm, ltn)) == 0) lL += G;
-  if (lL >= nunits) return;
-  Geom lgv = view(la, lb);
-  LD ld(dy, wt, lgv, (long)lgv.N * lgv.OH * lgv.OW, (long)ltm * BM, ltn * BN, wid, lane, xbytes, wbytes,
-        S2Cls{la, lb, g.H, g.W});
-  int issued = 0;
-  auto issue = [&]() {
-    if (lL >= nunits) return;
-    ld.issue(smem + (issued % NS) * C3_::STAGE, wid);
-    ++issued;
-    if (++lk == lnk) {
-      lk = 0;
-      do lL += G;
-      while (lL < nunits && (lnk = unit(lL, la, lb, ltm, ltn)) == 0);
-      if (lL < nunits) {
-        lgv = view(la, lb);
-        ld = LD(dy, wt, lgv, (long)lgv.N * lgv.OH * lgv.OW, (long)ltm * BM, ltn * BN, wid, lane, xbytes, wbytes,
-                S2Cls{la, lb, g.H, g.W});
-      }
-    }
-  };
-  issue();
-  if (NS == 3) issue();
-  int s = 0, r = 0;
-  for (int L = (int)blockIdx.x; L < nunits; L += G) {
-    int a, b, tm, tn;
-    const int nk = unit(L, a, b, tm, tn);
-    if (nk == 0) continue;
-    const Geom gv = view(a, b);
-    const long M = (long)gv.N * gv.OH * gv.OW;
-    f32x4 acc[NI][4];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt, ++s) {
-      // stage s landed: younger VMEM ops allowed = the next stage (if issued) + the previous unit's epilogue stores
-      // when they were issued after stage s (kt < NS - 1 on every unit but the block's first)
-      const bool nxt = issued > s + 1;
-      const bool epi = r > 0 && kt < NS - 1;
-      if (epi && accumulate) {
-        vm_wait<0>();
-      } else if (epi) {
-        if (nxt) vm_wait<PER + PP::NST>();
-        else vm_wait<PP::NST>();
-      } else {
-        if (nxt) vm_wait<PER>();
-        else vm_wait<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      if (issued < s + NS) issue();
-      const bf16* As = reinterpret_cast<const bf16*>(smem + (s % NS) * C3_::STAGE);
-      const bf16* Bs = As + BM * BK;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 af[NI], bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
-#pragma unroll
-        for (int i = 0; i < NI; ++i) af[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      }
-    }
-    // ---- register epilogue: acc[i][j][rr] = dX[class row m0 + wm WTR + 16 i + pl][channel n0 + wn 64 + 16 j + 4 q + rr]
-    const long mw = (long)tm * BM + wm * WTR;
-    const int nw = tn * BN + wn * 64;
-    const int chq = (q & 1) * 16 + (q >> 1) * 8;
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const long m = mw + 16 * i + pl;
-      const int j2 = (int)(m % gv.OW);
-      const long tq = m / gv.OW;
-      const int i2 = (int)(tq % gv.OH), bb = (int)(tq / gv.OH);
-      const long pix = ((long)bb * g.H + 2 * i2 + a) * g.W + 2 * j2 + b;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        const f32x4 &p0 = acc[i][2 * jp], &p1 = acc[i][2 * jp + 1];
-        const int n = nw + 32 * jp + chq;
-        const unsigned off = (m < M && n < g.C) ? (unsigned)((pix * g.xps + n) * 2) : kBufOob;
-        if (accumulate) {
-          const u4 o = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
-          float f[8];
-          unpack<bf16>(make_uint4(o[0], o[1], o[2], o[3]), f);
-          // this lane's 8 channels: (p0, p1) of 4 channels each, exchanged across the lane pair by the swap below --
-          // add in fp32 after the swap so the order matches the plain path
-          const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[0], p0[1]), pk2_bf16(p1[0], p1[1]), false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[2], p0[3]), pk2_bf16(p1[2], p1[3]), false, false);
-          float v[8];
-          unpack<bf16>(make_uint4(s0[0], s1[0], s0[1], s1[1]), v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += f[e];
-          const uint4 w4 = pack<bf16>(v);
-          __builtin_amdgcn_raw_buffer_store_b128(u4{w4.x, w4.y, w4.z, w4.w}, ry, off, 0, 0);
-        } else {
-          const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[0], p0[1]), pk2_bf16(p1[0], p1[1]), false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(p0[2], p0[3]), pk2_bf16(p1[2], p1[3]), false, false);
-          __builtin_amdgcn_raw_buffer_store_b128(u4{s0[0], s1[0], s0[1], s1[1]}, ry, off, 0, 0);
-        }
-      }
-    }
-    ++r;
-  }
+                                    m0, n0, cls, Epi{});
 }
 
 // ---------------------------------------------------------------- wide tile: 256 x 256 block, 128 x 64 per wave
 // Per K step a wave reads (128 + 64) x 64 bf16 from LDS for 64 MFMAs, against (64 + 64) x 64 for 32 in the
 // 64 x 64 wave tile: the LDS array (256 B/clk/CU) stops pacing the MFMAs on the MFMA-bound layers.  2 LDS stages
 // of 64 KiB (loads of step k + 1 in flight during step k), 8 waves (2 x 4), 128 accumulator registers per lane.
-// FF (fragments first): the first half-step's 12 fragment reads are issued before the next stage's LDS-DMA, so
-// the reads the MFMAs wait on are not queued behind the DMA's LDS writes.  DMY_WIDE_FF = 1 (default), 0 = DMA first.
-// Measured (round 4, profiles/r04/wide_ff_ab.log, cold caches): 3x3 256 @96^2 fwd 430 -> 418 us, 512 @96^2 fwd 1201 ->
-// 1171, dgrad 1156 -> 1114, 1024 @48^2 fwd 1254 -> 1211; DMA-1536 step 153.8 / 153.6 -> 154.8 / 154.4 img/s
-template <int BM, int BN, int NS, bool FF, class LD>
+// Fragments first: the first half-step's 12 fragment reads are issued before the next stage's LDS-DMA, so the reads
+// the MFMAs wait on are not queued behind the DMA's LDS writes.  Measured against DMA first (round 4,
+// profiles/r04/wide_ff_ab.log, cold caches): 3x3 256 @96^2 fwd 430 -> 418 us, 512 @96^2 fwd 1201 -> 1171, dgrad 1156 ->
+// 1114, 1024 @48^2 fwd 1254 -> 1211; DMA-1536 step 153.8 / 153.6 -> 154.8 / 154.4 img/s
+template <int BM, int BN, int NS, class LD>
 DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int lane) {
   using C3_ = Cfg3<BM, BN, NS, 128>;
   constexpr int PER = C3_::APW + C3_::BPW;
@@ -1995,7 +1628,6 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
     if (NS == 3 && kt + 1 < nk) vm_wait<PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (!FF && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
     const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * C3_::STAGE);
     const bf16* Bs = As + BM * BK;
 #pragma unroll
@@ -2005,7 +1637,7 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
       for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = frag_sw(As, wm * 128 + i * 16, h * 32, lane);
-      if (FF && h == 0) {
+      if (h == 0) {
         __builtin_amdgcn_sched_barrier(0);
         if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
         __builtin_amdgcn_sched_barrier(0);
@@ -2023,8 +1655,7 @@ template <int BM, int BN, bool P1, bool DG>
 __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
-                                                  Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep,
-                                                  BnB bb, int ff) {
+                                                  Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
   constexpr int NS = 2;
   static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
   using C3_ = Cfg3<BM, BN, NS, 128>;
@@ -2042,11 +1673,10 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
   FwdLdsB<BM, BN, NS, P1, DG, false, 2, 128> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
-  if (ff) mainloop_w<BM, BN, NS, true>(ld, nk, smem, acc, wid, lane);
-  else mainloop_w<BM, BN, NS, false>(ld, nk, smem, acc, wid, lane);
+  mainloop_w<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
-                                      n0, S2Cls{0, 0, 0, 0}, ep, bb);
+                                      n0, S2Cls{0, 0, 0, 0}, ep);
 }
 
 // ---------------------------------------------------------------- 256 x 256 half-tile pipeline (conv_fwd_8p, round 5)
@@ -2156,8 +1786,7 @@ template <bool P1, bool DG>
 __global__ void __launch_bounds__(512) conv_fwd_8p(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                    const float* __restrict__ bias, bf16* __restrict__ y,
                                                    float* __restrict__ psum, float* __restrict__ psq, int accumulate,
-                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep,
-                                                   BnB bb) {
+                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
   constexpr int BM = 256, BN = 256;
   __shared__ __attribute__((aligned(1024))) char smem[p8::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2261,7 +1890,7 @@ __global__ void __launch_bounds__(512) conv_fwd_8p(const bf16* __restrict__ x, c
   if (!grp) P8_BAR();  // group 0 catches up with group 1's extra barrier
   __syncthreads();
   v3_epilogue<BM, BN, 2, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0, n0,
-                                     S2Cls{0, 0, 0, 0}, ep, bb);
+                                     S2Cls{0, 0, 0, 0}, ep);
 }
 #undef P8_BAR
 
@@ -2278,18 +1907,17 @@ __global__ void __launch_bounds__(512) conv_fwd_8p(const bf16* __restrict__ x, c
 // G3: the same streaming GEMM over a 3x3 stride-1 pad-1 gather of a 16-channel input (the space-to-depth stem of every
 // yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
 // 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
-template <int KD, int NTH, bool G3 = false, bool EPI = false>
+template <int KD, int NTH, bool G3 = false>
 __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                 long M, int NC, int ng, long xps, long yps, unsigned xbytes,
-                                                int ntiles, int kwrow, int H, int W, Epi ep, int pf) {
+                                                int ntiles, int kwrow, int H, int W) {
   extern __shared__ __attribute__((aligned(16))) char p1s_smem[];
   constexpr int PITCH = KD + 8, KC = KD / 32, NW = NTH / 64;
   // 32-channel groups per column pass: 2 (64-column passes, whole 128-B output lines per pixel) up to 512 threads, 1 at
-  // 768 / 1024 threads (3-4 waves per SIMD: no room for the second group's accumulators) and in the KD 256 eval variant
-  // (its epilogue registers)
-  constexpr int NG2 = NTH <= 512 && !(EPI && KD > 128) ? 2 : 1, CP = 32 * NG2;
+  // 768 / 1024 threads (3-4 waves per SIMD: no room for the second group's accumulators)
+  constexpr int NG2 = NTH <= 512 ? 2 : 1, CP = 32 * NG2;
   bf16* ws = reinterpret_cast<bf16*>(p1s_smem);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* red = reinterpret_cast<float*>(p1s_smem + ng * PITCH * 2) + wid * 64;  // this wave's [2][32] partials
@@ -2314,7 +1942,7 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
   const int chq = (q & 1) * 16 + (q >> 1) * 8;
   // PF: the next tile's X fragments are loaded while this tile's column passes run (training variants, KD <= 128: 64
   // more VGPRs; DMY_P1S_PF = 0 turns it off at run time)
-  constexpr bool PF = !G3 && !EPI && KD <= 128;
+  constexpr bool PF = !G3 && KD <= 128;
   const int tstride = gridDim.x * NW;
   bf16x8 xf[4][KC];
   auto load_x = [&](bf16x8 (&dst)[4][KC], int tt) {
@@ -2344,11 +1972,11 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
     }
   };
   const int t0 = blockIdx.x * NW + wid;
-  if (PF && pf && t0 < ntiles) load_x(xf, t0);
+  if (PF && t0 < ntiles) load_x(xf, t0);
   for (int t = t0; t < ntiles; t += tstride) {
     const long p0 = (long)t * 64;
     bf16x8 xn[4][KC];
-    if (PF && pf) {
+    if (PF) {
       if (t + tstride < ntiles) load_x(xn, t + tstride);
     } else {
       load_x(xf, t);
@@ -2438,16 +2066,7 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
           v.w = s1[1];
           if (m < M) {
             uint4* dst = reinterpret_cast<uint4*>(y + m * yps + nb + gr * 32 + chq);
-            if (EPI && ep.on) {  // eval BN scale / shift + act (+ residual) on the bf16-rounded conv output (epi_store)
-              const int n = nb + gr * 32 + chq;
-              float f[8], r8[8], sc[8], sh[8];
-              unpack<bf16>(v, f);
-              if (ep.res != nullptr)
-                unpack<bf16>(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(ep.res) + m * ep.rps + n), r8);
-              epi_coef8(ep, n, sc, sh);
-              epi_apply8(ep.act, f, sc, sh, ep.res != nullptr ? r8 : nullptr);
-              v = pack<bf16>(f);
-            } else if (accumulate) {
+            if (accumulate) {
               float f[8], o[8];
               unpack<bf16>(v, f);
               unpack<bf16>(*dst, o);
@@ -2460,123 +2079,11 @@ __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, c
         }
       }
     }
-    if (PF && pf) {
+    if (PF) {
 #pragma unroll
       for (int pb = 0; pb < 4; ++pb)
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) xf[pb][kc] = xn[pb][kc];
-    }
-  }
-}
-
-// ---------------------------------------------------------------- small-M inference GEMM (conv_sk)
-// Batch-1 eval forwards (M = 2,304 .. 147,456 output pixels) are latency-bound: on the 256-row LDS-DMA tiles a 1x1
-// 96^2 256 -> 256 layer (4.7 MB in, 4.7 MB out) took 25-35 us of GPU time for ~2 us of HBM traffic.  Here a block is
-// 4 waves x 16 output pixels x BN channels: the X fragments of a wave's 16 pixels go from HBM straight into registers
-// (16-B buffer loads; a k x k gather with the tap's range check for 3x3 / strided layers, zeros past the reduction),
-// the block's BN x KC slice of W is LDS-DMA'd into the swizzled 128-B-row image of the v3 kernels, double-buffered over
-// KC-deep chunks (one chunk = the whole reduction of a <= KC-channel 1x1 layer: one memory round trip), and the MFMA runs
-// transposed (D[ch][px] = W X^T) so a lane ends with 4 consecutive channels of one pixel: a permlane16 swap pairs two
-// 16-channel blocks into 8 consecutive channels, and the inference epilogue (bias, bf16 rounding, eval-BN scale /
-// shift, activation, residual) is applied in registers before one 16-B store -- the value contract of the other paths
-// (conv output rounded to bf16, then the epilogue in fp32).  Grid = (M / 64) x (K / BN) blocks, XCD-contiguous.
-template <int BN, int KC>
-__global__ void __launch_bounds__(256) conv_sk(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                               const float* __restrict__ bias, bf16* __restrict__ y, Geom g, Epi ep,
-                                               int gm, int gn, unsigned xbytes, unsigned wbytes) {
-  constexpr int NCB = BN / 16, KS = KC / 32, SUB = KC / 64;
-  constexpr int CHUNK = BN * KC * 2, PIECES = CHUNK / 1024 / 4;  // 1-KiB LDS-DMA pieces per wave per chunk
-  static_assert(PIECES * 4 * 1024 == CHUNK && NCB % 2 == 0, "conv_sk tile");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * CHUNK];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, pl = lane & 15, q = lane >> 4;
-  const int tile = xcd_remap(blockIdx.x, gm * gn);
-  const int tm = tile / gn, tn = tile % gn;
-  const long M = (long)g.N * g.OH * g.OW;
-  const int Ktot = g.KH * g.KW * g.C, n0 = tn * BN, nch = (Ktot + KC - 1) / KC;
-  const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rw = make_rsrc(w, wbytes);
-  // this lane's pixel (X fragments: B operand column pl, k chunk q)
-  const long m = (long)tm * 64 + wid * 16 + pl;
-  const bool mv = m < M;
-  const int mm = mv ? (int)m : 0, ow = mm % g.OW, oh = (mm / g.OW) % g.OH, bi = mm / (g.OW * g.OH);
-  const int ih0 = oh * g.S - g.P, iw0 = ow * g.S - g.P;
-  // W pieces: piece pi = wid * PIECES + j covers sub-block pi / (BN / 8), rows (pi % (BN / 8)) * 8 + lane / 8; the lane
-  // reads the logical 16-B chunk (lane & 7) ^ (row & 6) of its row (frag_sw's swizzle on a lane-linear image)
-  const int wl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
-  auto issue = [&](int ck, char* buf, bf16x8 (&xr)[KS]) {
-#pragma unroll
-    for (int j = 0; j < PIECES; ++j) {
-      const int pi = wid * PIECES + j, sb = pi / (BN / 8), row = (pi % (BN / 8)) * 8 + (lane >> 3);
-      const int k = ck * KC + sb * 64 + wl, n = n0 + row;
-      blds16(rw, (n < g.K && k < Ktot) ? (unsigned)(n * Ktot + k) * 2u : kBufOob, buf + pi * 1024);
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int k = ck * KC + ks * 32 + q * 8;
-      unsigned off = kBufOob;
-      if (mv && k < Ktot) {
-        if (p1) {
-          off = (unsigned)(m * g.xps + k) * 2u;
-        } else {
-          const int tap = k / g.C, c = k - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-          const int ih = ih0 + kh, iw = iw0 + kw;
-          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-            off = (unsigned)(((bi * g.H + ih) * g.W + iw) * (int)g.xps + c) * 2u;
-        }
-      }
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-      xr[ks] = *reinterpret_cast<const bf16x8*>(&v);
-    }
-  };
-  f32x4 acc[NCB];
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 xc[KS], xn[KS];
-  issue(0, smem, xc);
-  for (int ck = 0; ck < nch; ++ck) {
-    vm_wait<0>();
-    __builtin_amdgcn_s_barrier();  // chunk ck's W image complete; every wave is done with the other buffer
-    if (ck + 1 < nch) issue(ck + 1, smem + ((ck + 1) & 1) * CHUNK, xn);
-    const bf16* ws = reinterpret_cast<const bf16*>(smem + (ck & 1) * CHUNK);
-    const int kv = Ktot - ck * KC;  // live k in this chunk (zero-filled past it: skip those MFMAs)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks * 32 >= kv) break;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const bf16x8 wf = frag_sw(ws + (ks >> 1) * BN * 64, cb * 16, (ks & 1) * 32, lane);
-        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xc[ks], acc[cb], 0, 0, 0);
-      }
-    }
-    if (ck + 1 < nch) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) xc[ks] = xn[ks];
-    }
-  }
-  // epilogue: lane holds channels n0 + cb * 16 + q * 4 + r of pixel m
-  const int chq = (q & 1) * 16 + (q >> 1) * 8;
-#pragma unroll
-  for (int pr = 0; pr < NCB / 2; ++pr) {
-    f32x4 a = acc[2 * pr], b = acc[2 * pr + 1];
-    const int nb = n0 + pr * 32;
-    if (bias != nullptr && nb < g.K) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] += bias[nb + q * 4 + r];
-        b[r] += bias[nb + 16 + q * 4 + r];
-      }
-    }
-    const auto s0 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[0], a[1]), pk2_bf16(b[0], b[1]), false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(pk2_bf16(a[2], a[3]), pk2_bf16(b[2], b[3]), false, false);
-    uint4 v;
-    v.x = s0[0];
-    v.y = s1[0];
-    v.z = s0[1];
-    v.w = s1[1];
-    const int n = nb + chq;  // 8 consecutive channels
-    if (mv && nb < g.K) {
-      if (ep.on) epi_store<bf16, 8>(ep, reinterpret_cast<const bf16*>(&v), y + m * g.yps + n, n, g.K, m, true);
-      else *reinterpret_cast<uint4*>(y + m * g.yps + n) = v;
     }
   }
 }
@@ -2587,23 +2094,12 @@ __global__ void __launch_bounds__(256) conv_sk(const bf16* __restrict__ x, const
 // writes its fp32 partial tile to a workspace slab, splitk_epi_kernel sums the slabs in split order and applies
 // bias + the inference epilogue (eval BN, act, residual) to the bf16-rounded sum -- the same value contract as
 // the one-launch path (deterministic; rounding order differs from the unsplit kernel).
-//
-// In-launch combine (fused = 1): the block that draws the last ticket of its tile sums the tile's slabs in split order and
-// applies the epilogue itself -- splitk_epi_kernel's arithmetic, so the same bits -- instead of a second launch reading
-// every slab back (MI355X_MICROARCH / cdna_hip_programming split-K recipe: plain slab stores, vmcnt drain, barrier, ONE
-// lane's agent-scope release + drain before a relaxed agent ticket; the reducer's one lane acquires at agent scope, drains,
-// and the barrier covers the workgroup; any XCD placement of a tile's splits is correct).  The tickets live in a device
-// array zeroed at load and re-zeroed by each tile's reducer, so launches that use it must not run concurrently on two
-// streams: launch_splitk gives the in-launch combine to the first stream that uses it only.
-constexpr int kSplitCnt = 8192;
-__device__ int g_split_cnt[kSplitCnt];
+
 
 template <int BM, int BN, int NS, bool P1>
 __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                                float* __restrict__ ws, Geom g, int gm, int gn, int per,
-                                                               unsigned xbytes, unsigned wbytes, int fused,
-                                                               const float* __restrict__ bias, bf16* __restrict__ y,
-                                                               Epi ep) {
+                                                               unsigned xbytes, unsigned wbytes) {
   using C3_ = Cfg3<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2622,7 +2118,7 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __res
   if (steps > 0) {
     FwdLdsB<BM, BN, NS, P1, false> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
     ld.skip(k0);
-    mainloop4<BM, BN, NS, false>(ld, steps, smem, acc, wid, lane);
+    mainloop4<BM, BN, NS>(ld, steps, smem, acc, wid, lane);
   }
   const int wm = wid % C3_::WM, wn = wid / C3_::WM;
   float* slab = ws + (long)split * M * g.K;
@@ -2636,46 +2132,6 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_fwd_split(const bf16* __res
         const int n = n0 + wn * 64 + j * 16 + (lane & 15);
         if (m < M && n < g.K) slab[m * g.K + n] = acc[i][j][r];
       }
-  if (!fused) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave's slab stores drained; the ring is idle, so smem carries the reducer flag
-  int* flag = reinterpret_cast<int*>(smem);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(&g_split_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (int)gridDim.y - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&g_split_cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  // this tile's outputs: the slabs summed in split order, + bias, rounded to bf16, epilogue (splitk_epi_kernel's math)
-  constexpr int CPR = BN / 8, NTH = BM * BN / 64;
-  const int sp = (int)gridDim.y;
-  for (int e = threadIdx.x; e < BM * CPR; e += NTH) {
-    const int row = e / CPR, c = n0 + (e % CPR) * 8;
-    const long m = m0 + row;
-    if (m >= M || c >= g.K) continue;
-    float f[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = 0.f;
-    for (int q = 0; q < sp; ++q) {
-      const float4* src = reinterpret_cast<const float4*>(ws + ((long)q * M + m) * g.K + c);
-      const float4 a = src[0], b = src[1];
-      f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
-      f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
-    }
-    bf16 t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = __float2bfloat16(f[j] + (bias != nullptr ? bias[c + j] : 0.f));
-    if (ep.on) epi_store<bf16, 8>(ep, t, y + m * g.yps + c, c, g.K, m, true);
-    else *reinterpret_cast<uint4*>(y + m * g.yps + c) = *reinterpret_cast<const uint4*>(t);
-  }
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3) forward, MX-scaled MFMA
@@ -2949,7 +2405,6 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
       if (NS == 3 && kt + 1 < nk) vm_wait<8>();
       else vm_wait<0>();
       __builtin_amdgcn_s_barrier();
-      if (BUF == 2 && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
       const bf16* Bs = As + 64 * BM;
       bf16x8 a[2][4], b[2][4];
@@ -2963,7 +2418,6 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
       __builtin_amdgcn_sched_barrier(0);
       if (BUF == 1 && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -2971,7 +2425,6 @@ __global__ void __launch_bounds__(256) conv_wgrad_v3(const bf16* __restrict__ x,
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
-      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   } else if (nk > 0) {
     WgradLds<NS> ld(x, dy, g, m0, n0, kt0, wid, lane);
@@ -3329,7 +2782,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
       __builtin_amdgcn_sched_barrier(0);
       if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -3337,7 +2789,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
-      if constexpr (DMY_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   vm_wait<0>();
@@ -3359,90 +2810,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_v4(const bf16* __restrict__ x,
   for (int e = threadIdx.x; e < BM * BN; e += 512) {
     const int row = e / BN, m = m0 + row;
     if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
-  }
-}
-
-// Weight-grad, wide tile (round 4): BM x BN = 256 x 256 (256 output channels x 256 GEMM columns), 8 waves of 128 x 64
-// (WM = 2 x WN = 4, 128 accumulators per lane), a 2-stage LDS-DMA ring of 64 KiB stages (the next stage streams in
-// under the current one's MFMAs, as the forward wide tile).  Against the 256 x 128 tile of conv_wgrad_v4: a wave reads
-// (128 + 64) x 64 bf16 of LDS per K step for 64 MFMAs instead of (64 + 64) x 64 for 32, and a split's dy rows are read
-// once per 256 columns instead of once per 128 -- the 1x1 weight-grads with >= 256 input and output channels run at
-// 750-865 TF/s (30-35 % of the MFMA peak) on the 256 x 128 tile.  The fp32 tile leaves through LDS in two 128-row
-// halves (the whole 256 x 260 fp32 tile would not fit).
-template <int BM, int BN>
-__global__ void __launch_bounds__(512) conv_wgrad_w(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                    float* __restrict__ dw, int kt_per_split, Geom g, int gm, int gn,
-                                                    unsigned xbytes, unsigned dybytes) {
-  constexpr int WM = BM / 128, NS = 2;
-  static_assert(WM * (BN / 64) == 8, "8 waves of 128 x 64");
-  using LD = WgradLdsNB<BM, BN, 8>;
-  constexpr int STAGE = WgradLdsN<BM, BN>::STAGE;
-  constexpr int RS = BN + 4;
-  constexpr int CT = 128 * RS * 4;  // one 128-row half of the fp32 tile
-  constexpr int LDSB = NS * STAGE > CT ? NS * STAGE : CT;
-  __shared__ __attribute__((aligned(1024))) char smem[LDSB];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid % WM, wn = wid / WM;
-  const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int tile = lin % (gm * gn), split = lin / (gm * gn);
-  const int tm = tile / gn, tn = tile % gn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const long NP = (long)g.N * g.OH * g.OW;
-  const int nk_all = (int)((NP + 63) / 64);
-  const int kt0 = split * kt_per_split;
-  const int nk = min(nk_all, kt0 + kt_per_split) - kt0;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk > 0) {
-    LD ld(x, dy, g, m0, n0, kt0, wid, lane, xbytes, dybytes);
-    ld.issue(smem, wid);
-    for (int kt = 0; kt < nk; ++kt) {
-      vm_wait<0>();  // stage kt landed (the only stage in flight)
-      __builtin_amdgcn_s_barrier();
-      if (kt + 1 < nk) ld.issue(smem + ((kt + 1) % NS) * STAGE, wid);  // under this step's MFMAs
-      const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
-      const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 a[8], b[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = frag_k<BN>(Bs, wn * 64 + j * 16, h * 32, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = frag_k<BM>(As, wm * 128 + i * 16, h * 32, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  }
-  vm_wait<0>();
-  __syncthreads();
-  float* ct = reinterpret_cast<float*>(smem);
-  const int Ntot = g.KH * g.KW * g.C;
-  static_assert(512 % BN == 0, "epilogue column must be fixed per thread");
-  const int c = threadIdx.x % BN, n = n0 + c;
-  const long coff = wgrad_col(g, n);
-#pragma unroll
-  for (int hh = 0; hh < WM; ++hh) {  // 128-row halves: the waves of wave row hh stage theirs, every thread stores
-    if (wm == hh) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ct[(i * 16 + 4 * (lane >> 4) + r) * RS + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 128 * BN; e += 512) {
-      const int row = e / BN, m = m0 + hh * 128 + row;
-      if (m < g.K && n < Ntot) wgrad_out(g, dw, split, (long)m * Ntot + coff, ct[row * RS + c]);
-    }
-    __syncthreads();
   }
 }
 
@@ -3562,10 +2929,9 @@ DEV bf16x8 frag_halo(const bf16* Bs, int kh, int kw, int ch0, int k0, int lane) 
 // waves are 1 (m) x 4 (n), wave tile BM x 144 (4 A + 9 B fragments per 36 MFMAs instead of 2 + 9 per 18): the
 // halo fragment reads, which bound the 64-channel layers on the LDS port, are amortised over twice the rows
 template <int BM, int NP = 1>
-__global__ void __launch_bounds__(256, (BM == 128 && NP == 2) ? 1 : 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+__global__ void __launch_bounds__(256, 2) conv_wgrad_tap(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                          float* __restrict__ dw, int kt_per_split, Geom g, int gm,
-                                                         int gn, int nk_all, unsigned xbytes, unsigned dybytes,
-                                                         int ff) {
+                                                         int gn, int nk_all, unsigned xbytes, unsigned dybytes) {
   using LD = WgradTapLds<BM, NP>;
   constexpr int NS = 3, STAGE = LD::STAGE;
   constexpr int TM = NP == 2 ? BM / 16 : BM / 32;           // NP 1: 2 (m) x 2 (n) waves; NP 2: 1 x 4
@@ -3595,20 +2961,14 @@ __global__ void __launch_bounds__(256, (BM == 128 && NP == 2) ? 1 : 2) conv_wgra
       if (kt + 1 < nk) vm_wait<LD::APW + 2 * NP>();
       else vm_wait<0>();
       __builtin_amdgcn_s_barrier();
-      if (!ff && kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
+      if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
       const bf16* As = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE);
       const bf16* Bs = reinterpret_cast<const bf16*>(smem + (kt % NS) * STAGE + LD::A_BYTES + wpl * 8192);
-      constexpr int HU = (BM == 128 && NP == 2) ? 1 : 2;  // the 288-accumulator tile: one k half live at a time
-#pragma unroll HU
+#pragma unroll
       for (int h = 0; h < 2; ++h) {
         bf16x8 a[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) a[i] = frag_k<BM>(As, wm * (BM / 2) + i * 16, h * 32, lane);
-        if (ff && h == 0) {  // fragments first (DMY_TAP_FF): the next stage's DMA after the first A reads
-          __builtin_amdgcn_sched_barrier(0);
-          if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * STAGE, wid);
-          __builtin_amdgcn_sched_barrier(0);
-        }
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
           const int f = wn * 9 + j, tap = f >> 1;
@@ -3700,7 +3060,7 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
                                                         bf16* __restrict__ y, float* __restrict__ psum,
                                                         float* __restrict__ psq, Geom g, int twn, int thn, int ntiles,
                                                         int per, unsigned xbytes, unsigned wbytes, unsigned ybytes,
-                                                        int accumulate, Epi ep, unsigned rbytes, int ff) {
+                                                        int accumulate, Epi ep, unsigned rbytes) {
   // the eval instantiation keeps the 64 channels' scale / shift after the ring (512 B, written before the first barrier)
   __shared__ __attribute__((aligned(1024))) char smem[halo::LDS + (EP ? 512 : 0)];
   if (EP && threadIdx.x < 128) {
@@ -3769,7 +3129,7 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
   for (int u = u0, it = 0; u < u1; ++u, ++it) {
     __builtin_amdgcn_s_barrier();  // halo(u) landed for every wave; every wave is done with the other buffer
     const char* const hl = smem + halo::WBYTES + (it & 1) * halo::HBYTES;
-    if (!ff && u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
+    if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
     int b, oh0, ow0;
     tile_pos(u, b, oh0, ow0);
     unsigned mrow[2], prow[2];
@@ -3821,12 +3181,6 @@ __global__ void __launch_bounds__(256, 1) conv3_halo64(const bf16* __restrict__ 
       }
     };
     load_half(0, fa[0], fb[0]);
-    if (ff) {  // fragments first (DMY_HALO_FF): the next halo's DMA after the first half-tap's reads and the
-      // accumulate / residual loads, so neither queues behind it
-      __builtin_amdgcn_sched_barrier(0);
-      if (u + 1 < u1) issue_halo(u + 1, smem + halo::WBYTES + ((it + 1) & 1) * halo::HBYTES);
-      __builtin_amdgcn_sched_barrier(0);
-    }
 #pragma unroll
     for (int h = 0; h < 18; ++h) {
       if (h + 1 < 18) load_half(h + 1, fa[(h + 1) & 1], fb[(h + 1) & 1]);
@@ -4022,115 +3376,49 @@ inline bool v3_ok(int C, long xps, int K, long yps, const void* x, const void* w
 
 // gv = GEMM view (rows N*OH*OW, columns K, gather tensor H x W x C with stride xps); BN partials need
 // 64-row wave rows, numbered 4 per 256-row tile (= dmy_conv_fwd_partial_rows when K > 64)
-inline int conv_buf_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_CONV_BUF");
-    return e ? atoi(e) : 1;
-  }();
-  return t;
-}
-
-// tile of the 1x1 (pure GEMM) layers: 0 = 256 x 128, 3 stages; 1 = 128 x 128, 2 stages (2 blocks / CU);
-// 2 = 128 x 128, 3 stages; 3 = 256 x 64, 2 stages (2 blocks / CU); 4 = 128 x 64, 3 stages (2 blocks / CU)
-inline int p1_tile_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_P1_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  return t;
-}
-
+// Routing of the bf16 training / inference convolutions.  Round 6 removed the measured-and-rejected variants and their
+// environment switches (DESIGN.md §3.1 keeps their numbers): the persistent 1x1 GEMM (conv_p1_persist: 15-40 % slower,
+// profiles/r02/ab_p1_persist.log), the small-M GEMM (conv_sk, profiles/r03/det_sk_ab.log), small-grid LDS-DMA tiles
+// (DMY_V3_FILL, profiles/r02/ab_fill.log), the persistent stride-2 class kernel (conv_s2p, gpurun_out/r5/ab_s2p.log),
+// the wide 256 x 256 weight-grad tile (conv_wgrad_w, profiles/r04/wgrad_wide_ab.log), the two-plane 128-row tap
+// weight-grad (profiles/r05/wgrad_tap_np128_ab.log), the in-launch split-K combine (profiles/r03/det_splitk_fused_ab.log),
+// the half-tile pipeline on 3x3 tiles (gpurun_out/r5/ab_w8p.log), the streaming GEMM's 1x1 eval epilogue
+// (profiles/r04/det_p1s_ep_ab.log) and the fragments-first orders of the halo / tap / persistent 1x1 loops
+// (profiles/r04/halo_tap_ff_ab.log, p1p_ff_ab.log).  What is left has one path per shape class.
 inline int num_cus();
-// persistent 1x1 GEMM kernel (v3::conv_p1_persist): 0 = off (default, one tile per block), 1 = on.  Measured
-// 15-40 % SLOWER on every DMA-YOLO / yolov5s 1x1 shape (profiles/r02/ab_p1_persist.log): one 4-wave block per CU
-// draining its stores before the next tile's steps loses to the hardware's block turnover at 8 waves per CU.
-inline int p1_persist_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_P1_PERSIST");
-    return e ? atoi(e) : 0;
-  }();
-  return t;
-}
-
-// wide 256 x 256 tiles (v3::conv_fwd_w) for GEMM views with at least this many columns (0 = off).  Default 256:
-// +9..21 % on every DMA-YOLO / yolov5s shape with >= 256 columns and >= one block per CU, 0.66-0.76x at 128
-// columns (half the tile idle) or with fewer blocks than CUs (profiles/r02/ab_wide.log)
-inline int wide_min_cols() {
-  static int t = [] {
-    const char* e = getenv("DMY_CONV_WIDE");
-    return e ? atoi(e) : 256;
-  }();
-  return t;
-}
-
-// tall 512 x 128 tiles (v3::conv_fwd_w) for k > 1 GEMM views with 65..128 columns and >= 4 blocks per CU: 0 = off,
-// 1 = on (default).  +4..8 % on the 128-channel 3x3 layers of DMA-YOLO / config 5, mixed (0.94..1.10) on 1x1 and on
-// smaller grids (profiles/r02/ab_tall.log)
-inline int tall_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_CONV_TALL");
-    return e ? atoi(e) : 1;
-  }();
-  return t;
-}
-
-// 1x1 streaming GEMM (v3::conv_p1s): DMY_P1S = 0 off / 1 (default) forward GEMMs with >= 2x as many columns as their
-// reduction (the output-heavy 1x1 layers, where it measured 1.05-1.38x the LDS-DMA tiles: profiles/r02/ab_p1s.log;
-// on the other 1x1 shapes those tiles already stream at 4.5-6 TB/s and stay faster) / 2 every eligible GEMM (A/B);
-// DMY_P1S_NTH = threads per block, DMY_P1S_LDS = KiB of W per block (column-group size), DMY_P1S_BPC = blocks per CU
-inline int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-// DMY_W8P: which 256 x 256 tiles run the half-tile pipeline (v3::conv_fwd_8p) instead of the 2-stage wide loop
-// (conv_fwd_w): 0 none, 1 (default) the 1x1 GEMM views, 2 all.  Measured (round 5, gpurun_out/r5/ab_w8p.log, cold
-// caches, two interleaved passes): 1x1 C1024 -> K1024 @48^2 bs32 fwd 200 -> 175 us, dgrad 186 -> 161; C2048 -> K1024
-// fwd 329 -> 288; C4096 -> K1024 fwd 592 -> 526, dgrad 629 -> 595; the other 1x1 shapes and every 3x3 shape within
-// +-1.5 % (3x3 256 @96^2 fwd 411 / 414, 1024 @48^2 1167 / 1149)
-inline int w8p_mode() {
-  static const int t = env_int("DMY_W8P", 1);
-  return t;
-}
-// DMY_P1S = 0 off, 1 (default) the output-heavy forwards (K >= 2 C), 3 those and the output-heavy data-grads, 2 every
-// eligible GEMM view (A/B)
-inline int p1s_mode() {
-  static int t = env_int("DMY_P1S", 1);
-  return t;
-}
-// eval forwards (inference epilogue: eval BN + act + residual in the store loop) on conv_p1s too: DMY_P1S_EP = 1 on,
-// 0 (default) off.  Measured SLOWER on the graph-replayed batch-1 detect (profiles/r04/det_p1s_ep_ab.log, two passes on
-// one box: DMA-1536 p50 4.662 / 4.653 ms on vs 4.524 / 4.515 off; yolov5s@640 0.777 / 0.776 vs 0.768 / 0.785): at
-// batch 1 a 64-pixel wave tile per 8-wave block leaves most CUs idle, where the v2 / LDS-DMA tiles spread the layer
-inline int p1s_eval() {
-  static int t = env_int("DMY_P1S_EP", 0);
-  return t;
-}
+// wide 256 x 256 tiles (v3::conv_fwd_w) for GEMM views with >= 256 columns and at least one block per CU: +9..21 % on
+// every DMA-YOLO / yolov5s shape with >= 256 columns, 0.66-0.76x at 128 columns or below one block per CU
+// (profiles/r02/ab_wide.log).  The 1x1 views among them run the half-tile pipeline (v3::conv_fwd_8p; round 5,
+// gpurun_out/r5/ab_w8p.log: C1024 -> K1024 @48^2 bs32 fwd 200 -> 175 us, dgrad 186 -> 161, C4096 -> K1024 fwd 592 ->
+// 526; every 3x3 shape within +-1.5 %, so those keep conv_fwd_w)
+constexpr int kWideMinCols = 256;
+// tall 512 x 128 tiles (v3::conv_fwd_w) for k > 1 GEMM views with 65..128 columns and >= 4 blocks per CU: +4..8 % on
+// the 128-channel 3x3 layers of DMA-YOLO / config 5 (profiles/r02/ab_tall.log)
+// 1x1 streaming GEMM (v3::conv_p1s) for the output-heavy stride-1 1x1 forwards (>= 2x as many columns as reduction):
+// 1.05-1.38x the LDS-DMA tiles there (profiles/r02/ab_p1s.log); on the other 1x1 shapes those tiles already stream at
+// 4.5-6 TB/s and stay faster
 inline bool p1s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
-  if (!p1s_mode() || gv.KH != 1 || gv.KW != 1 || gv.S != 1 || gv.P != 0) return false;
+  if (gv.KH != 1 || gv.KW != 1 || gv.S != 1 || gv.P != 0) return false;
   if (gv.C != 64 && gv.C != 128 && gv.C != 256) return false;
   if (gv.K % 32 != 0 || gv.xps % 8 != 0 || gv.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
     return false;
   return 2.0 * ((double)gv.N * gv.OH * gv.OW * gv.xps) < (double)v3::kBufOob;
 }
-// threads per block of the training stem (DMY_P1S_STEM_NTH): 512 = 64-column passes that write whole 128-B output lines
-// per pixel, 768 = round 2's 32-column passes; 0 (default) = 512 for >= 64 output channels, else 768.  Cold-cache
-// (profiles/r04/stem_ab.log): DMA-1536 stem (64 ch @768^2 bs32) 1483 -> 1185 us, config 5 (64 @960^2 bs8) 585 -> 434 us,
-// but yolov5s (32 ch @320^2 bs64: one 32-column pass either way) 213 -> 242 us with 512, so it keeps 768
-inline int stem_nth(int K) {
-  static const int t = env_int("DMY_P1S_STEM_NTH", 0);
-  return t ? t : (K >= 64 ? 512 : 768);
-}
-// the k3 s1 p1 view of the space-to-depth stem (16 input channels): DMY_P1S_STEM = 0 keeps the LDS-DMA tile
+// threads per block of the training stem: 512 = 64-column passes that write whole 128-B output lines per pixel, for
+// >= 64 output channels; 768 = 32-column passes otherwise.  Cold-cache (profiles/r04/stem_ab.log): DMA-1536 stem (64 ch
+// @768^2 bs32) 1483 -> 1185 us, config 5 (64 @960^2 bs8) 585 -> 434 us, but yolov5s (32 ch @320^2 bs64: one 32-column
+// pass either way) 213 -> 242 us with 512, so it keeps 768
+inline int stem_nth(int K) { return K >= 64 ? 512 : 768; }
+// the k3 s1 p1 view of the space-to-depth stem (16 input channels) on the streaming GEMM with its 3x3 gather
 inline bool stem_s_ok(const Geom& gv, const void* x, const void* w, const void* y) {
-  static const int on = env_int("DMY_P1S_STEM", 1);
-  if (!on || gv.C != 16 || gv.KH != 3 || gv.KW != 3 || gv.S != 1 || gv.P != 1 || gv.OH != gv.H || gv.OW != gv.W) return false;
+  if (gv.C != 16 || gv.KH != 3 || gv.KW != 3 || gv.S != 1 || gv.P != 1 || gv.OH != gv.H || gv.OW != gv.W) return false;
   if (gv.K % 32 != 0 || gv.K > 256 || gv.xps % 8 != 0 || gv.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
     return false;
   return 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps) < (double)v3::kBufOob && (long)gv.N * gv.H * gv.W < (1L << 31);
 }
-template <int KD, int NTH, bool G3 = false, bool EPI = false>
+template <int KD, int NTH, bool G3 = false>
 int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
-                  const Geom& gv, hipStream_t st, int lds_kib, int bpc, const Epi& ep = Epi{}) {
+                  const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
   constexpr int pitch_b = (KD + 8) * 2, scratch = NTH / 64 * 256;
   const long M = (long)gv.N * gv.OH * gv.OW;
   int ng = ((lds_kib * 1024 - scratch) / pitch_b) / 32 * 32;
@@ -4140,7 +3428,7 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   const int lds = ng * pitch_b + scratch;
   static bool raised = false;
   if (!raised) {
-    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     raised = true;
   }
@@ -4150,64 +3438,25 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   if (nbx > maxb) nbx = maxb;
   const dim3 grid((unsigned)nbx, (unsigned)G);
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps);
-  static const int pf = env_int("DMY_P1S_PF", 1);
-  v3::conv_p1s<KD, NTH, G3, EPI><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
-                                                    ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W, ep, pf);
+  v3::conv_p1s<KD, NTH, G3><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
+                                               ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W);
   return (int)hipGetLastError();
 }
+// training forwards: 512 threads, the whole 160 KiB of LDS for the W column group, one block per CU
 inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
-                      const Geom& gv, hipStream_t st, const Epi& ep = Epi{}) {
-  static const int nth = env_int("DMY_P1S_NTH", 512), lds = env_int("DMY_P1S_LDS", 160), bpc = env_int("DMY_P1S_BPC", 1);
-#define P1S_GO(KD_, NTH_)                                                                      \
-  return ep.on ? launch_p1s_kd<KD_, 512, false, true>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc, ep) \
-               : launch_p1s_kd<KD_, NTH_>(x, w, b, y, ps, pq, acc, gv, st, lds, bpc, ep)
-  if (gv.C == 64) {
-    if (nth == 1024) P1S_GO(64, 1024);
-    if (nth == 512) P1S_GO(64, 512);
-    P1S_GO(64, 256);
-  }
-  if (gv.C == 128) {
-    if (nth == 768 || nth == 1024) P1S_GO(128, 768);
-    if (nth == 512) P1S_GO(128, 512);
-    P1S_GO(128, 256);
-  }
-  if (nth >= 512) P1S_GO(256, 512);
-  P1S_GO(256, 256);
-#undef P1S_GO
+                      const Geom& gv, hipStream_t st) {
+  if (gv.C == 64) return launch_p1s_kd<64, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  if (gv.C == 128) return launch_p1s_kd<128, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  return launch_p1s_kd<256, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
 }
 
-// persistent 1x1 GEMM with the register epilogue (v3::conv_p1p): DMY_P1P = 0 off, 1 (default) = 256 x 128 tiles (3
-// stages) for <= p1p_maxn() columns, 2 = 256 x 256 (2 stages, 128-row wave tiles) for >= 256 columns, 3 = 128 x 128 (2 stages, 2 blocks
-// per CU).  Not for the inference epilogue, the fused producer-BN reduce or an accumulating data-grad.
-inline int p1p_mode() {
-  static const int t = env_int("DMY_P1P", 1);
-  return t;
-}
-// default routing: GEMM views with <= DMY_P1P_MAXN columns (cold-cache A/B on the DMA-YOLO 1x1 shapes,
-// profiles/r03/ab_p1p.log: 256 -> 256 @96^2 fwd 118.7 -> 94.8 us, 128 -> 128 @384^2 636 -> 492 us, 4..23 % on every
-// <= 256-column view; 7..15 % SLOWER on the 512..1280-column views, where the 256 x 256 wide tile reads each input
-// row once)
-// small-M (M < 65536: batch-1 detect) 1x1 forwards on conv_p1p's one-wave 64 x 64 tiles: DMY_P1P_SMALL = 1 (off by
-// default: measured SLOWER -- bs1 DMA-1536 detect conv time 5.87 -> 6.45 ms, profiles/r03/det_layers_p1p_small.log;
-// that run also left the trailing zero-pixel BN partial row of 64-row tiles unwritten, fixed since)
-inline int p1p_small() {
-  static const int t = env_int("DMY_P1P_SMALL", 0);
-  return t;
-}
-// eval forwards (inference epilogue) on conv_p1p too: DMY_P1P_EP = 0 off, 1 on
-inline int p1p_eval() {
-  static const int t = env_int("DMY_P1P_EP", 0);
-  return t;
-}
-inline int p1p_maxn() {
-  static const int t = env_int("DMY_P1P_MAXN", 256);
-  return t;
-}
-// per-lane BN partials in conv_p1p (LANE): DMY_P1P_LANE = 1 (default) for training forwards with one column tile
-inline int p1p_lane_mode() {
-  static const int t = env_int("DMY_P1P_LANE", 1);
-  return t;
-}
+// persistent 1x1 GEMM with the register epilogue (v3::conv_p1p): 256 x 128 tiles (3 stages; 256 x 64 for <= 64
+// columns) for GEMM views with <= 256 columns (cold-cache A/B on the DMA-YOLO 1x1 shapes, profiles/r03/ab_p1p.log: 256 ->
+// 256 @96^2 fwd 118.7 -> 94.8 us, 128 -> 128 @384^2 636 -> 492 us, 4..23 % on every <= 256-column view; 7..15 % SLOWER on
+// the 512..1280-column views, where the 256 x 256 wide tile reads each input row once).  Training forwards with one
+// column tile keep per-lane BN partials (LANE).  Not for the inference epilogue, the fused producer-BN reduce or an
+// accumulating data-grad.
+constexpr int kP1pMaxCols = 256;
 // conv_p1p's persistent grid: blocks per CU from the LDS footprint, capped at the tile count, a multiple of 8 (XCDs)
 // BN partial rows written by the last training forward launched on this host thread (dmy_conv_fwd_last_rows).  The
 // persistent kernels (halo, LANE conv_p1p) write one row per wave of their grid; every other kernel writes
@@ -4222,23 +3471,17 @@ inline int p1p_grid(int ntiles, int lds) {
 }
 // the tile configuration launch_p1p picks: f(BM, BN, NS, WTR) as integral constants; -1 when it declines
 template <bool DG, class F>
-int p1p_plan(const Geom& gv, int acc, const Epi& ep, bool small, F&& f) {
+int p1p_plan(const Geom& gv, int acc, const Epi& ep, F&& f) {
   const long M = (long)gv.N * gv.OH * gv.OW;
-  const int nk = gv.C / v3::BK, mode = p1p_mode();
+  const int nk = gv.C / v3::BK;
   const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
   const double rb = ep.res != nullptr ? 2.0 * ((double)(M - 1) * ep.rps + gv.K) : 0.0;
   if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || rb >= (double)v3::kBufOob || nk < 1 ||
-      (ep.res != nullptr && (ep.rps % 8 != 0 || !aligned16(ep.res))) || (mode == 1 && !small && gv.K > p1p_maxn()))
+      (ep.res != nullptr && (ep.rps % 8 != 0 || !aligned16(ep.res))) || gv.K > kP1pMaxCols)
     return -1;
   using std::integral_constant;
 #define P1P_CFG(BM, BN, NS, WTR) \
   return f(integral_constant<int, BM>{}, integral_constant<int, BN>{}, integral_constant<int, NS>{}, integral_constant<int, WTR>{})
-  if (small) {  // small M (batch-1 inference): one-wave 64 x 64 tiles, several blocks per CU, the short K ring
-    if (nk >= 2) P1P_CFG(64, 64, 3, 64);
-    P1P_CFG(64, 64, 2, 64);
-  }
-  if (mode == 3 && gv.K > 64) P1P_CFG(128, 128, 2, 64);
-  if (mode == 2 && gv.K >= 256) P1P_CFG(256, 256, 2, 128);
   if (gv.K > 64) {
     if (nk >= 2) P1P_CFG(256, 128, 3, 64);
     P1P_CFG(256, 128, 2, 64);
@@ -4247,10 +3490,9 @@ int p1p_plan(const Geom& gv, int acc, const Epi& ep, bool small, F&& f) {
 #undef P1P_CFG
 }
 // BN partial rows of a LANE launch (one per wave row of the persistent grid), or 0 when launch_p1p would not use LANE
-inline int p1p_lane_rows(const Geom& gv) {
-  if (!p1p_lane_mode()) return 0;
+inline long p1p_lane_rows(const Geom& gv) {
   const long M = (long)gv.N * gv.OH * gv.OW;
-  return p1p_plan<false>(gv, 0, Epi{}, false, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
+  return p1p_plan<false>(gv, 0, Epi{}, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
     using PP = v3::P1P<decltype(bm)::value, decltype(bn)::value, decltype(ns)::value, decltype(wtr)::value>;
     const int gm = ceil_div(M, decltype(bm)::value), gn = ceil_div(gv.K, decltype(bn)::value);
     const long r = gn == 1 ? (long)p1p_grid(gm * gn, PP::LDS) * PP::C3_::WM : 0;
@@ -4259,42 +3501,34 @@ inline int p1p_lane_rows(const Geom& gv) {
 }
 template <bool DG>
 int launch_p1p(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-               hipStream_t st, unsigned xbytes, unsigned wbytes, const Epi& ep = Epi{}, bool small = false) {
+               hipStream_t st, unsigned xbytes, unsigned wbytes, const Epi& ep, bool lane) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const double yb = 2.0 * ((double)(M - 1) * gv.yps + gv.K);
   const double rb = ep.res != nullptr ? 2.0 * ((double)(M - 1) * ep.rps + gv.K) : 0.0;
-  static const int ff = env_int("DMY_P1P_FF", 0);  // fragments first in conv_p1p's K loop (A/B)
-  return p1p_plan<DG>(gv, acc, ep, small, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
+  return p1p_plan<DG>(gv, acc, ep, [&](auto bm, auto bn, auto ns, auto wtr) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value, NS = decltype(ns)::value, WTR = decltype(wtr)::value;
     using PP = v3::P1P<BM, BN, NS, WTR>;
     const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN), ntiles = gm * gn;
     const int G = p1p_grid(ntiles, PP::LDS);
     if constexpr (!DG) {
-      if (ps != nullptr && !small && gn == 1 && p1p_lane_mode() && (long)G * PP::C3_::WM <= prow_persist_cap()) {
-        // one BN partial row per wave (dmy_conv_fwd_last_rows)
-        t_prow_last = (long)G * PP::C3_::WM;
+      if (lane) {  // one BN partial row per wave (plan_v3: p1p_lane_rows)
         v3::conv_p1p<BM, BN, NS, WTR, false, true><<<(unsigned)G, PP::NTH, 0, st>>>(
-            x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb, ff);
+            x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, (unsigned)yb, G * PP::C3_::WM, ep, (unsigned)rb);
         return (int)hipGetLastError();
       }
     }
     const int nprow = ps != nullptr ? dmy_conv_fwd_partial_rows(M, gv.K) : 0;
     v3::conv_p1p<BM, BN, NS, WTR, DG><<<(unsigned)G, PP::NTH, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
-                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb, ff);
+                                                                      wbytes, (unsigned)yb, nprow, ep, (unsigned)rb);
     return (int)hipGetLastError();
   });
 }
 
-// 3x3 stride-1 64 -> 64-channel layers on the persistent halo kernel (v3::conv3_halo64): DMY_HALO = 0 off, 1 (default)
-// on.  g = the GEMM view (gathered H x W x C with pixel stride xps, output OH x OW x K with stride yps); whole 8 x 32
+// 3x3 stride-1 64 -> 64-channel layers on the persistent halo kernel (v3::conv3_halo64).  g = the GEMM view (gathered H x W x C with pixel stride xps, output OH x OW x K with stride yps); whole 8 x 32
 // output tiles only, at least one tile per CU, no bias / inference epilogue (the callers check those).
-inline int halo_mode() {
-  static const int t = env_int("DMY_HALO", 1);
-  return t;
-}
 inline long halo_units(const Geom& g) { return (long)g.N * (g.H / v3::halo::TH) * (g.W / v3::halo::TW); }
 inline bool halo_ok(const Geom& g, const void* x, const void* w, const void* y) {
-  if (!halo_mode() || !conv_buf_mode() || g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.C != 64 || g.K != 64 ||
+  if (g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.C != 64 || g.K != 64 ||
       g.OH != g.H || g.OW != g.W || g.H % v3::halo::TH != 0 || g.W % v3::halo::TW != 0 || g.xps % 8 != 0 ||
       g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y))
     return false;
@@ -4319,105 +3553,101 @@ int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, con
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps));
   const unsigned yb = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned rb = ep.res != nullptr ? (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * ep.rps)) : 0u;
-  static const int ff = env_int("DMY_HALO_FF", 0);
   if (!DG && ep.on)  // inference epilogue: its own instantiation, so the training kernel's registers are untouched
     v3::conv3_halo64<false, true><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per,
-                                                                           xb, 2u * 64 * 576, yb, acc, ep, rb, ff);
+                                                                           xb, 2u * 64 * 576, yb, acc, ep, rb);
   else
     v3::conv3_halo64<DG><<<(unsigned)G, 64 * v3::halo::NW, 0, st>>>(x, w, y, ps, pq, g, twn, thn, nt, per, xb,
-                                                                    2u * 64 * 576, yb, acc, ep, rb, ff);
+                                                                    2u * 64 * 576, yb, acc, ep, rb);
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------- routing plans
+// One function decides which kernel a bf16 implicit-GEMM launch takes; the launch executes that plan and
+// dmy_conv_fwd_bn_rows reads the BN partial-row count off the same plan, so the two cannot drift.
+enum class Kern { HALO, SPLITK, P1S, STEM, P1P, PIPE8, WIDE, TALL, V3, V2 };
+struct Plan {
+  Kern k;
+  bool buf;   // buffer-descriptor loader (C % 64 == 0, byte offsets < 4 GiB)
+  bool lane;  // P1P: per-lane BN partials, one row per wave of the persistent grid
+  long rows;  // BN partial rows the launch writes (when it writes them)
+};
+// the v3 family for GEMM view gv (forward, or data-grad when DG)
 template <bool DG>
-int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
-              hipStream_t st, const Epi& ep = Epi{}, const v3::BnB& bb = v3::BnB{}, int tov = -1) {
+Plan plan_v3(const Geom& gv, const void* x, const void* w, const void* y, int acc, const Epi& ep) {
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
-  // eval epilogue on the streaming kernels (forward, no accumulate): the residual read as 16-B vectors
-  const bool ep_ok = !ep.on || (!DG && !acc && p1s_eval() && (ep.res == nullptr || (ep.rps % 8 == 0 && aligned16(ep.res))));
-  if (ep_ok && bb.z == nullptr && p1s_ok(gv, x, w, y) &&
-      (p1s_mode() == 2 || ((!DG || p1s_mode() == 3) && gv.K >= 2 * gv.C)))
-    return launch_p1s(x, w, b, y, ps, pq, acc, gv, st, ep);
-  if (!DG && ep_ok && bb.z == nullptr && stem_s_ok(gv, x, w, y))  // the 16-channel 3x3 stem view (p1s, G3 gather)
-    return ep.on ? launch_p1s_kd<160, 768, true, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
-           : stem_nth(gv.K) == 512 ? launch_p1s_kd<160, 512, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep)
-                               : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1, ep);
-  // buffer-descriptor loader: channel count a multiple of the 64-wide K step, byte offsets < 4 GiB
+  Plan pl{Kern::V3, false, false, dmy_conv_fwd_partial_rows(M, gv.K)};
+  if (!DG && !ep.on) {
+    if (p1s_ok(gv, x, w, y) && gv.K >= 2 * gv.C) return pl.k = Kern::P1S, pl;  // output-heavy 1x1: streaming GEMM
+    if (stem_s_ok(gv, x, w, y)) return pl.k = Kern::STEM, pl;  // the 16-channel 3x3 stem view (p1s, G3 gather)
+  }
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
-  const bool buf = conv_buf_mode() && gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
-  const unsigned xbytes = buf ? (unsigned)xb : 0u, wbytes = buf ? (unsigned)wb : 0u;
-#define V3_GO(BM, BN, NS, P1_, BUF_)                                                                          \
-  v3::conv_fwd_v3<BM, BN, NS, P1_, DG, BUF_><<<grid, BM * BN / 64, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, \
-                                                                          wbytes, v3::S2Cls{0, 0, 0, 0}, ep, bb)
-#define V3_LAUNCH(BM, BN, NS)                                \
-  {                                                          \
-    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN); \
-    const unsigned grid = (unsigned)gm * gn;                 \
-    if (buf && conv_buf_mode() == 2) {                       \
-      if (p1) V3_GO(BM, BN, NS, true, 2);                    \
-      else V3_GO(BM, BN, NS, false, 2);                      \
-    } else if (buf) {                                        \
-      if (p1) V3_GO(BM, BN, NS, true, 1);                    \
-      else V3_GO(BM, BN, NS, false, 1);                      \
-    } else {                                                 \
-      if (p1) V3_GO(BM, BN, NS, true, 0);                    \
-      else V3_GO(BM, BN, NS, false, 0);                      \
-    }                                                        \
-  }
-  if (p1 && buf && p1p_mode() && tov < 0 && bb.z == nullptr && (!ep.on || p1p_eval())) {  // persistent 1x1
-    const int r = launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes, ep);
-    if (r >= 0) return r;
-  }
-  if (p1 && buf && p1_persist_mode() && tov < 0) {  // persistent 1x1 GEMM (v3::conv_p1_persist)
-    const int NC = num_cus();
-    if (gv.K > 64) {
-      const int gm = ceil_div(M, 128), gn = ceil_div(gv.K, 128);
-      const unsigned grid = (unsigned)min(gm * gn, NC);
-      v3::conv_p1_persist<128, 128, DG><<<grid, 256, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
-    } else {
-      const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 64);
-      const unsigned grid = (unsigned)min(gm * gn, NC);
-      v3::conv_p1_persist<256, 64, DG><<<grid, 256, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
+  pl.buf = gv.C % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
+  if (p1 && pl.buf && !ep.on && p1p_plan<DG>(gv, acc, ep, [](auto, auto, auto, auto) { return 0; }) >= 0) {
+    pl.k = Kern::P1P;  // persistent 1x1 with the register epilogue
+    if (!DG) {
+      const long r = p1p_lane_rows(gv);
+      if (r > 0) pl.lane = true, pl.rows = r;
     }
-    return (int)hipGetLastError();
+    return pl;
   }
-#define W_GO(BM, BN)                                                                                               \
-  {                                                                                                                \
-    static const int ff = env_int("DMY_WIDE_FF", 1);                                                               \
-    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                       \
+  if (pl.buf && gv.K >= kWideMinCols && (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus())
+    return pl.k = p1 ? Kern::PIPE8 : Kern::WIDE, pl;  // 1x1 views: the half-tile pipeline (conv_fwd_8p)
+  if (pl.buf && !p1 && gv.K > 64 && gv.K <= 128 && (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
+    return pl.k = Kern::TALL, pl;
+  return pl;
+}
+template <bool DG>
+int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc, const Geom& gv,
+              hipStream_t st, const Epi& ep, const Plan& pl) {
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
+  const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps), wb = 2.0 * gv.K * gv.KH * gv.KW * gv.C;
+  const unsigned xbytes = pl.buf ? (unsigned)xb : 0u, wbytes = pl.buf ? (unsigned)wb : 0u;
+#define W_GO(BM, BN)                                                                                                 \
+  {                                                                                                                  \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                         \
     if (p1) v3::conv_fwd_w<BM, BN, true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, \
-                                                                              xbytes, wbytes, ep, bb, ff);        \
+                                                                              xbytes, wbytes, ep);                  \
     else v3::conv_fwd_w<BM, BN, false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn,   \
-                                                                               xbytes, wbytes, ep, bb, ff);       \
-    return (int)hipGetLastError();                                                                                 \
+                                                                               xbytes, wbytes, ep);                 \
+    return (int)hipGetLastError();                                                                                   \
   }
-  if (tov < 0 && buf && wide_min_cols() > 0 && gv.K >= wide_min_cols() && gv.K > 64 &&
-      (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
-    if ((w8p_mode() == 2 || (w8p_mode() == 1 && p1)) && bb.z == nullptr) {  // the half-tile pipeline (conv_fwd_8p)
+#define V3_GO(BM, BN, NS, BUF_)                                                                               \
+  {                                                                                                           \
+    const int gm = ceil_div(M, BM), gn = ceil_div(gv.K, BN);                                                  \
+    if (p1)                                                                                                   \
+      v3::conv_fwd_v3<BM, BN, NS, true, DG, BUF_><<<(unsigned)gm * gn, BM * BN / 64, 0, st>>>(                \
+          x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, v3::S2Cls{0, 0, 0, 0}, ep);                    \
+    else                                                                                                      \
+      v3::conv_fwd_v3<BM, BN, NS, false, DG, BUF_><<<(unsigned)gm * gn, BM * BN / 64, 0, st>>>(               \
+          x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, v3::S2Cls{0, 0, 0, 0}, ep);                    \
+    return (int)hipGetLastError();                                                                            \
+  }
+  switch (pl.k) {
+    case Kern::P1S: return launch_p1s(x, w, b, y, ps, pq, acc, gv, st);
+    case Kern::STEM:
+      return stem_nth(gv.K) == 512 ? launch_p1s_kd<160, 512, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1)
+                                   : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+    case Kern::P1P: return launch_p1p<DG>(x, w, b, y, ps, pq, acc, gv, st, xbytes, wbytes, ep, pl.lane);
+    case Kern::PIPE8: {
       const int gm = ceil_div(M, 256), gn = ceil_div(gv.K, 256);
-      if (p1) v3::conv_fwd_8p<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
-                                                                         wbytes, ep, bb);
-      else v3::conv_fwd_8p<false, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes,
-                                                                          wbytes, ep, bb);
+      v3::conv_fwd_8p<true, DG><<<(unsigned)gm * gn, 512, 0, st>>>(x, w, b, y, ps, pq, acc, gv, gm, gn, xbytes, wbytes, ep);
       return (int)hipGetLastError();
     }
-    W_GO(256, 256)
+    case Kern::WIDE: W_GO(256, 256)
+    case Kern::TALL: W_GO(512, 128)
+    default: break;
   }
-  if (tov < 0 && buf && tall_mode() && !p1 && gv.K > 64 && gv.K <= 128 &&
-      (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
-    W_GO(512, 128)
+  if (gv.K > 64) {
+    if (pl.buf) V3_GO(256, 128, 3, 1)
+    V3_GO(256, 128, 3, 0)
+  }
+  if (pl.buf) V3_GO(256, 64, 2, 1)
+  V3_GO(256, 64, 2, 0)
 #undef W_GO
-  const int pt = tov >= 0 ? tov : p1 ? p1_tile_mode() : 0;
-  if (gv.K > 64 && pt == 1) V3_LAUNCH(128, 128, 2)
-  else if (gv.K > 64 && pt == 2) V3_LAUNCH(128, 128, 3)
-  else if (gv.K > 64 && pt == 3) V3_LAUNCH(256, 64, 2)
-  else if (gv.K > 64 && pt == 4) V3_LAUNCH(128, 64, 3)
-  else if (gv.K > 64) V3_LAUNCH(256, 128, 3)
-  else V3_LAUNCH(256, 64, 2)
-#undef V3_LAUNCH
 #undef V3_GO
-  return (int)hipGetLastError();
 }
 
 // sum the split slabs in order, + bias, round to bf16, inference epilogue (or plain store)
@@ -4450,18 +3680,16 @@ __global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict
 // and the buffer loader applies; 0 = not split
 inline int splitk_plan(const Geom& g, const void* x, const void* w, const void* y, int& gm, int& gn, int& per) {
   const long M = (long)g.N * g.OH * g.OW;
-  static const long maxm = env_int("DMY_SPLITK_MAXM", 16384);
-  if (M >= maxm || M == 0 || g.C % 64 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || g.K < 32 ||
-      !aligned16(x) || !aligned16(w) || !aligned16(y) || !conv_buf_mode())
+  if (M >= 16384 || M == 0 || g.C % 64 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || g.K < 32 ||
+      !aligned16(x) || !aligned16(w) || !aligned16(y))
     return 0;
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
   if (xb >= (double)v3::kBufOob || wb >= (double)v3::kBufOob) return 0;
-  // tuning knobs (detect-path A/B, profiles/r02/det_splitk.log): DMY_SPLITK_PCT = target blocks in % of the CU count,
-  // DMY_SPLITK_P1 = 1 splits the 1x1 layers too (default 0: their fp32 slabs + the reduce pass cost more than the split
-  // gains; bs1 detect DMA-1536 6.68 -> 6.45 ms, yolov5s 1.035 -> 0.968 ms), DMY_SPLITK_MINK = fewest K steps per split
-  static const int pct = env_int("DMY_SPLITK_PCT", 200), sp1 = env_int("DMY_SPLITK_P1", 0),
-                   mink = env_int("DMY_SPLITK_MINK", 2);
-  if (!sp1 && g.KH == 1 && g.KW == 1) return 0;
+  // detect-path A/B (profiles/r02/det_splitk.log): target 2 blocks per CU, at least 2 K steps per split; 1x1 layers
+  // stay unsplit (their fp32 slabs + the reduce pass cost more than the split gains; bs1 detect DMA-1536 6.68 -> 6.45
+  // ms, yolov5s 1.035 -> 0.968 ms)
+  constexpr int pct = 200, mink = 2;
+  if (g.KH == 1 && g.KW == 1) return 0;
   const int BN = g.K > 64 ? 128 : 64;
   gm = (int)ceil_div(M, 128);
   gn = ceil_div(g.K, BN);
@@ -4487,127 +3715,48 @@ inline int launch_splitk(const bf16* x, const bf16* w, const float* b, bf16* y, 
   const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * g.KH * g.KW * g.C);
   const bool p1 = g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0;
   const dim3 grid((unsigned)gm * gn, (unsigned)sp);
-  // DMY_SPLITK_FUSED = 1: the in-launch combine (conv_fwd_split's last-ticket reducer), 0 (default): splitk_epi_kernel.
-  // Measured SLOWER on the bs1 detect (profiles/r03/det_splitk_fused_ab.log: DMA-1536 4.52 -> 5.19 ms, yolov5s 0.79 ->
-  // 1.17 ms): 256 KB of slabs per tile read serially by one reducer block + a release per block
-  static const int fz = env_int("DMY_SPLITK_FUSED", 0);
-  // the tickets are one device array: the stream of the first fused launch owns them, any other stream takes the
-  // two-launch path (two streams' fused launches would share counters).  Ownership is a separate claimed
-  // flag, not a null-pointer sentinel: torch's default stream IS the null stream
-  bool mine = false;
-  if (fz) {
-    static std::mutex mu;
-    static bool claimed = false;
-    static hipStream_t owner = nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!claimed) {
-      claimed = true;
-      owner = st;
-    }
-    mine = owner == st;
-  }
-  const int fused = mine && gm * gn <= v3::kSplitCnt ? 1 : 0;
   if (g.K > 64) {
-    if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
-    else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
+    if (p1) v3::conv_fwd_split<128, 128, 2, true><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    else v3::conv_fwd_split<128, 128, 2, false><<<grid, 256, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
   } else {
-    if (p1) v3::conv_fwd_split<128, 64, 2, true><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
-    else v3::conv_fwd_split<128, 64, 2, false><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb, fused, b, y, ep);
+    if (p1) v3::conv_fwd_split<128, 64, 2, true><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
+    else v3::conv_fwd_split<128, 64, 2, false><<<grid, 128, 0, st>>>(x, w, ws, g, gm, gn, per, xb, wb);
   }
-  if (!fused)
-    splitk_epi_kernel<<<grid_cap(ceil_div(M * (g.K / 8), 256), 4096), 256, 0, st>>>(ws, sp, M, g.K, b, y, g.yps, ep);
+  splitk_epi_kernel<<<grid_cap(ceil_div(M * (g.K / 8), 256), 4096), 256, 0, st>>>(ws, sp, M, g.K, b, y, g.yps, ep);
   return (int)hipGetLastError();
 }
 
-// small-grid tile of a forward without BN partials (eval / batch-1 inference): when the 256 x 128 tile grid leaves
-// CUs idle, run the LDS-DMA kernel on 128 x 128 (p1_tile_mode 2) or 128 x 64 (mode 4) tiles, also for M < 16384
-// (otherwise the v2 tiles).  DMY_V3_FILL = 1 on, 0 (default) off: measured SLOWER on the bs1 detect path (DMA-1536
-// conv time 5.54 -> 5.87 ms per forward, yolov5s p50 0.94 -> 1.11 ms; profiles/r02/ab_fill.log) -- twice the blocks
-// do not shorten a latency-bound 1-4 K-step tile.  Returns the tile mode or -1
-inline int fill_tile(const Geom& g, const void* x, const void* w, const void* y, const float* ps, const Epi& ep) {
-  static const int on = env_int("DMY_V3_FILL", 0);
+// the bf16 forward's plan: bn = the launch writes BN partials (training); ws_elems = the split-K workspace it has
+Plan plan_fwd(const Geom& g, const void* x, const void* w, const float* b, const void* y, bool bn, const Epi& ep,
+              long ws_elems) {
   const long M = (long)g.N * g.OH * g.OW;
-  if (!on || ps != nullptr || g.K <= 64 || M < 1024 || g.C % 64 != 0 || !conv_buf_mode()) return -1;
-  if (g.C % 8 != 0 || g.xps % 8 != 0 || g.K % 8 != 0 || g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) ||
-      !aligned16(y) || (ep.res && (ep.rps % 8 != 0 || !aligned16(ep.res))))
-    return -1;
-  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
-  if (xb >= (double)v3::kBufOob || wb >= (double)v3::kBufOob) return -1;
-  const long NC = num_cus();
-  if (ceil_div(M, 256) * ceil_div(g.K, 128) >= NC) return -1;
-  return ceil_div(M, 128) * ceil_div(g.K, 128) >= NC ? 2 : 4;
-}
-
-// small-M inference GEMM (v3::conv_sk): DMY_SK = 0 (default) off, 1 eval forwards without BN partials with M <= DMY_SK_MAXM
-// (measured SLOWER on the batch-1 detect path, graph-replayed p50 over two same-box rounds, profiles/r03/det_sk_ab.log:
-// DMA-1536 6.69 / 6.43 ms off vs 7.88 / 8.27 on, yolov5s@640 0.95 / 1.12 off vs 1.12 / 1.13 on)
-// output pixels (batch-1 detect), channel counts multiples of 32
-inline int sk_mode() {
-  static const int t = env_int("DMY_SK", 0);
-  return t;
-}
-inline bool sk_ok(const Geom& g, const void* x, const void* w, const void* y, const float* ps, const Epi& ep) {
-  static const long maxm = env_int("DMY_SK_MAXM", 65536);
-  const long M = (long)g.N * g.OH * g.OW;
-  if (!sk_mode() || ps != nullptr || M == 0 || M > maxm || g.C % 32 != 0 || g.K % 32 != 0 || g.xps % 8 != 0 ||
-      g.yps % 8 != 0 || !aligned16(x) || !aligned16(w) || !aligned16(y) || (ep.res && (ep.rps % 8 != 0 || !aligned16(ep.res))))
-    return false;
-  const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.KH * g.KW * g.C;
-  return xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
-}
-inline int launch_sk(const bf16* x, const bf16* w, const float* b, bf16* y, const Geom& g, hipStream_t st, const Epi& ep) {
-  const long M = (long)g.N * g.OH * g.OW;
-  const int Ktot = g.KH * g.KW * g.C, gm = (int)ceil_div(M, 64);
-  const unsigned xb = (unsigned)(2.0 * ((double)g.N * g.H * g.W * g.xps)), wb = (unsigned)(2.0 * g.K * Ktot);
-#define SK_GO(BN_, KC_)                                                                                            \
-  {                                                                                                                \
-    const int gn = ceil_div(g.K, BN_);                                                                             \
-    v3::conv_sk<BN_, KC_><<<(unsigned)gm * gn, 256, 0, st>>>(x, w, b, y, g, ep, gm, gn, xb, wb);                   \
-    return (int)hipGetLastError();                                                                                 \
+  const bool res_ok = !ep.res || (ep.rps % 8 == 0 && aligned16(ep.res));
+  if (b == nullptr && halo_ok(g, x, w, y) && (!ep.on || !bn) && halo_rows(g) <= prow_persist_cap() &&
+      (!ep.on || ep.res == nullptr ||
+       (res_ok && 2.0 * ((double)g.N * g.OH * g.OW * ep.rps) < (double)v3::kBufOob)))
+    return Plan{Kern::HALO, true, false, halo_rows(g)};  // one BN partial row per wave
+  if (ws_elems > 0 && !bn && res_ok) {
+    const long need = splitk_elems(g, x, w, y);
+    if (need > 0 && need <= ws_elems) return Plan{Kern::SPLITK, true, false, 0};
   }
-  if (g.K >= 128) {
-    if (Ktot <= 128) SK_GO(128, 128)
-    SK_GO(128, 256)
-  }
-  if (Ktot <= 128) SK_GO(64, 128)
-  SK_GO(64, 256)
-#undef SK_GO
+  if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && res_ok) return plan_v3<false>(g, x, w, y, 0, ep);
+  return Plan{Kern::V2, false, false, dmy_conv_fwd_partial_rows(M, g.K)};
 }
 
 template <typename T>
 int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps, float* pq, const Geom& g, hipStream_t st,
                const Epi& ep = Epi{}, float* ws = nullptr, long ws_elems = 0) {
   const long M = (long)g.N * g.OH * g.OW;
-  if (ps != nullptr) t_prow_last = dmy_conv_fwd_partial_rows(M, g.K);
+  Plan pl{Kern::V2, false, false, dmy_conv_fwd_partial_rows(M, g.K)};
+  if constexpr (sizeof(T) == 2) pl = plan_fwd(g, x, w, b, y, ps != nullptr, ep, ws != nullptr ? ws_elems : 0);
+  if (ps != nullptr) t_prow_last = pl.rows;
   if constexpr (sizeof(T) == 2) {
-    if (b == nullptr && halo_ok(g, x, w, y) && (!ep.on || ps == nullptr) && halo_rows(g) <= prow_persist_cap() &&
-        (!ep.on || ep.res == nullptr ||
-         (ep.rps % 8 == 0 && aligned16(ep.res) && 2.0 * ((double)g.N * g.OH * g.OW * ep.rps) < (double)v3::kBufOob)))
-    {
-      if (ps != nullptr) t_prow_last = halo_rows(g);
-      return launch_halo<false>((const bf16*)x, (const bf16*)w, (bf16*)y, ps, pq, g, st, 0, ep);
+    switch (pl.k) {
+      case Kern::HALO: return launch_halo<false>((const bf16*)x, (const bf16*)w, (bf16*)y, ps, pq, g, st, 0, ep);
+      case Kern::SPLITK: return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);
+      case Kern::V2: break;
+      default: return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep, pl);
     }
-    if (conv_buf_mode() && sk_ok(g, x, w, y, ps, ep))
-      return launch_sk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, st, ep);
-    // small-M 1x1 layers (batch-1 inference: M < 65536): the register-epilogue GEMM on one-wave 64 x 64 tiles
-    if (M < 65536 && M >= 64 && p1p_small() && g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0 && g.C % 64 == 0 &&
-        g.xps % 8 == 0 && g.yps % 8 == 0 && g.K % 8 == 0 && g.K >= 32 && aligned16(x) && aligned16(w) &&
-        aligned16(y) && conv_buf_mode()) {
-      const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), wb = 2.0 * g.K * g.C;
-      if (xb < (double)v3::kBufOob && wb < (double)v3::kBufOob) {
-        const int r = launch_p1p<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, (unsigned)xb,
-                                        (unsigned)wb, ep, true);
-        if (r >= 0) return r;
-      }
-    }
-    if (ws != nullptr && ps == nullptr && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res)))) {
-      const long need = splitk_elems(g, x, w, y);
-      if (need > 0 && need <= ws_elems) return launch_splitk((const bf16*)x, (const bf16*)w, b, (bf16*)y, g, ws, st, ep);
-    }
-    const int tov = fill_tile(g, x, w, y, ps, ep);
-    if (tov >= 0) return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep, v3::BnB{}, tov);
-    if (v3_ok(g.C, g.xps, g.K, g.yps, x, w, y, M) && (!ep.res || (ep.rps % 8 == 0 && aligned16(ep.res))))
-      return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep);
   }
   if (big_tile(M, g.K))
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
@@ -4616,58 +3765,23 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
 // stride-2 data-grad on the v3 buffer loader: one launch per output-parity class (a, b), each a GEMM
 // over the class's input pixels and only the taps of matching parity (FwdLdsB S2 mode)
 inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const void* dx) {
-  if (g.S != 2 || !conv_buf_mode() || g.K % 64 != 0 || g.KH < 2 || g.KW < 2) return false;
+  if (g.S != 2 || g.K % 64 != 0 || g.KH < 2 || g.KW < 2) return false;
   const long Mmin = (long)g.N * (g.H / 2) * (g.W / 2);
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
 }
-// DMY_S2P: 1 the stride-2 data-grads run the persistent class kernel (v3::conv_s2p), 0 (default) the one-tile kernels.
-// Built, parity-green (tests/test_gpu_conv*.py: 269 passed with it on) and measured SLOWER on every DMA-1536 shape
-// (gpurun_out/r5/ab_s2p.log, cold caches, two passes): 64 -> 128 @768^2 bs32 1997 -> 2511 us, 128 -> 256 @384^2
-// 1289 -> 1483, 256 -> 512 @192^2 947 -> 1320, 512 -> 1024 @96^2 857 -> 1244.  Its register epilogue writes each dx
-// pixel's 128-B line as two 64-B halves one instruction apart (every second pixel of a row, the class stride), the
-// store order round 4 measured at 3.3-4.1 TB/s against 5.6-5.9 for whole lines, and the persistent grid keeps one
-// 8-wave block per CU where the one-tile kernels overlap several
-inline int s2p_mode() {
-  static const int t = env_int("DMY_S2P", 0);
-  return t;
-}
 inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc, const Geom& g, hipStream_t st) {
   const unsigned xbytes = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned wbytes = (unsigned)(2.0 * g.C * g.KH * g.KW * g.K);
-  const double dxb = 2.0 * ((double)g.N * g.H * g.W * g.xps);
-  if (s2p_mode() && g.C % 64 == 0 && g.xps % 8 == 0 && dxb < (double)v3::kBufOob && aligned16(dx)) {
+  // one launch for the four classes of <= 64-channel data-grads, one per class above.  Measured
+  // (profiles/r02/ab_s2_merge.log): +4..14 % at 32 / 64 channels, 16-33 % slower on the 1-block-per-CU 256 x 128 tiles
+  // of the 128 / 256-channel layers, where the per-class launches stay.  The persistent class kernel (conv_s2p, round 5)
+  // was slower on every DMA-1536 shape (gpurun_out/r5/ab_s2p.log) and is gone.
+  if (g.C <= 64) {
     const long Mmax = (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2);  // class (0, 0) has the most rows
-    const int gmax = ceil_div(Mmax, 256);
-    if (g.C > 64) {
-      using PP = v3::P1P<256, 128, 3, 64>;
-      const int gn = ceil_div(g.C, 128), G = p1p_grid(4 * gmax * gn, 3 * PP::C3_::STAGE);
-      v3::conv_s2p<256, 128, 3, 64><<<(unsigned)G, PP::NTH, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes, wbytes,
-                                                                   (unsigned)dxb);
-    } else {
-      using PP = v3::P1P<256, 64, 2, 64>;
-      const int gn = 1, G = p1p_grid(4 * gmax * gn, 2 * PP::C3_::STAGE);
-      v3::conv_s2p<256, 64, 2, 64><<<(unsigned)G, PP::NTH, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes, wbytes,
-                                                                  (unsigned)dxb);
-    }
-    return (int)hipGetLastError();
-  }
-  // DMY_S2_MERGE: 0 one launch per parity class, 1 (default) one launch for <= 64-channel data-grads, 2 always.
-  // Measured (profiles/r02/ab_s2_merge.log): +4..14 % at 32 / 64 channels, 16-33 % slower on the 1-block-per-CU
-  // 256 x 128 tiles of the 128 / 256-channel layers, where the per-class launches stay.
-  static const int merged = env_int("DMY_S2_MERGE", 1);
-  if (merged == 2 || (merged == 1 && g.C <= 64)) {
-    const long Mmax = (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2);  // class (0, 0) has the most rows
-    const int gmax = ceil_div(Mmax, 256);
-    if (g.C > 64) {
-      const int gn = ceil_div(g.C, 128);
-      v3::conv_dgrad_s2_v3<256, 128, 3><<<(unsigned)(4 * gmax * gn), 512, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes,
-                                                                                 wbytes);
-    } else {
-      const int gn = ceil_div(g.C, 64);
-      v3::conv_dgrad_s2_v3<256, 64, 2><<<(unsigned)(4 * gmax * gn), 256, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes,
-                                                                                wbytes);
-    }
+    const int gmax = ceil_div(Mmax, 256), gn = ceil_div(g.C, 64);
+    v3::conv_dgrad_s2_v3<256, 64, 2><<<(unsigned)(4 * gmax * gn), 256, 0, st>>>(dy, wt, dx, acc, g, gmax, gn, xbytes,
+                                                                              wbytes);
     return (int)hipGetLastError();
   }
   for (int a = 0; a < 2; ++a)
@@ -4681,39 +3795,18 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
       if (g.C > 64) {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
         v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{}, v3::BnB{});
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
       } else {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 64);
         v3::conv_fwd_v3<256, 64, 2, false, true, 3><<<(unsigned)gm * gn, 256, 0, st>>>(
-            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{}, v3::BnB{});
+            dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
       }
     }
   return (int)hipGetLastError();
 }
 
-// partial rows of the fused producer-BN reduce (v3::BnB) when the bf16 data-grad of this geometry runs on a stride-1
-// v3 256 x 128 / wide 256 x 256 kernel (>= 128-column tiles), else 0 (then the data-grad cannot fuse them)
-inline long dgrad_bn_rows(const Geom& g, const void* dy, const void* wt, const void* dx) {
-  const long M = (long)g.N * g.H * g.W;
-  if (dgrad_s2_v3_ok(g, dy, wt, dx) || g.S != 1 || g.OH != g.H + 2 * g.P - g.KH + 1 ||
-      g.OW != g.W + 2 * g.P - g.KW + 1 || !v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M) || g.C <= 64)
-    return 0;
-  const bool p1 = g.KH == 1 && g.KW == 1 && g.P == 0;
-  const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
-  const bool buf = conv_buf_mode() && g.K % 64 == 0 && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
-  if (p1 && buf && p1_persist_mode()) return 0;
-  if (p1 && (p1s_mode() == 2 || (p1s_mode() == 3 && g.C >= 2 * g.K)) &&
-      p1s_ok(make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, 1, 1, 1, 0, g.H, g.W, g.xps), dy, wt, dx))
-    return 0;
-  if (p1 && p1_tile_mode() != 0) return 0;  // 128-row / 64-column tiles
-  if (buf && tall_mode() && !p1 && g.C <= 128 && (long)ceil_div(M, 512) * ceil_div(g.C, 128) >= 4L * num_cus())
-    return 0;  // the 512 x 128 tile (launch_v3) does not fuse them
-  return ceil_div(M, 256);  // one partial row per 256-row tile (v3 256 x 128 and wide 256 x 256)
-}
-
 template <typename T>
-int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st,
-                 const v3::BnB& bb = v3::BnB{}) {
+int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& g, hipStream_t st) {
   const long M = (long)g.N * g.H * g.W / (g.S == 2 ? 4 : 1);
   if constexpr (sizeof(T) == 2) {
     if (dgrad_s2_v3_ok(g, dy, wt, dx))
@@ -4722,21 +3815,14 @@ int conv_dgrad_t(const void* dy, const void* wt, void* dx, int acc, const Geom& 
         v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, M)) {
       // GEMM view: rows = input pixels (N, H, W), columns = C, gather dy (OH x OW x K, stride yps)
       Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 1, g.P, g.H, g.W, g.xps);
-      if (bb.z == nullptr && halo_ok(gv, dy, wt, dx))
+      if (halo_ok(gv, dy, wt, dx))
         return launch_halo<true>((const bf16*)dy, (const bf16*)wt, (bf16*)dx, nullptr, nullptr, gv, st, acc);
       return launch_v3<true>((const bf16*)dy, (const bf16*)wt, nullptr, (bf16*)dx, nullptr, nullptr, acc, gv, st,
-                             Epi{}, bb);
+                             Epi{}, plan_v3<true>(gv, dy, wt, dx, acc, Epi{}));
     }
   }
   if (big_tile(M, g.C)) return launch_dgrad<T, 128, 128>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
   return launch_dgrad<T, 64, 64>((const T*)dy, (const T*)wt, (T*)dx, acc, g, st);
-}
-inline int wgrad_target() {
-  static int t = [] {
-    const char* e = getenv("DMY_WGRAD_TARGET");
-    return e ? atoi(e) : 0;
-  }();
-  return t;
 }
 inline int num_cus() {
   static int n = [] {
@@ -4754,16 +3840,13 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, Geom g, hip
   const int gm = ceil_div(g.K, 128), gn = ceil_div(Ntot, 128);
   const int nk = ceil_div(NP, 64);
   // split-K over pixels.  Cost model (calibrated on MI355X): resident blocks R = 2 per CU; time ~
-  // rounds(tiles*s / R) * (K steps per split) * 1.9 us + tiles*s * 64 KiB of fp32 atomics at 1.3 TB/s.
-  // DMY_WGRAD_TARGET=<blocks> replaces the model by a fixed block-count target (tuning).
+  // rounds(tiles*s / R) * (K steps per split) * 1.9 us + tiles*s * 64 KiB of fp32 atomics at 1.3 TB/s.  It beat fixed
+  // 512 / 768-block targets on DMA-1536 (152.15 vs 150.76 / 147.91 img/s, profiles/r04/wgrad_target_ab.log)
   const int tiles = gm * gn;
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
   int splits = 1;
-  if (wgrad_target() > 0) {
-    splits = (wgrad_target() + tiles / 2) / tiles;
-    if (splits < 1) splits = 1;
-  } else {
+  {
     const double R = 2.0 * num_cus();
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
@@ -4779,16 +3862,8 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, Geom g, hip
   if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
-  const bool buf = conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
-  static const int ns3 = [] {
-    const char* e = getenv("DMY_WGRAD_NS");
-    return e ? atoi(e) == 3 : 0;
-  }();
-  if (buf && ns3)
-    v3::conv_wgrad_v3<3, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
-  else if (buf && conv_buf_mode() == 2)
-    v3::conv_wgrad_v3<2, 2><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
-  else if (buf)
+  const bool buf = xb < (double)v3::kBufOob && db < (double)v3::kBufOob;
+  if (buf)
     v3::conv_wgrad_v3<2, 1><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   else
     v3::conv_wgrad_v3<2, 0><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
@@ -4796,16 +3871,9 @@ inline int launch_wgrad_v3(const bf16* x, const bf16* dy, float* dw, Geom g, hip
   return (int)hipGetLastError();
 }
 
-// wgrad v4 tiles (0 = off): 1 = 128 x 256, 2 = 256 x 128, 3 = auto (default): 256 x 128 when K_out >= 256,
-// else the v3 128 x 128 kernel (tools/gpu/ab_conv.sh, profiles/r01/ab_wgrad_v4.log: +7-11 % at K_out >= 256,
-// the 256-row tile is half idle and the 128 x 256 one no faster at K_out = 128)
-inline int wgrad_v4_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_WGRAD_V4");
-    return e ? atoi(e) : 3;
-  }();
-  return t;
-}
+// wgrad v4 tile 256 x 128 for K_out >= 256, else the v3 128 x 128 kernel (tools/gpu/ab_conv.sh,
+// profiles/r01/ab_wgrad_v4.log: +7-11 % at K_out >= 256, the 256-row tile is half idle and a 128 x 256 one no faster at
+// K_out = 128)
 template <int BM, int BN>
 int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const long NP = (long)g.N * g.OH * g.OW;
@@ -4816,12 +3884,8 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
   int splits = 1;
-  if (wgrad_target() > 0) {
-    splits = (wgrad_target() + tiles / 2) / tiles;
-    if (splits < 1) splits = 1;
-  } else {
-    // launch_wgrad_v3's model with one resident block per CU, twice the tile per K step and atomics (the wide
-    // 256 x 256 tile: twice that again, per K step and per epilogue)
+  {
+    // launch_wgrad_v3's model with one resident block per CU, twice the tile per K step and atomics
     const double R = num_cus(), sc = (double)BM * BN / (256.0 * 128.0);
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
@@ -4837,62 +3901,30 @@ int launch_wgrad_v4(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_
   if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
-  if constexpr (BM == 256 && BN == 256)
-    v3::conv_wgrad_w<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
-  else
-    v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
+  v3::conv_wgrad_v4<BM, BN><<<grid, 512, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
-// the wide 256 x 256 weight-grad tile (v3::conv_wgrad_w) for K_out >= 256 and >= 256 GEMM columns: DMY_WGRAD_W = 1 on,
-// 0 (default) off.  Measured SLOWER than the 256 x 128 tile on every DMA-1536 1x1 weight-grad it takes (round 4,
-// profiles/r04/wgrad_wide_ab.log, cold-cache us: C1024->K256 96^2 284 vs 240, C256->K256 163 vs 133, C2048->K1024 48^2
-// 426 vs 385, C256->K1024 278 vs 231): a 2-stage ring of 64 KiB stages keeps one K step in flight where the
-// 3-stage ring of the 256 x 128 tile keeps two, and the halved tile count needs twice the splits to fill 256 CUs
-inline int wgrad_w_mode() {
-  static int t = env_int("DMY_WGRAD_W", 0);
-  return t;
-}
-
-// tap-fused 3x3 s1 weight-grad (v3::conv_wgrad_tap): 0 = off, 1 = on (default) where it applies
-inline int wgrad_tap_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_WGRAD_TAP");
-    return e ? atoi(e) : 1;
-  }();
-  return t;
-}
+// tap-fused 3x3 s1 weight-grad (v3::conv_wgrad_tap) where it applies
 inline bool wgrad_tap_ok(const Geom& g, const void* x, const void* dy) {
-  if (!wgrad_tap_mode() || g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.OH != g.H || g.OW != g.W) return false;
+  if (g.KH != 3 || g.KW != 3 || g.S != 1 || g.P != 1 || g.OH != g.H || g.OW != g.W) return false;
   if (g.C % 16 != 0 || g.xps % 8 != 0 || g.yps % 8 != 0 || g.K % 8 != 0 || !aligned16(x) || !aligned16(dy)) return false;
-  // C % 32 == 16 (the space-to-depth stem, 16 channels): DMY_WGRAD_TAP16 = 0 keeps it on the v3n column tiles
-  static const int t16 = env_int("DMY_WGRAD_TAP16", 1);
-  if (g.C % 32 != 0 && !t16) return false;
+  // C % 32 == 16 (the space-to-depth stem, 16 channels) included: the upper half of the halo plane loads zeros
+  // (yolov5s 3845 -> 3876 img/s against the v3n column tiles, profiles/r05/wgrad_tap16_ab.log)
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
   if (xb >= (double)v3::kBufOob || db >= (double)v3::kBufOob) return false;
   // enough (patch, tile) work units that the per-block fp32 atomics of the 288-column tile stay a small share
   // (tools/gpu/tune_conv.py: 20^2 / 40^2 / 80^2 yolov5s layers are faster on the v3 / v4 column tiles)
   const long units = (long)g.N * ceil_div(g.OH, 8) * ceil_div(g.OW, 8) * ceil_div(g.K, 128) * ceil_div(g.C, 32);
   // 10000: the yolov5s 64-channel @80^2 layers (12800 units) measured 96 -> 79 us on the tap kernel, the 256-channel
-  // @20^2 ones (9216) 70 -> 106 us (profiles/r02/ab_wgrad_v5s.log)
-  static const long min_units = env_int("DMY_WGRAD_TAP_UNITS", 10000);
-  return units >= min_units;
+  // @20^2 ones (9216) 70 -> 106 us (profiles/r02/ab_wgrad_v5s.log); lower thresholds were slower on yolov5s
+  // (profiles/r05/wgrad_tap_units_ab.log)
+  return units >= 10000;
 }
-// DMY_WGRAD_TAP_NP: 2 (default) the <= 64-output-channel layers with C % 64 == 0 run the two-plane tile, 1 the one-plane
-// tile (read per launch: the tests compare both in one process)
-inline int wgrad_tap_np(const Geom& g) {
-  const char* e = getenv("DMY_WGRAD_TAP_NP");
-  const int np = e ? atoi(e) : 2;
-  return (np == 2 && g.K <= 64 && g.C % 64 == 0) ? 2 : 1;
-}
-// DMY_WGRAD_TAP_NP128: 1 the > 64-output-channel layers with C % 64 == 0 run the two-plane 128-row tile (one block per
-// CU: 288 accumulator registers per lane), 0 (default) the one-plane tile.  Measured SLOWER: DMA-1536 158.25 ->
-// 154.9 img/s on one box (profiles/r05/wgrad_tap_np128_ab.log): one 4-wave block per CU hides too little latency
-inline int wgrad_tap_np128(const Geom& g) {
-  const char* e = getenv("DMY_WGRAD_TAP_NP128");
-  const int on = e ? atoi(e) : 0;
-  return (on == 1 && g.K > 64 && g.C % 64 == 0) ? 2 : 1;
-}
+// the <= 64-output-channel layers with C % 64 == 0 run the two-plane tile (a block owns 64 input channels: 13 fragment
+// reads per 36 MFMAs instead of 11 per 18; DMA-1536 158.4 -> 159.1 img/s, profiles/r05/wgrad_tap_np2_ab.log); the
+// same for the 128-row tile needs 288 accumulators, one block per CU, and measured 2 % slower
+// (profiles/r05/wgrad_tap_np128_ab.log)
 template <int BM, int NP = 1>
 int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream_t st) {
   const int gm = ceil_div(g.K, BM), gn = ceil_div(g.C, 32 * NP);
@@ -4901,14 +3933,11 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
   int splits = 1;
-  if (wgrad_target() > 0) {
-    splits = (wgrad_target() + tiles / 2) / tiles;
-    if (splits < 1) splits = 1;
-  } else {
+  {
     // two resident blocks per CU; ~1.1 us per patch step of the 128-row tile (288 MFMA per wave pair at ~45 %
     // of peak) and its 147 KiB fp32 tile of atomics per block at 1.3 TB/s (MI355X_MICROARCH.md §Global float
     // atomics); the 64-row tile halves both
-    const double R = ((BM == 128 && NP == 2) ? 1.0 : 2.0) * num_cus(), f = BM / 128.0 * NP;
+    const double R = 2.0 * num_cus(), f = BM / 128.0 * NP;
     double best = 1e300;
     for (int sp = 1; sp <= maxs; sp += (sp < 16 ? 1 : sp / 16)) {
       const double blocks = (double)tiles * sp;
@@ -4923,8 +3952,7 @@ int launch_wgrad_tap(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   if (wgrad_begin(g, splits)) return 0;
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * 9 * g.C, st);
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)g.N * g.OH * g.OW * g.yps);
-  static const int ff = env_int("DMY_TAP_FF", 0);
-  v3::conv_wgrad_tap<BM, NP><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db, ff);
+  v3::conv_wgrad_tap<BM, NP><<<grid, 256, 0, st>>>(x, dy, dw, per, g, gm, gn, nk, (unsigned)xb, (unsigned)db);
   wgrad_end(g, dw, splits, st);
   return (int)hipGetLastError();
 }
@@ -4940,10 +3968,7 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   int maxs = nk / 8;
   if (maxs < 1) maxs = 1;
   int splits = 1;
-  if (wgrad_target() > 0) {
-    splits = (wgrad_target() + tiles / 2) / tiles;
-    if (splits < 1) splits = 1;
-  } else {
+  {
     // same cost model as launch_wgrad_v3 with the tile's share of a 128 x 128 step and atomics
     const double R = 2.0 * num_cus() * (128.0 * 128.0) / (BM * BN) * 0.5;
     const double step = 1.9 * (BM * BN) / (128.0 * 128.0) + 0.25;
@@ -4962,7 +3987,7 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   if (!g.zeroed) (void)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)g.K * Ntot, st);
   constexpr int NS = 3 * v3::WgradLdsN<BM, BN>::STAGE <= 80 * 1024 ? 3 : 2;  // keep 2 blocks per CU
   const double xb = 2.0 * ((double)g.N * g.H * g.W * g.xps), db = 2.0 * ((double)NP * g.yps);
-  if (conv_buf_mode() && xb < (double)v3::kBufOob && db < (double)v3::kBufOob)
+  if (xb < (double)v3::kBufOob && db < (double)v3::kBufOob)
     v3::conv_wgrad_v3n<BM, BN, NS, true><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, (unsigned)xb, (unsigned)db);
   else
     v3::conv_wgrad_v3n<BM, BN, NS, false><<<grid, BN, 0, st>>>(x, dy, dw, per, g, gm, gn, 0u, 0u);
@@ -4970,22 +3995,10 @@ int launch_wgrad_v3n(const bf16* x, const bf16* dy, float* dw, Geom g, hipStream
   return (int)hipGetLastError();
 }
 
-// weight-grad of layers with <= 64 output channels: 0 = v2 register-staged 64 x 64 tiles, 1 = the
-// narrow LDS-DMA tiles (BM 32/64), 2 = the 128 x 128 LDS-DMA tile (half its rows idle at K = 64),
-// 3 = auto (default): narrow tiles past 8 M pixels at K = 64, the 128 tile otherwise (tools/gpu/ab_conv.sh:
-// 64 ch @768^2 x 32 narrow 483 / 128-tile 394 / v2 257 TFLOP/s; @384^2 280 / 384 / 261; yolov5s layers 128-tile best)
-inline int wgrad_narrow_mode() {
-  static int t = [] {
-    const char* e = getenv("DMY_WGRAD_NARROW");
-    return e ? atoi(e) : 3;
-  }();
-  return t;
-}
-inline int wgrad_narrow_for(const Geom& g, long NP) {
-  const int m = wgrad_narrow_mode();
-  if (m != 3) return m;
-  return (g.K == 64 && NP >= 8L * 1024 * 1024) ? 1 : 2;
-}
+// weight-grad of layers with <= 64 output channels: 1 = the narrow LDS-DMA tiles (BM 32/64) past 8 M pixels at
+// K = 64, 2 = the 128 x 128 LDS-DMA tile (half its rows idle at K = 64) otherwise (tools/gpu/ab_conv.sh: 64 ch @768^2
+// x 32 narrow 483 / 128-tile 394 / v2 257 TFLOP/s; @384^2 280 / 384 / 261; yolov5s layers 128-tile best)
+inline int wgrad_narrow_for(const Geom& g, long NP) { return (g.K == 64 && NP >= 8L * 1024 * 1024) ? 1 : 2; }
 
 template <typename T>
 int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStream_t st) {
@@ -4994,27 +4007,19 @@ int conv_wgrad_t(const void* x, const void* dy, float* dw, const Geom& g, hipStr
     const int Ntot = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0 && g.xps % 8 == 0 && g.K % 8 == 0 && g.yps % 8 == 0 && aligned16(x) && aligned16(dy);
     const int nm = wgrad_narrow_for(g, NP);
-    const int v4 = wgrad_v4_mode();
     const double xb4 = 2.0 * ((double)g.N * g.H * g.W * g.xps), db4 = 2.0 * ((double)NP * g.yps);
     if (wgrad_tap_ok(g, x, dy))
-      return g.K <= 64 ? (wgrad_tap_np(g) == 2 ? launch_wgrad_tap<64, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
-                                               : launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st))
-                       : (wgrad_tap_np128(g) == 2 ? launch_wgrad_tap<128, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
-                                                  : launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st));
-    if (vec && v4 && g.K > 64 && Ntot >= 128 && NP >= 16384 && conv_buf_mode() && xb4 < (double)v3::kBufOob &&
-        db4 < (double)v3::kBufOob) {
-      if (wgrad_w_mode() && g.K >= 256 && Ntot >= 256)
-        return launch_wgrad_v4<256, 256>((const bf16*)x, (const bf16*)dy, dw, g, st);
-      if (v4 == 2 || (v4 == 3 && g.K >= 256)) return launch_wgrad_v4<256, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
-      if (v4 == 1) return launch_wgrad_v4<128, 256>((const bf16*)x, (const bf16*)dy, dw, g, st);
-    }
+      return g.K > 64 ? launch_wgrad_tap<128>((const bf16*)x, (const bf16*)dy, dw, g, st)
+             : g.C % 64 == 0 ? launch_wgrad_tap<64, 2>((const bf16*)x, (const bf16*)dy, dw, g, st)
+                             : launch_wgrad_tap<64>((const bf16*)x, (const bf16*)dy, dw, g, st);
+    if (vec && g.K >= 256 && Ntot >= 128 && NP >= 16384 && xb4 < (double)v3::kBufOob && db4 < (double)v3::kBufOob)
+      return launch_wgrad_v4<256, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && (g.K > 64 || nm == 2) && Ntot >= 64 && NP >= 16384)
       return launch_wgrad_v3((const bf16*)x, (const bf16*)dy, dw, g, st);
     if (vec && g.K <= 64 && Ntot >= 128 && NP >= 16384 && nm == 1) {
       // one 256-column tile also for 128 < Ntot < 256 (the 144-column space-to-depth stem view: on 128-column tiles
-      // the second tile re-read every dy row for 16 columns of work): DMY_WGRAD_ONE_TILE = 0 keeps two tiles
-      static const int one = env_int("DMY_WGRAD_ONE_TILE", 1);
-      const bool wide = Ntot >= 512 || Ntot % 256 == 0 || (one && Ntot > 128 && Ntot < 256);
+      // the second tile re-read every dy row for 16 columns of work; profiles/r04/stem_wgrad_ab.log 1638 -> 1276 us)
+      const bool wide = Ntot >= 512 || Ntot % 256 == 0 || (Ntot > 128 && Ntot < 256);
       if (g.K <= 32) return wide ? launch_wgrad_v3n<32, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
                                  : launch_wgrad_v3n<32, 128>((const bf16*)x, (const bf16*)dy, dw, g, st);
       return wide ? launch_wgrad_v3n<64, 256>((const bf16*)x, (const bf16*)dy, dw, g, st)
@@ -5127,26 +4132,11 @@ DMY_API long dmy_conv_fwd_bound_rows(long M, int K) {
 DMY_API long dmy_conv_fwd_last_rows() { return t_prow_last; }
 
 DMY_API int dmy_conv_fwd_bn_rows(int dtype, const void* x, const void* w, const float* bias, const void* y,
-                                        int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P,
-                                        int OH, int OW, long yps) {
+                                 int N, int H, int W, int C, long xps, int K, int KH, int KW, int S, int P,
+                                 int OH, int OW, long yps) {
   const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  if (dtype && bias == nullptr && halo_ok(g, x, w, y) && halo_rows(g) <= prow_persist_cap())
-    return halo_rows(g);  // one row per wave (conv3_halo64)
-  if (dtype) {  // the training forward's route through conv_fwd_t / launch_v3 to a LANE conv_p1p: one row per wave
-    const long M = (long)N * OH * OW;
-    const bool p1 = KH == 1 && KW == 1 && S == 1 && P == 0;
-    const bool small = M < 65536 && M >= 64 && p1p_small() && p1 && C % 64 == 0 && xps % 8 == 0 && yps % 8 == 0 &&
-                       K % 8 == 0 && K >= 32 && aligned16(x) && aligned16(w) && aligned16(y) && conv_buf_mode() &&
-                       2.0 * ((double)N * H * W * xps) < (double)v3::kBufOob && 2.0 * K * C < (double)v3::kBufOob;
-    if (p1 && !small && v3_ok(C, xps, K, yps, x, w, y, M) &&
-        !(p1s_ok(g, x, w, y) && (p1s_mode() == 2 || K >= 2 * C)) && !stem_s_ok(g, x, w, y) && p1p_mode() &&
-        conv_buf_mode() && C % 64 == 0 && 2.0 * ((double)N * H * W * xps) < (double)v3::kBufOob &&
-        2.0 * K * C < (double)v3::kBufOob) {
-      const int r = p1p_lane_rows(g);
-      if (r > 0) return r;
-    }
-  }
-  return dmy_conv_fwd_partial_rows((long)N * OH * OW, K);
+  if (!dtype) return dmy_conv_fwd_partial_rows((long)N * OH * OW, K);
+  return (int)plan_fwd(g, x, w, bias, y, true, Epi{}, 0).rows;  // the training forward's own plan (conv_fwd_t)
 }
 
 DMY_API int dmy_conv_fwd(int dtype, const void* x, const void* w, const float* bias, void* y, float* psum, float* psq,
@@ -5224,27 +4214,6 @@ DMY_API int dmy_conv_fwd_fp8(const void* x8, const void* w8, const float* xamax,
   else F8_GO(256, 64, 2)
 #undef F8_GO
   return (int)hipGetLastError();
-}
-
-// Data-grad that also writes the backward-reduce partials of the BatchNorm (+ act) producing the conv's input:
-// dmy_conv_dgrad_bn_rows gives the partial rows (0: this geometry cannot fuse them -- call dmy_conv_dgrad and
-// dmy_bn_bwd_reduce instead); pdb / pdg [rows][C] then feed dmy_bn_bwd_finalize like dmy_bn_bwd_reduce's.
-DMY_API long dmy_conv_dgrad_bn_rows(int dtype, const void* dy, const void* wt, const void* dx, int N, int H, int W,
-                                    int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps) {
-  if (!dtype) return 0;
-  const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  return dgrad_bn_rows(g, dy, wt, dx);
-}
-
-DMY_API int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* wt, void* dx, int accumulate, int N, int H, int W,
-                              int C, long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps,
-                              const void* z, long zps, const float* scale, const float* shift, const float* mean,
-                              const float* invstd, int act, float* pdb, float* pdg, void* stream) {
-  const Geom g = make_geom(N, H, W, C, xps, K, KH, KW, S, P, OH, OW, yps);
-  if (!dtype || dgrad_bn_rows(g, dy, wt, dx) == 0 || zps % 8 != 0 || !aligned16(z)) return (int)hipErrorInvalidValue;
-  if ((long)N * H * W == 0 || C == 0) return 0;
-  const v3::BnB bb{(const bf16*)z, zps, scale, shift, mean, invstd, act, pdb, pdg};
-  return conv_dgrad_t<bf16>(dy, wt, dx, accumulate, g, (hipStream_t)stream, bb);
 }
 
 // Inference forward with a split-K workspace for small M (batch-1 detect): dmy_conv_fwd_act semantics; when

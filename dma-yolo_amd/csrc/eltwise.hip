@@ -1150,15 +1150,9 @@ __global__ void cast_kernel(const S* __restrict__ x, D* __restrict__ y, long n, 
     y[i] = from_f<D>(to_f(x[i]) * scale);
 }
 
-// grid of the grid-stride elementwise kernels: blocks of 256 threads, capped at DMY_ELT_GRID (default 16384: DMA-1536
-// step 157.61 / 157.98 -> 158.13 / 158.32 img/s against 8192, alternating on one box, profiles/r05/elt_grid_ab.log)
-inline int egrid(long n) {
-  static const int cap = [] {
-    const char* e = getenv("DMY_ELT_GRID");
-    return e ? atoi(e) : 16384;
-  }();
-  return grid_cap(ceil_div(n, 256), cap);
-}
+// grid of the grid-stride elementwise kernels: blocks of 256 threads, capped at 16384 (DMA-1536 step 157.61 / 157.98
+// -> 158.13 / 158.32 img/s against 8192, alternating on one box, profiles/r05/elt_grid_ab.log)
+inline int egrid(long n) { return grid_cap(ceil_div(n, 256), 16384); }
 
 }  // namespace
 

@@ -17,8 +17,8 @@ if os.environ.get('DMY_LIB_AB'):  # kernel A/B tooling only: another in-tree bui
 P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_double
 
 # name -> argtypes, exactly the header's parameter list (tests/test_abi.py derives both from include/dmayolo.h and
-# compares them); the return type is the header's: long for the *_bytes / *_elems queries and dmy_conv_dgrad_bn_rows,
-# else int (a hipError_t, or a size for the *_rows / *_blocks / *_groups queries)
+# compares them); the return type is the header's: long for the *_bytes / *_elems queries and the *_bound_rows /
+# *_last_rows queries, else int (a hipError_t, or a size for the *_rows / *_blocks / *_groups queries)
 SIGNATURES = {
     # conv.hip
     'dmy_conv_fwd_partial_rows': [L, I],
@@ -54,8 +54,6 @@ SIGNATURES = {
     'dmy_conv_fwd_fp8_partial_rows': [L, I],
     'dmy_conv_fwd_fp8': [P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, L, P, P, I, P, L, P],
     'dmy_conv_wgrad_to_oihw': [P, P, I, I, I, I, I, P],
-    'dmy_conv_dgrad_bn_rows': [I, P, P, P, I, I, I, I, L, I, I, I, I, I, I, I, L],
-    'dmy_conv_dgrad_bn': [I, P, P, P, I, I, I, I, I, L, I, I, I, I, I, I, I, L, P, L, P, P, P, P, I, P, P, P],
     # bn.hip
     'dmy_bn_partial_rows': [L],
     'dmy_bn_stats': [I, P, L, L, I, P, P, P],
@@ -148,7 +146,7 @@ SIGNATURES = {
 
 # symbols whose argtypes dmayolo/optim.py sets itself (multi-tensor optimizer / GradScaler / EMA kernels)
 SELF_BOUND = {'dmy_chunk_size', 'dmy_sgd', 'dmy_adam', 'dmy_ema', 'dmy_amp_check', 'dmy_amp_update'}
-LONG_RET = {'dmy_conv_dgrad_bn_rows', 'dmy_conv_fwd_bound_rows', 'dmy_conv_fwd_last_rows'}
+LONG_RET = {'dmy_conv_fwd_bound_rows', 'dmy_conv_fwd_last_rows'}
 
 
 def restype(name):

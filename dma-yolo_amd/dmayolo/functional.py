@@ -538,25 +538,19 @@ def eval_coef(spec, dev):
 
 
 class BnLink:
-    """A train-mode BN (+ act) layer's output, as seen by the conv that consumes it: that conv's data-grad can write the
-    layer's backward-reduce partials itself (dmy_conv_dgrad_bn), saving bn_bwd_reduce's pass over dy.  `ready` holds
-    (the data-grad buffer, its pixel stride, pdb, pdg, rows); the producer's backward uses the partials only when the
-    gradient it receives IS that buffer, unmodified.  Holding the buffer keeps autograd from accumulating another
-    contribution into it in place: any other contribution then arrives as a new tensor and the producer falls back
-    to dmy_bn_bwd_reduce."""
-    __slots__ = ('z', 'zps', 'scale', 'shift', 'mean', 'invstd', 'act', 'K', 'ready')
+    """A train-mode BN layer whose BN the consumer applies (SCConv's k3, applied by its gate: SCGateFn): the consumer's
+    backward writes the layer's backward-reduce partials itself (dmy_scgate_bn_bwd), saving bn_bwd_reduce's pass over
+    dy.  `ready` holds (the gradient buffer, its pixel stride, pdb, pdg, rows, its version); the producer's backward
+    uses the partials only when the gradient it receives IS that buffer, unmodified, and falls back to
+    dmy_bn_bwd_reduce otherwise.  (Round 2's data-grad-epilogue variant of the same partials, dmy_conv_dgrad_bn, measured
+    slower end to end -- DMA-1536 140.8 -> 138.1 img/s, profiles/r02/ab_bnfuse.log -- and was removed in round 6.)"""
+    __slots__ = ('scale', 'shift', 'mean', 'invstd', 'act', 'K', 'ready')
 
-    def __init__(self, z, scale, shift, mean, invstd, act, K):
-        self.z, self.zps = z, K
+    def __init__(self, scale, shift, mean, invstd, act, K):
         self.scale, self.shift, self.mean, self.invstd, self.act, self.K = scale, shift, mean, invstd, act, K
         self.ready = None
 
 
-# data-grad epilogues write the producer BN's reduce partials (dmy_conv_dgrad_bn).  Off by default
-# (DMY_FUSE_BN_REDUCE=1 turns it on): measured SLOWER end to end -- DMA-1536 140.8 -> 138.1 img/s, yolov5s@640
-# 3421 -> 3325 (profiles/r02/ab_bnfuse.log): the epilogue's extra z stream and reduction lengthen the data-grad by
-# more than the separate streaming bn_bwd_reduce pass it saves.
-FUSE_BN_REDUCE = [os.environ.get('DMY_FUSE_BN_REDUCE', '0') == '1']
 # SCConv's k3 BatchNorm applied by its gate (SCGateFn, dmy_scgate_bn_*): DMY_DEFER_AFFINE=0 restores the separate
 # bn_act_fwd / bn_bwd_reduce passes
 DEFER_AFFINE = [os.environ.get('DMY_DEFER_AFFINE', '1') == '1']
@@ -571,12 +565,11 @@ BWD1X1 = [os.environ.get('DMY_BWD1X1', '1') == '1']
 
 def _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc, N, C, H, W, K, k, s, p, M):
     """-> (dx, dw) when the fused kernel took the layer's apply + data-grad + weight-grad, else None.  Eligible: bf16
-    storage, train-mode BN, 1x1 stride 1, both gradients wanted, no producer-BN reduce link, a (K, C) pair the kernel
+    storage, train-mode BN, 1x1 stride 1, both gradients wanted, a (K, C) pair the kernel
     is built for (dmy_conv1x1_bwd_bn_ok).  Deterministic mode: the weight-grad partials go through a workspace summed
     in block order instead of fp32 atomics."""
     if not (BWD1X1[0] and ctx.train_bn and k == 1 and s == 1 and p == 0 and not ctx.s2d and ctx.cp == C and
-            dy.dtype == torch.bfloat16 and wt is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and
-            not (ctx.link_in is not None and FUSE_BN_REDUCE[0])):
+            dy.dtype == torch.bfloat16 and wt is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]):
         return None
     buf_probe = ctx.xsink.peek(N, C, H, W) if ctx.xsink is not None else None
     bps_probe = buf_probe[1] if buf_probe is not None else C
@@ -601,7 +594,6 @@ def _bwd1x1(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc,
 class ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, res, spec, xsink=None, rsink=None, grad_on=True):
-        link_in = getattr(x, '_dmy_bnlink', None)
         s2d = getattr(x, '_dmy_s2d', 0)
         f8in, prod = getattr(x, '_dmy_f8', None), getattr(x, '_dmy_prod', None)
         out_req, _OUT[0] = _OUT[0], None  # conv_bn_act's out view, checked against the output geometry below
@@ -719,12 +711,9 @@ class ConvBNActFn(torch.autograd.Function):
                 # the link must NOT hold z here: z is this Function's OUTPUT, so ctx -> link -> z -> grad_fn -> ctx would
                 # be a reference cycle through the C++ autograd node that Python's GC cannot break (round 4 leaked
                 # every SCConv's z, ~4 GiB per DMA-1536 step).  The gate receives z as its own input.
-                ctx.bnlink = BnLink(None, scale, shift, mean, invstd, spec.act, K)
+                ctx.bnlink = BnLink(scale, shift, mean, invstd, spec.act, K)
                 z._dmy_affine, z._dmy_bnlink = (scale, shift, mean, invstd), ctx.bnlink
                 ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, False
-                ctx.link_in = link_in if (link_in is not None and link_in.z is not None and not s2d and Cp == C and
-                                          link_in.K == C and link_in.z.shape[0] == N and
-                                          link_in.z.shape[2:] == (H, W)) else None
                 ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
                 ctx.ggeom = (Hg, Wg, kg, sg, pg)
                 ctx.cp = Cp
@@ -748,8 +737,6 @@ class ConvBNActFn(torch.autograd.Function):
                 y._dmy_prod = spec  # an fp8 consumer may ask this layer to emit its e4m3 copy (F8Emit)
             ctx.save_for_backward(x, wt, z, scale, shift, mean, invstd, bn.weight if bn.weight is not None else None)
             ctx.bnlink = None
-            if train_bn and need_grad and dt == torch.bfloat16 and FUSE_BN_REDUCE[0]:
-                ctx.bnlink = y._dmy_bnlink = BnLink(z, scale, shift, mean, invstd, spec.act, K)
         else:
             _launch_conv_fwd(x, xps, wf, bias, z, K, None, None, K, kg, sg, pg, OH, OW, C, k, f8=f8)
             if spec.act != ACT_NONE or res is not None:
@@ -761,8 +748,6 @@ class ConvBNActFn(torch.autograd.Function):
                 y = z
             ctx.save_for_backward(x, wt, z)
         ctx.spec, ctx.train_bn, ctx.has_res = spec, train_bn, res is not None
-        ctx.link_in = link_in if (link_in is not None and link_in.z is not None and not s2d and Cp == C and
-                                  link_in.K == C and link_in.z.shape[0] == N and link_in.z.shape[2:] == (H, W)) else None
         ctx.geom = (N, C, H, W, xps, K, k, s, p, OH, OW)
         ctx.ggeom = (Hg, Wg, kg, sg, pg)
         ctx.cp = Cp
@@ -855,24 +840,12 @@ class ConvBNActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if Cp != C or ctx.s2d:
                 raise NotImplementedError('input gradient of a channel-padded stem conv')
-            link = ctx.link_in
-            last = ctx.xsink is None or ctx.xsink.seen == ctx.xsink.n - 1  # this data-grad completes dx
             buf, bps, acc = sink_target(ctx.xsink, N, C, H, W, z)
             kw = dict(tag=(N, C, H, W, K, k, s),
                       nbytes=z.element_size() * (M * K + K * C * k * k + (1 + acc) * N * H * W * C))
             fl = 2.0 * M * K * C * k * k
-            P = call('dmy_conv_dgrad_bn_rows', dt, ptr(dz), ptr(wt), ptr(buf), N, H, W, C, bps, K, k, k, s, p, OH, OW,
-                     dzps) if (link is not None and last and FUSE_BN_REDUCE[0]) else 0
-            if P > 0:
-                pdb, pdg = f32(P * C, dev), f32(P * C, dev)
-                KernelTimer.run('conv_dgrad', fl, 'dmy_conv_dgrad_bn', dt, ptr(dz), ptr(wt), ptr(buf), acc, N, H, W, C,
-                                bps, K, k, k, s, p, OH, OW, dzps, ptr(link.z), link.zps, ptr(link.scale),
-                                ptr(link.shift), ptr(link.mean), ptr(link.invstd), link.act, ptr(pdb), ptr(pdg),
-                                stream(), **kw)
-                link.ready = (buf, bps, pdb, pdg, P, buf._version)
-            else:
-                KernelTimer.run('conv_dgrad', fl, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf), acc, N, H, W, C, bps,
-                                K, k, k, s, p, OH, OW, dzps, stream(), **kw)
+            KernelTimer.run('conv_dgrad', fl, 'dmy_conv_dgrad', dt, ptr(dz), ptr(wt), ptr(buf), acc, N, H, W, C, bps,
+                            K, k, k, s, p, OH, OW, dzps, stream(), **kw)
             dx = sink_result(ctx.xsink, buf)
         if ctx.needs_input_grad[1] and ctx.s2d:
             Cs = ctx.s2d

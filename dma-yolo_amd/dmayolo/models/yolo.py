@@ -26,7 +26,7 @@ from ..utils.general import make_divisible
 from ..utils.torch_utils import initialize_weights, fuse_conv_and_bn
 
 _CAT_PLAN = os.environ.get('DMY_CAT_PLAN', '1') == '1'  # see Model._make_cat_plan
-_MODEL_SINKS = os.environ.get('DMY_MODEL_SINKS', '0') != '0'  # Model-level gradient fan-out sinks
+_MODEL_SINKS = os.environ.get('DMY_MODEL_SINKS', '1') != '0'  # Model-level gradient fan-out sinks
 
 
 class Detect(nn.Module):
@@ -303,11 +303,11 @@ class Model(nn.Module):
 
     # gradient fan-out: a layer output read by several layers (the BiFPN skips, the P3-P5 outputs read by a Conv and
     # Detect) gets one GradSink that the sink-aware consumers' backward kernels write / accumulate into, so autograd
-    # does not sum their contributions with separate add kernels (DMY_MODEL_SINKS, module-level _MODEL_SINKS).
-    # Off by default: same-box A/Bs (profiles/r02/ab_model_sinks.log) put it within the ±0.5 % run-to-run noise --
-    # DMA-1536 +0.35 % with Detect included, -0.3 %..+0.05 % without; yolov5s -0.3 % with Detect (its only
-    # multi-consumer outputs are read by a Conv and Detect, whose narrow-K data-grad then accumulates), so Detect
-    # joins only under DMY_SINK_DETECT=1.  GPU model / module tests pass with it on.
+    # does not sum their contributions with separate ATen add kernels (DMY_MODEL_SINKS=0 turns it off).  On by default
+    # since round 6 (no ATen arithmetic on the hot path); same-box A/Bs (profiles/r02/ab_model_sinks.log,
+    # profiles/r04/model_sinks_ab.log) put it within the +-0.5 % run-to-run noise -- DMA-1536 +0.35 % with Detect
+    # included, -0.3 %..+0.05 % without; yolov5s -0.3 % with Detect (its only multi-consumer outputs are read by a Conv
+    # and Detect, whose narrow-K data-grad then accumulates), so Detect joins only under DMY_SINK_DETECT=1.
     _SINK_TYPES = ('Conv', 'SCConv', 'AdConcat2', 'AdConcat3') + (('Detect',) if os.environ.get('DMY_SINK_DETECT') == '1'
                                                                   else ())
 

@@ -55,15 +55,6 @@ int dmy_conv_fwd_act_ws(int dtype, const void* x, const void* w_ohwi, const floa
                         const float* shift, int act, const void* res, long rps, float* ws, long ws_elems, void* stream);
 int dmy_conv_dgrad(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
                    long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
-/* data-grad + the backward-reduce partials of the train-mode BN (+ act) that produced the conv input (its z, coefficients
- * and act; bn.hip bn_bwd_reduce arithmetic): replaces dmy_conv_dgrad + dmy_bn_bwd_reduce when the data-grad output is
- * that BN layer's complete output gradient.  _rows: partial rows written, 0 = geometry not fusable. */
-long dmy_conv_dgrad_bn_rows(int dtype, const void* dy, const void* w_ihwo, const void* dx, int N, int H, int W, int C,
-                            long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps);
-int dmy_conv_dgrad_bn(int dtype, const void* dy, const void* w_ihwo, void* dx, int accumulate, int N, int H, int W, int C,
-                      long xps, int K, int KH, int KW, int S, int P, int OH, int OW, long yps, const void* z, long zps,
-                      const float* scale, const float* shift, const float* mean, const float* invstd, int act,
-                      float* pdb, float* pdg, void* stream);
 int dmy_conv_wgrad(int dtype, const void* x, const void* dy, float* dw_ohwi, int N, int H, int W, int C, long xps,
                    int K, int KH, int KW, int S, int P, int OH, int OW, long yps, void* stream);
 /* bwd1x1.hip: fused backward of a train-mode 1x1 stride-1 Conv -> BatchNorm -> act (models/common.py:67-73, k = 1),

@@ -9,8 +9,8 @@ run again with the roundings a reduced-precision run performs, and the product i
   mode 'bf16'     the product's storage model: 'bf16_act' + the conv / linear weights rounded to bf16 in the forward
                    and data-gradient (the kernels read bf16 OHWI / IHWO copies of the fp32 master weights; the weight
                    gradient itself stays fp32) + the outputs of the composite modules whose result the product stores
-                   in bf16 (Bottleneck / Swin residual sums, CoorAttention's x * a_w * a_h, the AdConcat weighted
-                   copies, SCConv's gate product, CBAM's ca, ca * x, pooled map, spatial gate and output);
+                   in bf16 (Bottleneck / Swin residual sums, CoorAttention's pooled means and x * a_w * a_h, the
+                   AdConcat weighted copies, SCConv's gate product, CBAM's ca, ca * x, pooled map, spatial gate and output);
   mode 'bf16_sink' 'bf16' + each leaf's INPUT gradient rounded to bf16 as it leaves the leaf: the product's data-grad
                    kernels store every contribution to an input gradient in bf16 and accumulate the next one into that
                    bf16 buffer (functional.GradSink; autograd's own sums of bf16 gradients), where 'bf16' sums the
@@ -155,6 +155,18 @@ def emulate(model, mode):
                     sa = RoundAct.apply(torch.sigmoid(m.spatial_attention.conv2d(s2)), dt)
                     return RoundAct.apply(sa * out1, dt)
                 mod.forward = cbam_fwd
+    if hasattr(onn, 'CoorAttention'):
+        for mod in model.modules():
+            if isinstance(mod, onn.CoorAttention):
+                def ca_fwd(x, m=mod):  # the product stores the pooled row / column means (CAPoolFn) in bf16
+                    _, _, H, W = x.shape
+                    pooled = RoundAct.apply(torch.cat([x.mean(3, keepdim=True), x.mean(2, keepdim=True).transpose(2, 3)],
+                                                      2), dt)
+                    y = m.act(onn._bn_train_or_eval(m.bn1, m.conv1(pooled)))
+                    ah = torch.sigmoid(m.conv_h(y[:, :, :H]))
+                    aw = torch.sigmoid(m.conv_w(y[:, :, H:].transpose(2, 3)))
+                    return x * aw * ah
+                mod.forward = ca_fwd
     if hasattr(onn, 'SCConv'):
         for mod in model.modules():
             if isinstance(mod, onn.SCConv):

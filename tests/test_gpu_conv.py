@@ -148,8 +148,7 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
         z = ref.bfloat16().float()  # the epilogue acts on the bf16-rounded conv output
         ref = F.silu(z * sc.view(1, K, 1, 1) + sh.view(1, K, 1, 1)) + res.float()
     assert _rel(y.float(), ref) < 1e-2
-    # the in-launch combine sums the slabs in split order whichever block draws the last ticket: 20 launches on a
-    # NaN-filled workspace give the same bits every time
+    # the split slabs are summed in split order: 20 launches on a NaN-filled workspace give the same bits every time
     first = y.clone()
     for i in range(20):
         ws.fill_(float('nan'))  # a reducer that read a slab before its producer's stores were visible would show NaN
@@ -161,31 +160,23 @@ def test_conv_fwd_splitk_vs_torch(N, C, H, W, K, k, s, epi):
 @pytest.mark.parametrize('N,C,H,W,K', [(16, 64, 160, 160, 64), (16, 64, 150, 146, 48), (10, 128, 128, 136, 32),
                                        (16, 128, 100, 104, 128), (8, 256, 96, 96, 256), (10, 128, 96, 96, 192),
                                        (8, 16, 288, 288, 64), (8, 16, 290, 282, 32)])
-def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K, monkeypatch):
-    """3x3 s1 weight-grad on the tap-fused kernel, two halo planes (64 input channels per block: DMY_WGRAD_TAP_NP=2 for
-    <= 64 output channels, DMY_WGRAD_TAP_NP128=1 for more) and one: both against torch's fp32 conv2d_weight, and
-    against each other.  C = 16 is the space-to-depth stem's view (half a plane, the rest loads zeros)"""
-    import os
+def test_conv_wgrad_tap_two_planes_vs_torch(N, C, H, W, K):
+    """3x3 s1 weight-grad on the tap-fused kernel against torch's fp32 conv2d_weight: two halo planes (64 input channels
+    per block) for <= 64 output channels with C % 64 == 0, one plane otherwise (the 128-row tile, C % 64 != 0).  C = 16
+    is the space-to-depth stem's view (half a plane, the rest loads zeros)"""
     from dmayolo.functional import call, ptr, stream
-    monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP128', '1')
     g = torch.Generator().manual_seed(N + C + K + H)
     x = torch.randn(N, C, H, W, generator=g).bfloat16()
     dy = torch.randn(N, K, H, W, generator=g).bfloat16()
     ref = torch.nn.grad.conv2d_weight(x.float().cuda(), (K, C, 3, 3), dy.float().cuda(), stride=1, padding=1)
     xd = x.cuda().contiguous(memory_format=torch.channels_last)
     dyd = dy.cuda().contiguous(memory_format=torch.channels_last)
-    out = {}
-    for np_ in ('2', '1'):
-        monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP', np_)
-        monkeypatch.setitem(os.environ, 'DMY_WGRAD_TAP_NP128', '1' if np_ == '2' else '0')
-        dwo = torch.empty(K * C * 9, device='cuda')
-        dw = torch.empty(K, C, 3, 3, device='cuda')
-        assert call('dmy_conv_wgrad', 1, ptr(xd), ptr(dyd), ptr(dwo), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K, stream()) == 0
-        call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, C, 3, 3, stream())
-        torch.cuda.synchronize()
-        out[np_] = dw
-        assert _rel(dw, ref) < 2e-3, (np_, _rel(dw, ref))
-    assert _rel(out['2'], out['1']) < 1e-4
+    dwo = torch.empty(K * C * 9, device='cuda')
+    dw = torch.empty(K, C, 3, 3, device='cuda')
+    assert call('dmy_conv_wgrad', 1, ptr(xd), ptr(dyd), ptr(dwo), N, H, W, C, C, K, 3, 3, 1, 1, H, W, K, stream()) == 0
+    call('dmy_conv_wgrad_to_oihw', ptr(dwo), ptr(dw), K, C, C, 3, 3, stream())
+    torch.cuda.synchronize()
+    assert _rel(dw, ref) < 2e-3, _rel(dw, ref)
 
 
 def test_conv_fwd_1x1_small_m_unsplit():
@@ -197,13 +188,12 @@ def test_conv_fwd_1x1_small_m_unsplit():
                 256) == 0
 
 
-# eval forwards (dmy_conv_fwd_act) whose 256-row tile grid leaves CUs idle -- the v2 tiles, or the LDS-DMA kernel on
-# 128 x 128 / 128 x 64 tiles under DMY_V3_FILL=1 (fill_tile) -- ragged M / columns, a residual, a concat-slice output
+# eval forwards (dmy_conv_fwd_act) whose 256-row tile grid leaves CUs idle (the v2 tiles, split-K, halo), ragged M /
+# columns, a residual, a concat-slice output
 FILL_SHAPES = [(1, 256, 96, 96, 256, 1, 1), (1, 128, 192, 192, 128, 1, 1), (1, 128, 190, 186, 128, 3, 1),
                (1, 512, 48, 48, 512, 1, 1), (1, 1024, 37, 41, 200, 1, 1), (2, 64, 45, 47, 136, 1, 1),
                (1, 256, 96, 96, 1024, 1, 1), (3, 128, 65, 67, 512, 3, 2),
-               # output-heavy 1x1 eval forwards (M >= 16384, K >= 2C; on the streaming GEMM's epilogue,
-               # conv_p1s<.., EPI>, under DMY_P1S_EP=1): 64-column passes, a 32-column tail pass, a 16-B residual
+               # output-heavy 1x1 eval forwards (M >= 16384, K >= 2C): 64-column tiles, a 32-column tail, a residual
                (1, 128, 192, 192, 512, 1, 1), (2, 64, 130, 126, 128, 1, 1), (1, 256, 128, 130, 544, 1, 1)]
 
 
@@ -239,16 +229,15 @@ def test_conv_fwd_fill_tiles_vs_torch(N, C, H, W, K, k, s, res):
     assert torch.equal(yb[:, K:].float().cpu(), torch.full((N, 64, OH, OW), 7.0)), 'columns past K must stay untouched'
 
 
-# small-M eval forwards on the register-epilogue GEMM (v3::conv_sk, M <= 65536, channels % 32): 1x1 with one and several
-# KC chunks, 3x3 stride 1 / 2 gathers with a partial last chunk, channel tiles past K (K % BN != 0), C % 64 != 0,
-# M not a multiple of 64, bias + eval-BN + SiLU + residual, output into a concat-buffer slice
+# small-M eval forwards (batch-1 detect shapes, the inference routes): 1x1 and 3x3 stride 1 / 2, channel tiles past K,
+# C % 64 != 0, M not a multiple of 64, bias + eval-BN + SiLU + residual, output into a concat-buffer slice
 SK_SHAPES = [(1, 256, 96, 96, 256, 1, 1, True), (1, 1024, 48, 48, 1024, 1, 1, False), (1, 64, 97, 95, 64, 3, 1, True),
              (1, 128, 61, 59, 256, 3, 2, False), (2, 96, 33, 35, 96, 3, 1, True), (1, 32, 70, 66, 32, 1, 1, False),
              (1, 512, 24, 26, 160, 3, 1, True), (3, 192, 21, 23, 352, 1, 1, True), (1, 2048, 12, 12, 512, 1, 1, False)]
 
 
 @pytest.mark.parametrize('N,C,H,W,K,k,s,res', SK_SHAPES)
-def test_conv_fwd_small_m_sk_vs_torch(N, C, H, W, K, k, s, res):
+def test_conv_fwd_small_m_eval_vs_torch(N, C, H, W, K, k, s, res):
     from dmayolo.functional import call, ptr, stream, prep_weight
     from dmayolo._lib import ACT_SILU
     g = torch.Generator().manual_seed(N * 31 + C + 3 * K + k + int(res))

@@ -26,7 +26,7 @@ def wrapped(ctx, dy, dps, x, xps, wt, z, scale, shift, mean, invstd, ca, cb, cc,
         why = 'fused' if r is not None else ','.join(n for n, c in (
             ('needs_dx', not ctx.needs_input_grad[0]), ('needs_dw', not ctx.needs_input_grad[1]),
             ('wt', wt is None), ('s2d', bool(ctx.s2d)), ('cp', ctx.cp != C), ('dtype', dy.dtype != torch.bfloat16),
-            ('stride', s != 1 or p != 0), ('link', ctx.link_in is not None and fn.FUSE_BN_REDUCE[0])) if c) or \
+            ('stride', s != 1 or p != 0)) if c) or \
             f'ok-query (K {K} C {C} dps {dps} xps {xps} sink {ctx.xsink is not None})'
         seen[(K, C, why)] += 1
     return r
