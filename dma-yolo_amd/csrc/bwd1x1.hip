@@ -334,11 +334,17 @@ int num_cus() {
 struct Plan {
   int cb, tp, px;
 };
+#ifndef B1_TP256  // A/B build switch (round 6): pixels per tile of the K = 256 column-split shapes
+#define B1_TP256 32
+#endif
+#ifndef B1_PX256
+#define B1_PX256 1
+#endif
 constexpr Plan plan(int K, int C) {
   return (K == 64 && C == 64) ? Plan{64, 128, 2} : (K == 128 && C == 64) ? Plan{64, 128, 2}
        : (K == 64 && C == 128) ? Plan{128, 64, 2} : (K == 128 && C == 128) ? Plan{128, 64, 2}
        : (K == 128 && C == 256) ? Plan{256, 64, 2} : (K == 128 && C == 512) ? Plan{256, 64, 2}
-       : (K == 256 && C == 256) ? Plan{128, 32, 1} : (K == 256 && C == 128) ? Plan{128, 32, 1}
+       : (K == 256 && C == 256) ? Plan{128, B1_TP256, B1_PX256} : (K == 256 && C == 128) ? Plan{128, B1_TP256, B1_PX256}
        : (K == 64 && C == 256) ? Plan{256, 64, 2} : Plan{0, 0, 0};
 }
 

@@ -1022,10 +1022,12 @@ __global__ void ca_apply_fwd_kernel(const T* __restrict__ x, long xps, const T* 
     const int h = (int)(t % H);
     const int b = (int)(t / H);
     const long pix = ((long)b * H + h) * W + w;
-    const float ah = to_f(from_f<T>(sigmoidf_(to_f(lh[((long)b * (H + W) + h) * C + c]))));
-    const float aw = to_f(from_f<T>(sigmoidf_(to_f(lw[((long)b * (H + W) + H + w) * C + c]))));
+    // x * a_w * a_h in fp32, rounded once to the storage type (round 6: the attention weights and x * a_w were rounded
+    // to bf16 on the way, three extra roundings that put the bf16 output error at 1.8x the storage emulation's)
+    const float ah = sigmoidf_(to_f(lh[((long)b * (H + W) + h) * C + c]));
+    const float aw = sigmoidf_(to_f(lw[((long)b * (H + W) + H + w) * C + c]));
     const float xv = to_f(x[pix * xps + c]);
-    out[pix * ops + c] = from_f<T>(to_f(from_f<T>(xv * aw)) * ah);
+    out[pix * ops + c] = from_f<T>(xv * aw * ah);
   }
 }
 
