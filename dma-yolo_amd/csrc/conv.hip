@@ -907,10 +907,15 @@ template <int BM, int BN, int NS = 3, int WTR = 64> struct Cfg3 {
   static constexpr int NSTAGE = NS;
   static constexpr int WM = BM / WTR, WN = BN / 64, NW = WM * WN, NTH = NW * 64;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  static constexpr int APW = A_BYTES / 1024 / NW, BPW = B_BYTES / 1024 / NW;  // 1-KiB pieces per wave
+  // 1-KiB LDS-DMA pieces of a stage (8 rows of 128 B) and per wave.  BM = 288 (the 288-row wide tile) has 36 A pieces
+  // for 8 waves: waves take pieces j * NW + wid, the first PA % NW waves one more; only with NS = 2, whose main loop
+  // waits for vmcnt(0), so the per-wave counts never enter a counted wait
+  static constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024;
+  static constexpr int APW = (PA + NW - 1) / NW, BPW = PB / NW;
+  static constexpr bool AEVEN = PA % NW == 0;
   static constexpr int CT = BM * (BN + 8) * 2;
   static constexpr int LDS = NSTAGE * STAGE > CT ? NSTAGE * STAGE : CT;
-  static_assert(APW >= 1 && BPW >= 1 && APW * NW * 1024 == A_BYTES && BPW * NW * 1024 == B_BYTES, "tile");
+  static_assert(APW >= 1 && BPW >= 1 && PA * 1024 == A_BYTES && BPW * NW == PB && (AEVEN || NS == 2), "tile");
 };
 
 DEV void glds16(const void* g, char* lds_wave_base) {
@@ -931,6 +936,7 @@ DEV bf16x8 frag_sw(const bf16* X, int r0, int k0, int lane) {
 template <int BM, int BN, int NS, bool P1, bool DG>
 struct FwdLds {
   using C3_ = Cfg3<BM, BN, NS>;
+  static_assert(C3_::AEVEN, "FwdLds: whole A pieces per wave");
   const bf16* x; const bf16* w; Geom g; int Ktot;
   int k, ci, kh, kw;  // this lane's K chunk for the next issue (advanced incrementally)
   long abase[C3_::APW]; int ih0[C3_::APW], iw0[C3_::APW]; bool aval[C3_::APW];
@@ -1047,7 +1053,7 @@ struct FwdLdsB {
     kl = ((lane & 7) ^ ((lane >> 3) & 6)) * (16 / ES);
 #pragma unroll
     for (int j = 0; j < C3_::APW; ++j) {
-      const long m = m0 + (wid * C3_::APW + j) * 8 + (lane >> 3);
+      const long m = m0 + apiece(wid, j) * 8 + (lane >> 3);
       aval[j] = m < M;
       const int mm = (int)(aval[j] ? m : 0);
       const int ow = mm % g.OW, t = mm / g.OW, oh = t % g.OH, b = t / g.OH;
@@ -1064,6 +1070,9 @@ struct FwdLdsB {
       boff[j] = n < g.K ? (unsigned)(n * Ktot + kl) * (unsigned)ES : kBufOob;
     }
   }
+  // the A piece (8 rows) a wave's j-th load covers: consecutive per wave, or interleaved when the pieces do not split
+  // evenly (BM = 288); a piece index >= PA is no load at all (wave-uniform)
+  static DEV int apiece(int wid, int j) { return C3_::AEVEN ? wid * C3_::APW + j : j * C3_::NW + wid; }
   // advance the cursor by n K steps without loading (split-K: start at this split's first step)
   DEV void skip(int n) {
     kpos += n * BKE;
@@ -1086,9 +1095,11 @@ struct FwdLdsB {
     const int bk = S2 ? (kh * KW + kw) * C + ci0 : kpos;  // this step's column of the (kh, kw, c) weight rows
 #pragma unroll
     for (int j = 0; j < C3_::APW; ++j) {
+      const int pc = apiece(wid, j);
+      if (!C3_::AEVEN && pc >= C3_::PA) break;
       bool ok = aval[j];
       if (!P1) ok = ok && (unsigned)(ih0[j] + dh) < (unsigned)H && (unsigned)(iw0[j] + dw) < (unsigned)W;
-      blds16(rx, ok ? (unsigned)(pix[j] + delta) * (unsigned)ES : kBufOob, stage + (wid * C3_::APW + j) * 1024);
+      blds16(rx, ok ? (unsigned)(pix[j] + delta) * (unsigned)ES : kBufOob, stage + pc * 1024);
     }
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j)
@@ -1185,7 +1196,11 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
                      float* __restrict__ psum, float* __restrict__ psq, int accumulate, const Geom& g, int tm,
                      long m0, int n0, const v3::S2Cls& cls, const Epi& ep) {
   using C3_ = Cfg3<BM, BN, NS, WTR>;
-  constexpr int NI = WTR / 16, NQ = NI / 2;  // 16-row fragments and 32-row groups per wave
+  // 16-row fragments and 32-row groups per wave; PW: wave tiles of a row count that is no multiple of 32 (the 288-row
+  // wide tile, 144 rows per wave) write ONE BN partial row per wave and tile, row tm * WM + wm (plan_v3's row count)
+  constexpr int NI = WTR / 16;
+  constexpr bool PW = WTR % 32 != 0;
+  constexpr int NQ = PW ? 1 : NI / 2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long M = (long)g.N * g.OH * g.OW;
   const int wm = wid % C3_::WM, wn = wid / C3_::WM;
@@ -1207,8 +1222,8 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
         const float v = acc[i][j][r] + bv;
         ct[row * RS + c] = __float2bfloat16(v);
         if (m0 + row < M) {
-          s1[i >> 1] += v;
-          s2[i >> 1] += v * v;
+          s1[PW ? 0 : i >> 1] += v;
+          s2[PW ? 0 : i >> 1] += v * v;
         }
       }
     if (psum != nullptr) {
@@ -1220,7 +1235,13 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
         s2[q] += __shfl_xor(s2[q], 32, 64);
       }
       const int n = n0 + c;
-      if (lane < 16 && n < g.K) {
+      if constexpr (PW) {
+        if (lane < 16 && n < g.K) {
+          const long wr = (long)tm * C3_::WM + wm;
+          psum[wr * g.K + n] = s1[0];
+          psq[wr * g.K + n] = s2[0];
+        }
+      } else if (lane < 16 && n < g.K) {
         const long b32 = (long)tm * (BM / 32) + wm * (WTR / 32);  // first 32-row block of this wave
         if (half) {
 #pragma unroll
@@ -1617,9 +1638,10 @@ __global__ void __launch_bounds__(BM * BN / 64) conv_dgrad_s2_v3(const bf16* __r
 // the MFMAs wait on are not queued behind the DMA's LDS writes.  Measured against DMA first (round 4,
 // profiles/r04/wide_ff_ab.log, cold caches): 3x3 256 @96^2 fwd 430 -> 418 us, 512 @96^2 fwd 1201 -> 1171, dgrad 1156 ->
 // 1114, 1024 @48^2 fwd 1254 -> 1211; DMA-1536 step 153.8 / 153.6 -> 154.8 / 154.4 img/s
-template <int BM, int BN, int NS, class LD>
-DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int lane) {
-  using C3_ = Cfg3<BM, BN, NS, 128>;
+template <int BM, int BN, int NS, int WTR, class LD>
+DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[WTR / 16][4], int wid, int lane) {
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
+  constexpr int NI = WTR / 16;
   constexpr int PER = C3_::APW + C3_::BPW;
   const int wm = wid % C3_::WM, wn = wid / C3_::WM;
   ld.issue(smem, wid);
@@ -1632,33 +1654,35 @@ DEV void mainloop_w(LD& ld, int nk, char* smem, f32x4 (&acc)[8][4], int wid, int
     const bf16* Bs = As + BM * BK;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8 a[8], b[4];
+      bf16x8 a[NI], b[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = frag_sw(Bs, wn * 64 + j * 16, h * 32, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = frag_sw(As, wm * 128 + i * 16, h * 32, lane);
+      for (int i = 0; i < NI; ++i) a[i] = frag_sw(As, wm * WTR + i * 16, h * 32, lane);
       if (h == 0) {
         __builtin_amdgcn_sched_barrier(0);
         if (kt + NS - 1 < nk) ld.issue(smem + ((kt + NS - 1) % NS) * C3_::STAGE, wid);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
 }
 
-// BM x BN = 256 x 256 (2 x 4 waves) or 512 x 128 (4 x 2 waves, the 128-column layers; 2 x 80 KiB of LDS)
+// BM x BN = 256 x 256 (2 x 4 waves of 128 x 64), 288 x 256 (2 x 4 waves of 144 x 64: the row count whose tile grid
+// fills whole rounds of the chip on the DMA-YOLO / config-5 maps, see plan_v3) or 512 x 128 (4 x 2 waves, the
+// 128-column layers; 2 x 80 KiB of LDS)
 template <int BM, int BN, bool P1, bool DG>
 __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   float* __restrict__ psum, float* __restrict__ psq, int accumulate,
                                                   Geom g, int gm, int gn, unsigned xbytes, unsigned wbytes, Epi ep) {
-  constexpr int NS = 2;
-  static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
-  using C3_ = Cfg3<BM, BN, NS, 128>;
+  constexpr int NS = 2, WN = BN / 64, WM = 8 / WN, WTR = BM / WM;
+  static_assert(WM * WN == 8 && WTR % 16 == 0, "8 waves of WTR x 64");
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int tile = xcd_remap(blockIdx.x, gm * gn);
@@ -1666,16 +1690,16 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
   const long M = (long)g.N * g.OH * g.OW;
   const long m0 = (long)tm * BM;
   const int n0 = tn * BN;
-  f32x4 acc[8][4];
+  f32x4 acc[WTR / 16][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < WTR / 16; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (g.KH * g.KW * g.C + BK - 1) / BK;
-  FwdLdsB<BM, BN, NS, P1, DG, false, 2, 128> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
-  mainloop_w<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  FwdLdsB<BM, BN, NS, P1, DG, false, 2, WTR> ld(x, w, g, M, m0, n0, wid, lane, xbytes, wbytes);
+  mainloop_w<BM, BN, NS, WTR>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
-  v3_epilogue<BM, BN, NS, DG, 1, 128>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
+  v3_epilogue<BM, BN, NS, DG, 1, WTR>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
                                       n0, S2Cls{0, 0, 0, 0}, ep);
 }
 
@@ -3565,7 +3589,7 @@ int launch_halo(const bf16* x, const bf16* w, bf16* y, float* ps, float* pq, con
 // ---------------------------------------------------------------- routing plans
 // One function decides which kernel a bf16 implicit-GEMM launch takes; the launch executes that plan and
 // dmy_conv_fwd_bn_rows reads the BN partial-row count off the same plan, so the two cannot drift.
-enum class Kern { HALO, SPLITK, P1S, STEM, P1P, PIPE8, WIDE, TALL, V3, V2 };
+enum class Kern { HALO, SPLITK, P1S, STEM, P1P, PIPE8, WIDE, WIDE288, TALL, V3, V2 };
 struct Plan {
   Kern k;
   bool buf;   // buffer-descriptor loader (C % 64 == 0, byte offsets < 4 GiB)
@@ -3592,8 +3616,21 @@ Plan plan_v3(const Geom& gv, const void* x, const void* w, const void* y, int ac
     }
     return pl;
   }
-  if (pl.buf && gv.K >= kWideMinCols && (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus())
-    return pl.k = p1 ? Kern::PIPE8 : Kern::WIDE, pl;  // 1x1 views: the half-tile pipeline (conv_fwd_8p)
+  if (pl.buf && gv.K >= kWideMinCols && (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
+    if (p1) return pl.k = Kern::PIPE8, pl;  // 1x1 views: the half-tile pipeline (conv_fwd_8p)
+    // k > 1: 256- or 288-row tiles, whichever grid ends in fewer row-weighted rounds of the chip.  A block per CU at a
+    // time, so a grid of 4.5 rounds (3x3 256 @96^2 bs32: 1152 tiles of 256 rows) costs 5 and idles half the chip for
+    // the last; 288 = 9 x 32 divides every DMA-YOLO @1536 / config-5 @1920 map (1536^2 and 1920^2 carry a factor 9):
+    // 1024 tiles, 4 rounds of 288 rows = 1152 row-times against 1280.  (2.25 -> 2 rounds at 512 @48^2.)
+    const long gn = ceil_div(gv.K, 256), NC = num_cus();
+    const long t256 = ceil_div(ceil_div(M, 256) * gn, NC) * 256, t288 = ceil_div(ceil_div(M, 288) * gn, NC) * 288;
+    if (t288 < t256) {
+      pl.k = Kern::WIDE288;
+      pl.rows = ceil_div(M, 288) * 2;  // one BN partial row per wave row (2) and row tile
+      return pl;
+    }
+    return pl.k = Kern::WIDE, pl;
+  }
   if (pl.buf && !p1 && gv.K > 64 && gv.K <= 128 && (long)ceil_div(M, 512) * ceil_div(gv.K, 128) >= 4L * num_cus())
     return pl.k = Kern::TALL, pl;
   return pl;
@@ -3637,6 +3674,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
       return (int)hipGetLastError();
     }
     case Kern::WIDE: W_GO(256, 256)
+    case Kern::WIDE288: W_GO(288, 256)
     case Kern::TALL: W_GO(512, 128)
     default: break;
   }
