@@ -328,23 +328,20 @@ int num_cus() {
 // the prefetch point) measured 1-11 % SLOWER on every shape (profiles/r05/bwd1x1_depth2_ab.log): the PMC passes show
 // these launches issue-bound (~50 % of wave cycles issuing, 25-39 % waiting, profiles/r05/pmc_bwd1x1.txt), not
 // starved for loads in flight
+// 64-pixel tiles for the K = 256 column-split shapes (PX 1 or 2) spill 29-32 VGPRs at 256 VGPRs + 256 AGPRs and
+// measured slower: C256 -> K256 @96^2 bs32 266 -> 307..326 us, @192^2 911 -> 1071..1147 us (round 6,
+// profiles/r06/bwd1x1_tp_ab.log)
 // An 8-wave single block per tile for the K = 256 layers (no column split, the transform once; 4 x 2 or 2 x 4 wave grid)
 // does not fit: 2 waves per SIMD leave 256 registers per wave, and the kernel's working set besides the weight-grad
 // accumulators is ~290 (63-80 VGPRs spilled at 256 x 256 / 256 x 128), so it was not built
 struct Plan {
   int cb, tp, px;
 };
-#ifndef B1_TP256  // A/B build switch (round 6): pixels per tile of the K = 256 column-split shapes
-#define B1_TP256 32
-#endif
-#ifndef B1_PX256
-#define B1_PX256 1
-#endif
 constexpr Plan plan(int K, int C) {
   return (K == 64 && C == 64) ? Plan{64, 128, 2} : (K == 128 && C == 64) ? Plan{64, 128, 2}
        : (K == 64 && C == 128) ? Plan{128, 64, 2} : (K == 128 && C == 128) ? Plan{128, 64, 2}
        : (K == 128 && C == 256) ? Plan{256, 64, 2} : (K == 128 && C == 512) ? Plan{256, 64, 2}
-       : (K == 256 && C == 256) ? Plan{128, B1_TP256, B1_PX256} : (K == 256 && C == 128) ? Plan{128, B1_TP256, B1_PX256}
+       : (K == 256 && C == 256) ? Plan{128, 32, 1} : (K == 256 && C == 128) ? Plan{128, 32, 1}
        : (K == 64 && C == 256) ? Plan{256, 64, 2} : Plan{0, 0, 0};
 }
 
