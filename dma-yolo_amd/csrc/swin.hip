@@ -508,6 +508,51 @@ __global__ void sample_scale_kernel(const T* __restrict__ x, const float* __rest
     y[i] = from_f<T>(to_f(x[i]) * sc[i / per]);
 }
 
+// DropPath fused with the residual add it feeds (an active SwinTransformerLayer drop_path, common.py:621-627):
+// y = x + f * s[b], s[b] = floor(keep + u[b]) / keep -- torch's (keep + rand).floor_().div_(keep) on the drawn u, in
+// fp32, one rounding of the sum (the unfused pair rounded f * s first).  grad: df = dy * s[b] (dx = dy needs no pass).
+// Samples are contiguous blocks of `per` elements (NHWC); 8-element vectors when per % 8 == 0 and 16-B aligned.
+DEV float dp_scale(const float* u, long b, float keep) { return floorf(keep + u[b]) / keep; }
+template <typename T>
+__global__ void droppath_add_kernel(const T* __restrict__ x, const T* __restrict__ f, const float* __restrict__ u,
+                                    float keep, T* __restrict__ y, long per, long n, int vec) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (vec) {
+    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n / 8; v += stride) {
+      const long i = v * 8;
+      const float sc = dp_scale(u, i / per, keep);
+      float a[8], b[8];
+      unpack<T>(*reinterpret_cast<const uint4*>(x + i), a);
+      unpack<T>(*reinterpret_cast<const uint4*>(f + i), b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += b[j] * sc;
+      *reinterpret_cast<uint4*>(y + i) = pack<T>(a);
+    }
+    return;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = from_f<T>(to_f(x[i]) + to_f(f[i]) * dp_scale(u, i / per, keep));
+}
+template <typename T>
+__global__ void droppath_grad_kernel(const T* __restrict__ dy, const float* __restrict__ u, float keep,
+                                     T* __restrict__ df, long per, long n, int vec) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (vec) {
+    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n / 8; v += stride) {
+      const long i = v * 8;
+      const float sc = dp_scale(u, i / per, keep);
+      float a[8];
+      unpack<T>(*reinterpret_cast<const uint4*>(dy + i), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] *= sc;
+      *reinterpret_cast<uint4*>(df + i) = pack<T>(a);
+    }
+    return;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+    df[i] = from_f<T>(to_f(dy[i]) * dp_scale(u, i / per, keep));
+}
+
 // ---------------------------------------------------------------- bf16 window attention on MFMA
 // Throughput mode: one wave per (window, head), NW waves per workgroup sharing one head (the
 // bias-table column is staged once per workgroup).  All six products are 16x16x32 bf16 MFMAs
@@ -969,6 +1014,25 @@ DMY_API int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const 
   else winattn_bwd_kernel<float><<<grid, 256, 0, st>>>((const float*)qkv, (const float*)dout, table, (float*)dqkv, dtab_part, nwin, wpb, g);
   const int ntab = (2 * WS - 1) * (2 * WS - 1) * nh;
   dtab_reduce_kernel<<<ntab, 256, 0, st>>>(dtab_part, groups, nh, dtab);
+  return (int)hipGetLastError();
+}
+
+DMY_API int dmy_droppath_add(int dtype, const void* x, const void* f, const float* u, float keep, void* y, long per,
+                             long n, void* stream) {
+  if (n == 0) return 0;
+  const int vec = dtype && per % 8 == 0 && (((uintptr_t)x | (uintptr_t)f | (uintptr_t)y) & 15) == 0;
+  const int g = grid_cap(ceil_div(vec ? n / 8 : n, 256), 16384);
+  if (dtype) droppath_add_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>((const bf16*)x, (const bf16*)f, u, keep, (bf16*)y, per, n, vec);
+  else droppath_add_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)x, (const float*)f, u, keep, (float*)y, per, n, 0);
+  return (int)hipGetLastError();
+}
+DMY_API int dmy_droppath_grad(int dtype, const void* dy, const float* u, float keep, void* df, long per, long n,
+                              void* stream) {
+  if (n == 0) return 0;
+  const int vec = dtype && per % 8 == 0 && (((uintptr_t)dy | (uintptr_t)df) & 15) == 0;
+  const int g = grid_cap(ceil_div(vec ? n / 8 : n, 256), 16384);
+  if (dtype) droppath_grad_kernel<bf16><<<g, 256, 0, (hipStream_t)stream>>>((const bf16*)dy, u, keep, (bf16*)df, per, n, vec);
+  else droppath_grad_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)dy, u, keep, (float*)df, per, n, 0);
   return (int)hipGetLastError();
 }
 

@@ -141,6 +141,8 @@ SIGNATURES = {
     'dmy_winattn_bwd_groups': [I, I, I, I],
     'dmy_winattn_bwd': [I, P, P, P, P, P, P, I, I, I, I, I, I, F, P],
     'dmy_sample_scale': [I, P, P, P, L, L, P],
+    'dmy_droppath_add': [I, P, P, P, F, P, L, L, P],
+    'dmy_droppath_grad': [I, P, P, F, P, L, L, P],
 }
 
 

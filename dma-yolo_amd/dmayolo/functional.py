@@ -1430,6 +1430,34 @@ class SampleScaleFn(torch.autograd.Function):
         return dx, None
 
 
+class DropPathAddFn(torch.autograd.Function):
+    """x + DropPath(f) (common.py:386-403 with the residual of common.py:621-627): y = x + f * s[b], s[b] = floor(keep +
+    u[b]) / keep on torch's drawn uniforms u [N] (csrc/swin.hip droppath_add_kernel: one pass, one rounding of the sum;
+    was dmy_sample_scale + AddFn + torch's floor / div).  Backward: dx = dy (through the residual's GradSink when it
+    has one), df = dy * s[b]."""
+
+    @staticmethod
+    def forward(ctx, x, f, u, keep, xsink=None):
+        x, f = _sample_major(x), _sample_major(f)
+        assert x.shape == f.shape and u.numel() == x.shape[0] and u.dtype == torch.float32
+        y = torch.empty_like(x)
+        call('dmy_droppath_add', dcode(x), ptr(x), ptr(f), ptr(u), float(keep), ptr(y), x.numel() // x.shape[0],
+             x.numel(), stream())
+        ctx.save_for_backward(u)
+        ctx.keep, ctx.xsink = float(keep), xsink
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (u,) = ctx.saved_tensors
+        dy = _sample_major(dy)
+        df = torch.empty_like(dy)
+        call('dmy_droppath_grad', dcode(dy), ptr(dy), ptr(u), ctx.keep, ptr(df), dy.numel() // dy.shape[0], dy.numel(),
+             stream())
+        dx = dy if ctx.xsink is None else ctx.xsink.passthrough(dy)
+        return dx, df, None, None, None
+
+
 # ------------------------------------------------------------------ space_to_depth / TDetect flatten
 
 class SpaceToDepthFn(torch.autograd.Function):

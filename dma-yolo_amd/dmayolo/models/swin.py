@@ -20,6 +20,11 @@ class DropPath(nn.Module):
         s = (keep + torch.rand((x.shape[0],), dtype=torch.float32, device=x.device)).floor_().div_(keep)
         return Fn.SampleScaleFn.apply(x, s)
 
+    def add(self, x, f, xsink=None):
+        """x + self(f) in one pass (functional.DropPathAddFn): the same uniforms and keep rule as forward"""
+        u = torch.rand((f.shape[0],), dtype=torch.float32, device=f.device)
+        return Fn.DropPathAddFn.apply(x, f, u, 1 - self.drop_prob, xsink)
+
 
 class Mlp(nn.Module):
     def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
@@ -79,8 +84,8 @@ class SwinTransformerLayer(nn.Module):
         o = Fn.WinAttnFn.apply(qkv, a.relative_position_bias_table, a.num_heads, self.shift_size, a.scale)
         dp = isinstance(self.drop_path, DropPath) and self.training and self.drop_path.drop_prob
         if dp:
-            x = Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias,
-                                                                None, 1, 0, Fn.ACT_NONE)), s1)
+            x = self.drop_path.add(x, Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias, None, 1, 0,
+                                                     Fn.ACT_NONE), s1)
         else:
             x = Fn.conv_bn_act(o, a.proj.weight.view(c, c, 1, 1), a.proj.bias, None, 1, 0, Fn.ACT_NONE, res=x,
                                rsink=s1)
@@ -89,8 +94,8 @@ class SwinTransformerLayer(nn.Module):
         hd = m.fc1.weight.shape[0]
         h = Fn.conv_bn_act(u2, m.fc1.weight.view(hd, c, 1, 1), m.fc1.bias, None, 1, 0, Fn.ACT_GELU)
         if dp:
-            return Fn.AddFn.apply(x, self.drop_path(Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias,
-                                                                   None, 1, 0, Fn.ACT_NONE)), s2)
+            return self.drop_path.add(x, Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0,
+                                                        Fn.ACT_NONE), s2)
         return Fn.conv_bn_act(h, m.fc2.weight.view(c, hd, 1, 1), m.fc2.bias, None, 1, 0, Fn.ACT_NONE, res=x,
                               rsink=s2, out=out)
 

@@ -270,6 +270,12 @@ int dmy_winattn_bwd_groups(int B, int H, int W, int nh);
 int dmy_winattn_bwd(int dtype, const void* qkv, const void* dout, const float* table, void* dqkv, float* dtab_part,
                     float* dtab, int B, int H, int W, int C, int nh, int shift, float scale, void* stream);
 int dmy_sample_scale(int dtype, const void* x, const float* scale, void* y, long per, long n, void* stream);
+/* DropPath fused with the residual add of an active SwinTransformerLayer drop_path (common.py:386-403, 621-627): y = x +
+ * f * s[b], s[b] = floor(keep + u[b]) / keep on torch's drawn uniforms u [N] (samples = contiguous blocks of `per`
+ * elements); _grad: df = dy * s[b]. */
+int dmy_droppath_add(int dtype, const void* x, const void* f, const float* u, float keep, void* y, long per, long n,
+                     void* stream);
+int dmy_droppath_grad(int dtype, const void* dy, const float* u, float keep, void* df, long per, long n, void* stream);
 
 /* ---- optimizer step / EMA (train.py:216-222, 449-454; utils/torch_utils.py:329-339) and the GradScaler
  *      (train.py:354, 445-450).  scale / found: device [1] fp32 loss scale and non-finite flag, or both NULL

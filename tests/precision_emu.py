@@ -19,6 +19,9 @@ run again with the roundings a reduced-precision run performs, and the product i
   mode 'fp16'     the reference's own training precision, CUDA autocast (train.py:434): the same roundings to fp16
                    (conv / linear / activation outputs and weights fp16, BatchNorm statistics and the loss fp32),
                    backward seeded with a 2^16 loss scale as GradScaler does, so that fp16 gradients do not underflow;
+  (round 6: also C3TR's stored tensors -- in-projected q / k / v, the attention probabilities, the attention output and
+  the residual sums, which the oracle's functional projections had hidden from the leaf hooks -- and CoorAttention's
+  pooled means)
   mode 'fp8_sink' 'fp8' with 'bf16_sink's input-gradient roundings (the per-layer comparison of the fp8 product);
   mode 'fp8'      config 5's storage: 'bf16', and every conv the product runs on the e4m3 kernel (functional.set_fp8:
                    k >= 3, C % 128 == 0, K % 8 == 0, K >= 32) computes its FORWARD from e4m3 operands -- the input
@@ -155,6 +158,41 @@ def emulate(model, mode):
                     sa = RoundAct.apply(torch.sigmoid(m.spatial_attention.conv2d(s2)), dt)
                     return RoundAct.apply(sa * out1, dt)
                 mod.forward = cbam_fwd
+    if hasattr(onn, 'TransformerLayer'):
+        # C3TR (config 5) as the product stores it: the in-projected q / k / v, the attention probabilities P (the
+        # flash kernel's bf16 P . V MFMA operand), the attention output o and the two residual sums (out-projection and
+        # fc2 with the residual fused into their conv epilogues: one rounding of the sum) -- the oracle calls the
+        # projections functionally, so the leaf hooks saw none of them
+        rw = lambda w: RoundWeight.apply(w, dt)  # noqa: E731
+        ra = lambda t: RoundAct.apply(t, dt)  # noqa: E731
+        for mod in model.modules():
+            if isinstance(mod, onn.TransformerLayer):
+                def tl_fwd(x, m=mod):
+                    c = x.shape[-1]
+                    x_ = m.ln1(x)
+                    q_, k_, v_ = m.q(x_), m.k(x_), m.v(x_)
+                    L, B, _ = q_.shape
+                    h = m.num_heads
+                    d = c // h
+                    W, b = m.ma.in_proj_weight, m.ma.in_proj_bias
+                    q = ra(F.linear(q_, rw(W[:c]), b[:c])).reshape(L, B * h, d).transpose(0, 1)
+                    k = ra(F.linear(k_, rw(W[c:2 * c]), b[c:2 * c])).reshape(L, B * h, d).transpose(0, 1)
+                    v = ra(F.linear(v_, rw(W[2 * c:]), b[2 * c:])).reshape(L, B * h, d).transpose(0, 1)
+                    a = ra(torch.softmax((q * (1.0 / d ** 0.5)) @ k.transpose(1, 2), dim=-1))
+                    o = ra((a @ v).transpose(0, 1).reshape(L, B, c))
+                    x = ra(m.dropout(F.linear(o, rw(m.ma.out_proj.weight), m.ma.out_proj.bias)) + x)
+                    hd = m.act(m.fc1(m.ln2(x)))
+                    return ra(x + m.dropout(F.linear(m.dropout(hd), rw(m.fc2.weight))))
+                mod.forward = tl_fwd
+            if isinstance(mod, onn.TransformerBlock):
+                def tb_fwd(x, m=mod):
+                    if m.conv is not None:
+                        x = m.conv(x)
+                    bsz, _, hh, ww = x.shape
+                    p_ = x.flatten(2).permute(2, 0, 1)
+                    t = ra(F.linear(p_, rw(m.linear.weight), m.linear.bias) + p_)
+                    return m.tr(t).permute(1, 2, 0).reshape(bsz, m.c2, hh, ww)
+                mod.forward = tb_fwd
     if hasattr(onn, 'CoorAttention'):
         for mod in model.modules():
             if isinstance(mod, onn.CoorAttention):

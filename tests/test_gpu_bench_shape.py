@@ -330,7 +330,10 @@ def test_c5_layers_fp32_product_vs_oracle():
     """Config 5 @1920 bs2 per layer in fp32 storage (act_dtype float32: the fp32 kernels, fp32 generic attention over
     3,600 tokens) against the fp32 oracle module on the same inputs and upstream gradient -- the config-5 counterpart of
     test_bench_shape_fp32_product_vs_oracle, per layer so that CBAM / SPP argmax near-ties do not chain.  No storage
-    rounding on either side: outputs <= 1e-4, input and parameter gradients <= 1e-3 relative L2, norms within 1e-3."""
+    rounding on either side: outputs <= 1e-4, input and parameter gradients <= 1e-3 relative L2, norms within 1e-3.
+    SPP's input gradient gets 2e-3: its cv1 output is summed in another fp32 order by the product and the oracle, and
+    the k = 5 / 9 / 13 max-pools route each window's gradient to whichever input wins on those last bits (round 6
+    measured 3.4e-4 .. 9.6e-4 on the four SPP layers, every other layer <= 4.3e-4, profiles/r06/c5_layers_1920.log)."""
     from module_parity import layer_parity
     rows = _collect(layer_parity('yolov5l-xs-tr-cbam-spp-bifpn.yaml', 1920, 2, prod='fp32'))
     assert len(rows) >= 15 and any(name == 'C3TR' for _, name, _ in rows)
@@ -343,7 +346,8 @@ def test_c5_layers_fp32_product_vs_oracle():
         if row['y'][0] > 1e-4:
             bad.append((i, name, 'y', row['y'][0]))
         for kd in ('dx', 'w'):
-            if kd in row and row[kd][0] > 1e-3:
+            lim = 2e-3 if (kd == 'dx' and name in ('SPP', 'SPPF')) else 1e-3
+            if kd in row and row[kd][0] > lim:
                 bad.append((i, name, kd, row[kd][0]))
         for kd in ('dxn', 'wn'):
             if kd in row and abs(row[kd][0] - 1) > 1e-3:

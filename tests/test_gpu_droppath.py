@@ -1,4 +1,5 @@
-"""GPU: DropPath's product path (models/swin.py DropPath -> Fn.SampleScaleFn -> dmy_sample_scale), which the
+"""GPU: DropPath's product paths (models/swin.py DropPath -> Fn.SampleScaleFn -> dmy_sample_scale, and DropPath.add ->
+Fn.DropPathAddFn -> dmy_droppath_add, the form the Swin layers use), which the
 model goldens bypass (they set drop_path = Identity to be deterministic).  Reference semantics, models/common.py
 drop_path: keep = 1 - p; mask = floor(keep + rand(N, 1, ...)); out = x / keep * mask -- one uniform draw per sample
 from torch's generator, so the same seed gives the same mask here.  Forward and backward are compared with that
@@ -35,6 +36,36 @@ def test_drop_path_matches_reference_formula(dtype, shape):
     kept = mask.flatten()
     assert 0 < int(kept.sum()) < shape[0], 'the seed should drop some samples and keep others'
     assert torch.all(y.float().flatten(1)[kept == 0] == 0)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(8, 64, 12, 10), (6, 49, 96), (5, 40, 7, 9)])
+def test_drop_path_add_matches_reference_formula(dtype, shape):
+    """DropPath.add (functional.DropPathAddFn, one dmy_droppath_add pass): x + DropPath(f) on the same torch draw as
+    the reference formula; dx = dy, df = dy * mask / keep.  (5, 40, 7, 9): a sample size that is no multiple of 8 (the
+    scalar path)"""
+    from dmayolo.models.swin import DropPath
+    p = 0.375
+    g = torch.Generator().manual_seed(6)
+    mk = lambda: torch.randn(*shape, generator=g).to(dtype).cuda()  # noqa: E731
+    x, f, dy = mk(), mk(), mk()
+    if x.dim() == 4:
+        x, f = (t.contiguous(memory_format=torch.channels_last) for t in (x, f))
+    x.requires_grad_(True)
+    f.requires_grad_(True)
+    m = DropPath(p).train()
+    torch.cuda.manual_seed(321)
+    y = m.add(x, f)
+    y.backward(dy)
+    torch.cuda.manual_seed(321)
+    keep = 1 - p
+    mask = (keep + torch.rand((shape[0],) + (1,) * (len(shape) - 1), dtype=torch.float32, device='cuda')).floor_()
+    ref = x.detach().float() + f.detach().float() * (mask / keep)
+    tol = dict(rtol=1e-6, atol=1e-6) if dtype == torch.float32 else dict(rtol=8e-3, atol=1e-2)
+    torch.testing.assert_close(y.float(), ref, **tol)
+    torch.testing.assert_close(x.grad.float(), dy.float(), rtol=0, atol=0)
+    torch.testing.assert_close(f.grad.float(), dy.float() * (mask / keep), **tol)
+    assert 0 < int(mask.sum()) < shape[0], 'the seed should drop some samples and keep others'
 
 
 def test_drop_path_identity_in_eval_and_at_zero():
