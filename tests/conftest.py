@@ -7,6 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, 'dma-yolo_amd')):
     if p not in sys.path:
         sys.path.insert(0, p)
+# The GPU tests' fp32 oracle / emulation runs use torch convolutions (MIOpen).  On a fresh box MIOpen's default find
+# mode compiles kernels for every new conv configuration: ~100 s per bench-shape model (config 5 @1920 bs2: 80.6 s of
+# its first forward + backward, 1.8 s with FAST; profiles/r06/miopen_probe.log).  FAST picks from its heuristics without
+# that search; the oracle is fp32 either way (TF32 off) and every GPU bound is a tolerance, not a bit pattern.
+os.environ.setdefault('MIOPEN_FIND_MODE', 'FAST')
 
 
 def pytest_configure(config):

@@ -50,6 +50,11 @@ SETS = {
              (32, 512, 96, 96, 512, 1, 1), (32, 256, 96, 96, 1024, 1, 1), (32, 256, 96, 96, 768, 1, 1),
              (32, 4096, 48, 48, 1024, 1, 1)],
     'one': [(32, 256, 96, 96, 256, 3, 1), (32, 1024, 48, 48, 1024, 3, 1)],
+    # the k > 1 GEMM views of DMA-YOLO-l @1536 bs32 with >= 256 columns (wide / 288-row / quad tiles)
+    'quad': [(32, 256, 96, 96, 256, 3, 1), (32, 512, 96, 96, 512, 3, 1), (32, 1024, 48, 48, 1024, 3, 1),
+             (32, 512, 48, 48, 512, 3, 1), (32, 256, 192, 192, 256, 3, 1), (32, 128, 384, 384, 256, 3, 2),
+             (32, 256, 192, 192, 512, 3, 2), (32, 256, 192, 192, 256, 3, 2), (32, 512, 96, 96, 1024, 3, 2),
+             (32, 512, 96, 96, 512, 3, 2)],
     # the slowest batch-1 @1536 detect layers (round-5 trace): SPPFCSPC at 48^2, the s2 3x3 / 96^2 C3 layers
     'det48': [(1, 512, 48, 48, 512, 3, 1), (1, 2048, 48, 48, 512, 1, 1), (1, 1024, 48, 48, 512, 1, 1),
               (1, 1024, 48, 48, 1024, 1, 1), (1, 512, 96, 96, 1024, 3, 2), (1, 256, 96, 96, 256, 3, 1),
