@@ -1278,7 +1278,16 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
       const int i2 = (int)(t % g.OH), bb = (int)(t / g.OH);
       pix = ((long)bb * cls.HX + 2 * i2 + cls.a) * cls.WX + 2 * j2 + cls.b;
     }
-    uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + n);
+    int nc = n;  // the output channel of column n
+    if (BUF == 4) {  // 2 x 2 class GEMM (conv_dgrad_q2): row (b, i, j), column cls * 64 + c -> dx pixel (2 i + a, 2 j + b)
+      const int j = (int)(m % g.OW);
+      const long t = m / g.OW;
+      const int i = (int)(t % g.OH), bb = (int)(t / g.OH), ca = n >> 7, cb = (n >> 6) & 1;
+      if (2 * i + ca >= cls.HX || 2 * j + cb >= cls.WX) continue;
+      pix = ((long)bb * cls.HX + 2 * i + ca) * cls.WX + 2 * j + cb;
+      nc = n & 63;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + nc);
     if (!DG && ep.on) {
       epi_store<bf16, 8>(ep, ct + row * RS + cv * 8, y + pix * g.yps + n, n, g.K, pix, true);
       continue;
@@ -1701,6 +1710,95 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
   __syncthreads();
   v3_epilogue<BM, BN, NS, DG, 1, WTR>(acc, reinterpret_cast<bf16*>(smem), bias, y, psum, psq, accumulate, g, tm, m0,
                                       n0, S2Cls{0, 0, 0, 0}, ep);
+}
+
+// ---------------------------------------------------------------- stride-2 data-grad of a 64-channel layer, one GEMM
+// dx of a 3x3 stride-2 pad-1 conv at the four output parities (a, b) of the 2 x 2 block (2i .. 2i + 1, 2j .. 2j + 1)
+// reads only dy[i .. i + 1][j .. j + 1] (class a = 0: tap kh = 1 from row i; a = 1: kh = 2 from row i, kh = 0 from row
+// i + 1; the same for columns).  So the whole data-grad is ONE GEMM over dy pixels: rows (b, i, j), K = the 2 x 2 dy
+// window x C_out (a stride-1 2 x 2 gather, zeros past the edge), columns = 4 classes x 64 input channels = 256 -- one
+// 256 x 256 wide tile (conv_fwd_w's loop and epilogue) -- with the B operand gathered from the IHWO weights:
+// B[cls * 64 + c][(dh, dw, co)] = W[c][a + 1 - 2 dh][b + 1 - 2 dw][co], zero where that tap does not exist.  It spends
+// 16 / 9 of the useful MFMA work on those zeros, against the four class GEMMs' 2..8-step K loops over 256 x 64 tiles:
+// 64 <- 128 @768^2 bs32 1936 -> 1711..1729 us, 64 <- 128 @160^2 bs64 170 -> 164 us (profiles/r06/q2_ab.log, cold caches).
+struct LdsQ2 {
+  using C3_ = Cfg3<256, 256, 2, 128>;
+  __amdgpu_buffer_rsrc_t rx, rw;
+  int H, W, xps, Cout;
+  int dh, dw, ci0;  // uniform cursor: dy window tap, channel base
+  int kl;
+  int pix[C3_::APW], i0[C3_::APW], j0[C3_::APW];
+  bool aval[C3_::APW];
+  int wrow[C3_::BPW], ra[C3_::BPW], rb[C3_::BPW];  // B row: weight row base (c * 9 * Cout), the row's class (a, b)
+  DEV LdsQ2(const bf16* dy, const bf16* wt, const Geom& g, long M, long m0, int wid, int lane, unsigned xbytes,
+            unsigned wbytes)
+      : H(g.H), W(g.W), xps((int)g.xps), Cout(g.C), dh(0), dw(0), ci0(0) {
+    rx = make_rsrc(dy, xbytes);
+    rw = make_rsrc(wt, wbytes);
+    kl = ((lane & 7) ^ ((lane >> 3) & 6)) * 8;
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      const long m = m0 + (wid * C3_::APW + j) * 8 + (lane >> 3);
+      aval[j] = m < M;
+      const int mm = (int)(aval[j] ? m : 0);
+      const int ow = mm % g.OW, t = mm / g.OW, oh = t % g.OH, b = t / g.OH;
+      i0[j] = oh;
+      j0[j] = ow;
+      pix[j] = ((b * g.H + oh) * g.W + ow) * xps;
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j) {
+      const int n = (wid * C3_::BPW + j) * 8 + (lane >> 3), cls = n >> 6;
+      wrow[j] = (n & 63) * 9 * Cout;
+      ra[j] = cls >> 1;
+      rb[j] = cls & 1;
+    }
+  }
+  DEV void issue(char* stage, int wid) {
+    const int delta = (dh * W + dw) * xps + ci0 + kl;
+#pragma unroll
+    for (int j = 0; j < C3_::APW; ++j) {
+      const bool ok = aval[j] && i0[j] + dh < H && j0[j] + dw < W;
+      blds16(rx, ok ? (unsigned)(pix[j] + delta) * 2u : kBufOob, stage + (wid * C3_::APW + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < C3_::BPW; ++j) {
+      const int kh = ra[j] + 1 - 2 * dh, kw = rb[j] + 1 - 2 * dw;
+      const bool ok = (unsigned)kh < 3u && (unsigned)kw < 3u;
+      blds16(rw, ok ? (unsigned)(wrow[j] + (kh * 3 + kw) * Cout + ci0 + kl) * 2u : kBufOob,
+             stage + C3_::A_BYTES + (wid * C3_::BPW + j) * 1024);
+    }
+    ci0 += BK;
+    if (ci0 == Cout) {
+      ci0 = 0;
+      if (++dw == 2) { dw = 0; ++dh; }
+    }
+  }
+};
+
+// gq = the GEMM view: (H, W, C, xps) = dy, (OH, OW) = dy's map (rows), K = 256, yps = dx's pixel stride; cls carries
+// dx's (HX, WX)
+__global__ void __launch_bounds__(512) conv_dgrad_q2(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
+                                                   bf16* __restrict__ dx, int accumulate, Geom gq, int gm,
+                                                   unsigned xbytes, unsigned wbytes, S2Cls cls) {
+  constexpr int NS = 2, WTR = 128;
+  using C3_ = Cfg3<256, 256, NS, WTR>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tm = xcd_remap(blockIdx.x, gm);
+  const long M = (long)gq.N * gq.OH * gq.OW;
+  const long m0 = (long)tm * 256;
+  f32x4 acc[WTR / 16][4];
+#pragma unroll
+  for (int i = 0; i < WTR / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = 4 * gq.C / BK;
+  LdsQ2 ld(dy, wt, gq, M, m0, wid, lane, xbytes, wbytes);
+  mainloop_w<256, 256, NS, WTR>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  v3_epilogue<256, 256, NS, true, 4, WTR>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr,
+                                          accumulate, gq, tm, m0, 0, cls, Epi{});
 }
 
 // ---------------------------------------------------------------- 256 x 256 half-tile pipeline (conv_fwd_8p, round 5)
@@ -3440,6 +3538,12 @@ inline bool stem_s_ok(const Geom& gv, const void* x, const void* w, const void* 
     return false;
   return 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps) < (double)v3::kBufOob && (long)gv.N * gv.H * gv.W < (1L << 31);
 }
+// column groups of a streaming-GEMM launch (conv_p1s, 512 threads, 160 KiB of LDS): each group holds ng columns of W
+// in LDS and streams every X row again
+inline int p1s_groups(int KD, int NC) {
+  const int ng = ((160 * 1024 - 512 / 64 * 256) / ((KD + 8) * 2)) / 32 * 32;
+  return ceil_div(NC, ng);
+}
 template <int KD, int NTH, bool G3 = false>
 int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
                   const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
@@ -3602,6 +3706,11 @@ Plan plan_v3(const Geom& gv, const void* x, const void* w, const void* y, int ac
   const long M = (long)gv.N * gv.OH * gv.OW;
   const bool p1 = gv.KH == 1 && gv.KW == 1 && gv.S == 1 && gv.P == 0;
   Plan pl{Kern::V3, false, false, dmy_conv_fwd_partial_rows(M, gv.K)};
+  // output-heavy 1x1 data-grads (dx channels >= 2 x dy channels) on the streaming GEMM too, when W fits <= 4 column
+  // groups (profiles/r06/p1sdg_ab.log, cold caches: 512 <- 128 @192^2 bs32 465 -> 355 us, 1024 <- 256 @96^2 269 -> 230;
+  // 1280 <- 256 (5 groups, X streamed 5 times) 318 -> 450, kept on the LDS-DMA tiles)
+  if (DG && !ep.on && p1s_ok(gv, x, w, y) && gv.K >= 2 * gv.C && p1s_groups(gv.C, gv.K) <= 4)
+    return pl.k = Kern::P1S, pl;
   if (!DG && !ep.on) {
     if (p1s_ok(gv, x, w, y) && gv.K >= 2 * gv.C) return pl.k = Kern::P1S, pl;  // output-heavy 1x1: streaming GEMM
     if (stem_s_ok(gv, x, w, y)) return pl.k = Kern::STEM, pl;  // the 16-channel 3x3 stem view (p1s, G3 gather)
@@ -3808,9 +3917,21 @@ inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const 
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
 }
+// the one-GEMM form (v3::conv_dgrad_q2) for 64 input channels, 3x3 stride 2 pad 1, a grid of >= one 256-row tile per CU
+inline bool dgrad_q2_ok(const Geom& g) {
+  return g.C == 64 && g.KH == 3 && g.KW == 3 && g.P == 1 && g.S == 2 && g.K % 64 == 0 &&
+         g.OH == (g.H + 1) / 2 && g.OW == (g.W + 1) / 2 && g.xps % 8 == 0 &&
+         ceil_div((long)g.N * g.OH * g.OW, 256) >= num_cus();
+}
 inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc, const Geom& g, hipStream_t st) {
   const unsigned xbytes = (unsigned)(2.0 * ((double)g.N * g.OH * g.OW * g.yps));
   const unsigned wbytes = (unsigned)(2.0 * g.C * g.KH * g.KW * g.K);
+  if (dgrad_q2_ok(g)) {
+    const Geom gq = make_geom(g.N, g.OH, g.OW, g.K, g.yps, 256, 2, 2, 1, 0, g.OH, g.OW, g.xps);
+    const int gm = (int)ceil_div((long)g.N * g.OH * g.OW, 256);
+    v3::conv_dgrad_q2<<<(unsigned)gm, 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes, v3::S2Cls{0, 0, g.H, g.W});
+    return (int)hipGetLastError();
+  }
   // one launch for the four classes of <= 64-channel data-grads, one per class above.  Measured
   // (profiles/r02/ab_s2_merge.log): +4..14 % at 32 / 64 channels, 16-33 % slower on the 1-block-per-CU 256 x 128 tiles
   // of the 128 / 256-channel layers, where the per-class launches stay.  The persistent class kernel (conv_s2p, round 5)

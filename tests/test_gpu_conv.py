@@ -92,6 +92,36 @@ def test_conv_dgrad_bf16_vs_torch(N, C, H, W, K, k, s, acc):
     assert _rel(dx.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize('N,H,W,K', [(4, 256, 256, 128), (3, 383, 257, 64), (10, 192, 160, 192)])
+@pytest.mark.parametrize('acc', [0, 1])
+def test_conv_dgrad_s2_one_gemm_vs_torch(N, H, W, K, acc):
+    """64-channel 3x3 stride-2 data-grad as one GEMM over dy pixels (conv_dgrad_q2: the 2 x 2 dy window against the
+    four parity classes' weights, 256 columns), taken when the grid has >= one 256-row tile per CU: even and odd maps
+    (the a = 1 / b = 1 rows and columns past an odd edge are not stored), 64 / 128 / 192 dy channels, accumulate."""
+    from dmayolo.functional import call, ptr, stream, prep_weight
+    C, k, s, p = 64, 3, 2, 1
+    g = torch.Generator().manual_seed(N * 1000 + H + K)
+    w = (torch.randn(K, C, k, k, generator=g) / (K * k * k) ** 0.5)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    assert N * OH * OW >= 256 * 256
+    dy = torch.randn(N, K, OH, OW, generator=g).bfloat16()
+    prev = torch.randn(N, C, H, W, generator=g).bfloat16()
+    conv = torch.nn.grad.conv2d_input((N, C, H, W), w.bfloat16().float().cuda(), dy.float().cuda(), stride=s, padding=p)
+    ref = conv + prev.float().cuda() if acc else conv
+    _, wt = prep_weight(w.cuda(), torch.bfloat16, True)
+    dyd = dy.cuda().contiguous(memory_format=torch.channels_last)
+    dx = prev.cuda().contiguous(memory_format=torch.channels_last)
+    rc = call('dmy_conv_dgrad', 1, ptr(dyd), ptr(wt), ptr(dx), acc, N, H, W, C, C, K, k, k, s, p, OH, OW, K, stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert _rel(dx.float(), ref) < 1e-2
+    # every pixel and channel, not just the norm: within the bf16 roundings of the stored result (the conv output,
+    # and with accumulate the sum with the previous dx as well), so relative to |conv| (+ |prev|)
+    scale = conv.abs() + (prev.float().cuda().abs() if acc else 0) + 1e-2
+    err = (dx.float() - ref).abs() / scale
+    assert float(err.max()) < 1.6e-2
+
+
 @pytest.mark.parametrize('N,C,H,W,K,k,s', SHAPES)
 def test_conv_wgrad_bf16_vs_torch(N, C, H, W, K, k, s):
     """weight gradient (v3 LDS-DMA split-K for wide layers, v2 otherwise), fp32 accumulation."""
