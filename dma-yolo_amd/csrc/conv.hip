@@ -3607,6 +3607,10 @@ int p1p_plan(const Geom& gv, int acc, const Epi& ep, F&& f) {
   if (acc || gv.K % 8 != 0 || yb >= (double)v3::kBufOob || rb >= (double)v3::kBufOob || nk < 1 ||
       (ep.res != nullptr && (ep.rps % 8 != 0 || !aligned16(ep.res))) || gv.K > kP1pMaxCols)
     return -1;
+  // 129..256 columns over a >= 1024-deep reduction: the 256 x 256 half-tile pipeline reads each input row once and
+  // keeps its 16+ K steps in flight (profiles/r06/route_ab.log, cold caches: 1024 -> 256 @96^2 fwd 224 -> 201 us,
+  // 1280 -> 256 fwd 288 -> 245, data-grad 256 <- 1024 208 -> 184; the 256-deep 256 -> 256 stays here, 86 vs 102 us)
+  if (gv.K > 128 && gv.C >= 1024) return -1;
   using std::integral_constant;
 #define P1P_CFG(BM, BN, NS, WTR) \
   return f(integral_constant<int, BM>{}, integral_constant<int, BN>{}, integral_constant<int, NS>{}, integral_constant<int, WTR>{})
