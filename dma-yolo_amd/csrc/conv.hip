@@ -2029,7 +2029,9 @@ __global__ void __launch_bounds__(512) conv_fwd_8p(const bf16* __restrict__ x, c
 // G3: the same streaming GEMM over a 3x3 stride-1 pad-1 gather of a 16-channel input (the space-to-depth stem of every
 // yolov5 / DMA-YOLO model as a k3 conv): K index = tap * 16 + channel, KD = 160 (144 + a zero tap), each
 // 16-B fragment is 8 channels of one tap of one pixel, out-of-image taps read zeros through the buffer range check.
-template <int KD, int NTH, bool G3 = false>
+// DG: the launch is a data-grad (the GEMM is the same; the argument only names the call family in a profile, so
+// tools/pmc_traffic.py can attribute its dispatches)
+template <int KD, int NTH, bool G3 = false, bool DG = false>
 __global__ void __launch_bounds__(NTH, 1) conv_p1s(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                 const float* __restrict__ bias, bf16* __restrict__ y,
                                                 float* __restrict__ psum, float* __restrict__ psq, int accumulate,
@@ -3544,7 +3546,7 @@ inline int p1s_groups(int KD, int NC) {
   const int ng = ((160 * 1024 - 512 / 64 * 256) / ((KD + 8) * 2)) / 32 * 32;
   return ceil_div(NC, ng);
 }
-template <int KD, int NTH, bool G3 = false>
+template <int KD, int NTH, bool G3 = false, bool DG = false>
 int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
                   const Geom& gv, hipStream_t st, int lds_kib, int bpc) {
   constexpr int pitch_b = (KD + 8) * 2, scratch = NTH / 64 * 256;
@@ -3556,7 +3558,7 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   const int lds = ng * pitch_b + scratch;
   static bool raised = false;
   if (!raised) {
-    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)v3::conv_p1s<KD, NTH, G3, DG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     raised = true;
   }
@@ -3566,16 +3568,17 @@ int launch_p1s_kd(const bf16* x, const bf16* w, const float* b, bf16* y, float* 
   if (nbx > maxb) nbx = maxb;
   const dim3 grid((unsigned)nbx, (unsigned)G);
   const double xb = 2.0 * ((double)gv.N * gv.H * gv.W * gv.xps);
-  v3::conv_p1s<KD, NTH, G3><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
+  v3::conv_p1s<KD, NTH, G3, DG><<<grid, NTH, lds, st>>>(x, w, b, y, ps, pq, acc, M, gv.K, ng, gv.xps, gv.yps, (unsigned)xb,
                                                ntiles, gv.KH * gv.KW * gv.C, gv.H, gv.W);
   return (int)hipGetLastError();
 }
 // training forwards: 512 threads, the whole 160 KiB of LDS for the W column group, one block per CU
+template <bool DG = false>
 inline int launch_p1s(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, float* pq, int acc,
                       const Geom& gv, hipStream_t st) {
-  if (gv.C == 64) return launch_p1s_kd<64, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
-  if (gv.C == 128) return launch_p1s_kd<128, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
-  return launch_p1s_kd<256, 512>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  if (gv.C == 64) return launch_p1s_kd<64, 512, false, DG>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  if (gv.C == 128) return launch_p1s_kd<128, 512, false, DG>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
+  return launch_p1s_kd<256, 512, false, DG>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);
 }
 
 // persistent 1x1 GEMM with the register epilogue (v3::conv_p1p): 256 x 128 tiles (3 stages; 256 x 64 for <= 64
@@ -3776,7 +3779,7 @@ int launch_v3(const bf16* x, const bf16* w, const float* b, bf16* y, float* ps, 
     return (int)hipGetLastError();                                                                            \
   }
   switch (pl.k) {
-    case Kern::P1S: return launch_p1s(x, w, b, y, ps, pq, acc, gv, st);
+    case Kern::P1S: return launch_p1s<DG>(x, w, b, y, ps, pq, acc, gv, st);
     case Kern::STEM:
       return stem_nth(gv.K) == 512 ? launch_p1s_kd<160, 512, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1)
                                    : launch_p1s_kd<160, 768, true>(x, w, b, y, ps, pq, acc, gv, st, 160, 1);

@@ -24,9 +24,10 @@ OUT = os.path.join(ROOT, 'profiles', 'pmc_mfma.json')
 
 def is_3x3(name):
     """a dispatch of a k > 1 layer: the kernels that only run them, and the shared implicit-GEMM tiles with P1 = false"""
-    if any(t in name for t in ('conv3_halo64<', 'conv_wgrad_tap<', 'conv_dgrad_s2_v3<', 'conv_s2p<', 'conv_fwd_f8<')):
+    if any(t in name for t in ('conv3_halo64<', 'conv_wgrad_tap<', 'conv_dgrad_s2_v3<', 'conv_dgrad_q2', 'conv_s2p<',
+                               'conv_fwd_f8<')):
         return True
-    if 'conv_p1s<' in name:  # <KD, NTH, G3, EPI>: G3 = the space-to-depth stem's 3x3 gather
+    if 'conv_p1s<' in name:  # <KD, NTH, G3, DG>: G3 = the space-to-depth stem's 3x3 gather
         return _targs(name, 'conv_p1s<')[2] == 'true'
     for tok, i in (('conv_fwd_w<', 2), ('conv_fwd_v3<', 3), ('conv_fwd_8p<', 0)):  # the P1 template argument
         if tok in name:

@@ -41,10 +41,10 @@ _DG_ARG = {'conv_fwd_v3<': 4,     # <BM, BN, NS, P1, DG, BUF>
            'conv_fwd_8p<': 1,     # <P1, DG>
            'conv_p1p<': 4,        # <BM, BN, NS, WTR, DG, ...>
            'conv3_halo64<': 0,    # <DG, EVAL>
-           'conv_p1_persist<': 2}
-_FWD = ('conv_p1s<',          # output-heavy 1x1 forwards and the stem (DMY_P1S=3 would also route 1x1 data-grads)
-        'conv_sk<', 'conv_fwd_split<', 'splitk_epi_kernel', 'conv_fwd_kernel<')
-_DGRAD = ('conv_dgrad_s2_v3<', 'conv_s2p<', 'conv_dgrad_kernel<')
+           'conv_p1_persist<': 2,
+           'conv_p1s<': 3}        # <KD, NTH, G3, DG>: output-heavy 1x1 forwards, the stem, output-heavy 1x1 data-grads
+_FWD = ('conv_sk<', 'conv_fwd_split<', 'splitk_epi_kernel', 'conv_fwd_kernel<')
+_DGRAD = ('conv_dgrad_s2_v3<', 'conv_dgrad_q2', 'conv_s2p<', 'conv_dgrad_kernel<')
 _WGRAD = ('conv_wgrad_v3<', 'conv_wgrad_v3n<', 'conv_wgrad_v4<', 'conv_wgrad_w<', 'conv_wgrad_tap<', 'conv_wgrad_kernel<',
           'wgrad_to_oihw_kernel', 'wgrad_s2d_to_oihw_kernel', 'wgrad_split_reduce')
 _BWD1 = ('conv1x1_bwd_bn<', 'conv1x1_bwd_bn', 'wgrad_slots_reduce')
