@@ -1712,6 +1712,38 @@ __global__ void __launch_bounds__(512) conv_fwd_w(const bf16* __restrict__ x, co
                                       n0, S2Cls{0, 0, 0, 0}, ep);
 }
 
+// ---------------------------------------------------------------- stride-2 data-grad classes on the wide / tall tiles
+// One parity class (a, b) of a stride-2 data-grad (FwdLdsB S2 mode: the class's input pixels as rows, only the taps of
+// matching parity) on conv_fwd_w's 128 x 64 wave tiles, 256 x 256 blocks, for >= 256 input channels -- the tile the
+// stride-1 views of the same widths take (the 256 x 128 / 64 x 64-wave class tiles read (64 + 64) x 64 of LDS per 32
+// MFMAs, these (128 + 64) x 64 per 64).
+template <int BM, int BN>
+__global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
+                                                     bf16* __restrict__ dx, int accumulate, Geom gv, int gm, int gn,
+                                                     unsigned xbytes, unsigned wbytes, S2Cls cls) {
+  constexpr int NS = 2, WN = BN / 64, WM = 8 / WN, WTR = BM / WM;
+  static_assert(WM * WN == 8 && WTR % 32 == 0, "8 waves of WTR x 64");
+  using C3_ = Cfg3<BM, BN, NS, WTR>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gm * gn);
+  const int tm = tile / gn, tn = tile % gn;
+  const long M = (long)gv.N * gv.OH * gv.OW;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+  f32x4 acc[WTR / 16][4];
+#pragma unroll
+  for (int i = 0; i < WTR / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = ((gv.KH - ((cls.a + gv.P) & 1) + 1) / 2) * ((gv.KW - ((cls.b + gv.P) & 1) + 1) / 2) * (gv.C / BK);
+  FwdLdsB<BM, BN, NS, false, true, true, 2, WTR> ld(dy, wt, gv, M, m0, n0, wid, lane, xbytes, wbytes, cls);
+  mainloop_w<BM, BN, NS, WTR>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, true, 3, WTR>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr, accumulate,
+                                        gv, tm, m0, n0, cls, Epi{});
+}
+
 // ---------------------------------------------------------------- stride-2 data-grad of a 64-channel layer, one GEMM
 // dx of a 3x3 stride-2 pad-1 conv at the four output parities (a, b) of the 2 x 2 block (2i .. 2i + 1, 2j .. 2j + 1)
 // reads only dy[i .. i + 1][j .. j + 1] (class a = 0: tap kh = 1 from row i; a = 1: kh = 2 from row i, kh = 0 from row
@@ -3958,7 +3990,13 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
       const Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 2, g.P, H2, W2, g.xps);
       const long M = (long)g.N * H2 * W2;
       const v3::S2Cls cls{a, b, g.H, g.W};
-      if (g.C > 64) {
+      // >= 256 input channels: the class on the 256 x 256 wide tile (profiles/r06/s2w_ab.log, cold caches: 256 <- 256
+      // @192^2 bs32 604 -> 519 us, 256 <- 512 919 -> 843, 512 <- 1024 @96^2 834 -> 770; the 512 x 128 tall tile for
+      // 128 channels measured 1228 -> 1257 and is not used)
+      if (g.C % 256 == 0 && (long)ceil_div(M, 256) * (g.C / 256) >= num_cus()) {
+        const int gm = ceil_div(M, 256), gn = g.C / 256;
+        v3::conv_dgrad_s2_w<256, 256><<<(unsigned)gm * gn, 512, 0, st>>>(dy, wt, dx, acc, gv, gm, gn, xbytes, wbytes, cls);
+      } else if (g.C > 64) {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
         v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
             dy, wt, nullptr, dx, nullptr, nullptr, acc, gv, gm, gn, xbytes, wbytes, cls, Epi{});
