@@ -1722,7 +1722,7 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
                                                      bf16* __restrict__ dx, int accumulate, Geom gv, int gm, int gn,
                                                      unsigned xbytes, unsigned wbytes, S2Cls cls) {
   constexpr int NS = 2, WN = BN / 64, WM = 8 / WN, WTR = BM / WM;
-  static_assert(WM * WN == 8 && WTR % 32 == 0, "8 waves of WTR x 64");
+  static_assert(WM * WN == 8 && WTR % 16 == 0, "8 waves of WTR x 64");
   using C3_ = Cfg3<BM, BN, NS, WTR>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3990,12 +3990,23 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
       const Geom gv = make_geom(g.N, g.OH, g.OW, g.K, g.yps, g.C, g.KH, g.KW, 2, g.P, H2, W2, g.xps);
       const long M = (long)g.N * H2 * W2;
       const v3::S2Cls cls{a, b, g.H, g.W};
-      // >= 256 input channels: the class on the 256 x 256 wide tile (profiles/r06/s2w_ab.log, cold caches: 256 <- 256
-      // @192^2 bs32 604 -> 519 us, 256 <- 512 919 -> 843, 512 <- 1024 @96^2 834 -> 770; the 512 x 128 tall tile for
-      // 128 channels measured 1228 -> 1257 and is not used)
+      // >= 256 input channels: the class on the wide tile, 256 or 288 rows (profiles/r06/s2w_ab.log and s2w288_ab.log,
+      // cold caches, against the 256 x 128 class tiles: 256 <- 256 @192^2 bs32 604 -> 519 (256 rows) -> 460 us (288),
+      // 256 <- 512 919 -> 843 -> 784, 512 <- 1024 @96^2 834 -> 758 -> 600; the 512 x 128 tall tile for 128 channels
+      // measured 1228 -> 1257 and is not used)
       if (g.C % 256 == 0 && (long)ceil_div(M, 256) * (g.C / 256) >= num_cus()) {
-        const int gm = ceil_div(M, 256), gn = g.C / 256;
-        v3::conv_dgrad_s2_w<256, 256><<<(unsigned)gm * gn, 512, 0, st>>>(dy, wt, dx, acc, gv, gm, gn, xbytes, wbytes, cls);
+        const int gn = g.C / 256;
+        const long NC = num_cus();
+        // 288-row tiles when their grid ends in fewer row-weighted rounds of the chip (plan_v3's rule)
+        if (ceil_div(ceil_div(M, 288) * gn, NC) * 288 < ceil_div(ceil_div(M, 256) * gn, NC) * 256) {
+          const int gm = ceil_div(M, 288);
+          v3::conv_dgrad_s2_w<288, 256><<<(unsigned)gm * gn, 512, 0, st>>>(dy, wt, dx, acc, gv, gm, gn, xbytes, wbytes,
+                                                                            cls);
+        } else {
+          const int gm = ceil_div(M, 256);
+          v3::conv_dgrad_s2_w<256, 256><<<(unsigned)gm * gn, 512, 0, st>>>(dy, wt, dx, acc, gv, gm, gn, xbytes, wbytes,
+                                                                            cls);
+        }
       } else if (g.C > 64) {
         const int gm = ceil_div(M, 256), gn = ceil_div(g.C, 128);
         v3::conv_fwd_v3<256, 128, 3, false, true, 3><<<(unsigned)gm * gn, 512, 0, st>>>(
