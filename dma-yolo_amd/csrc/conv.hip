@@ -3458,7 +3458,10 @@ inline void wgrad_end(const Geom& g, float* dw, int splits, hipStream_t st) {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // tile choice shared by launch and partial-row query
-inline bool big_tile(long M, int N) { return M >= 4096 && N > 64; }
+// v2 (register-staged) tiles: 128 x 128 only when that grid still fills the chip; the batch-1 96^2 1x1 layers
+// (9216 rows) run 64 x 64 tiles, 4x the blocks (profiles/r06/bigt_ab.log, graph-replayed: 256 -> 256 12.0 -> 8.0 us,
+// 1024 -> 256 22.1 -> 16.9 us; batch-1 detect p50 DMA-1536 4.41 -> 4.30 ms, yolov5s 0.629 -> 0.608 ms)
+inline bool big_tile(long M, int N) { return M >= 4096 && N > 64 && ceil_div(M, 128) * ceil_div(N, 128) >= 256; }
 
 template <typename T, int BM, int BN>
 int launch_fwd(const T* x, const T* w, const float* b, T* y, float* ps, float* pq, const Geom& g, hipStream_t st,
