@@ -3768,7 +3768,11 @@ Plan plan_v3(const Geom& gv, const void* x, const void* w, const void* y, int ac
     return pl;
   }
   if (pl.buf && gv.K >= kWideMinCols && (long)ceil_div(M, 256) * ceil_div(gv.K, 256) >= num_cus()) {
-    if (p1) return pl.k = Kern::PIPE8, pl;  // 1x1 views: the half-tile pipeline (conv_fwd_8p)
+    // 1x1 views: the half-tile pipeline (conv_fwd_8p); an inference launch with <= 2 K steps (<= 128 input channels)
+    // keeps the 256 x 128 tiles, whose grid is twice as wide (batch-1 128 -> 512 @192^2 37.6 -> 31.7 us, detect p50
+    // @1536 4.25 -> 4.19 ms, profiles/r06/ep8_ab.log)
+    if (p1 && ep.on && gv.C <= 128) return pl;
+    if (p1) return pl.k = Kern::PIPE8, pl;
     // k > 1: 256- or 288-row tiles, whichever grid ends in fewer row-weighted rounds of the chip.  A block per CU at a
     // time, so a grid of 4.5 rounds (3x3 256 @96^2 bs32: 1152 tiles of 256 rows) costs 5 and idles half the chip for
     // the last; 288 = 9 x 32 divides every DMA-YOLO @1536 / config-5 @1920 map (1536^2 and 1920^2 carry a factor 9):
