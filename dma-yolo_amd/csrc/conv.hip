@@ -3458,10 +3458,14 @@ inline void wgrad_end(const Geom& g, float* dw, int splits, hipStream_t st) {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // tile choice shared by launch and partial-row query
-// v2 (register-staged) tiles: 128 x 128 only when that grid still fills the chip; the batch-1 96^2 1x1 layers
-// (9216 rows) run 64 x 64 tiles, 4x the blocks (profiles/r06/bigt_ab.log, graph-replayed: 256 -> 256 12.0 -> 8.0 us,
-// 1024 -> 256 22.1 -> 16.9 us; batch-1 detect p50 DMA-1536 4.41 -> 4.30 ms, yolov5s 0.629 -> 0.608 ms)
-inline bool big_tile(long M, int N) { return M >= 4096 && N > 64 && ceil_div(M, 128) * ceil_div(N, 128) >= 256; }
+// v2 (register-staged) tiles.  The BN partial-row numbering of every training forward (dmy_conv_fwd_partial_rows:
+// one row per 64 output rows when 128-row tiles are taken, per 32 otherwise) follows big_tile_rows, so a launch that
+// writes partials keeps that rule.  Launches without partials (inference, data-grads) take 128 x 128 tiles only when
+// that grid still fills the chip: the batch-1 96^2 1x1 layers (9216 rows) run 64 x 64 tiles, 4x the blocks
+// (profiles/r06/bigt_ab.log, graph-replayed: 256 -> 256 12.0 -> 8.0 us, 1024 -> 256 22.1 -> 16.9 us; batch-1 detect
+// p50 DMA-1536 4.41 -> 4.30 ms, yolov5s 0.629 -> 0.608 ms)
+inline bool big_tile_rows(long M, int N) { return M >= 4096 && N > 64; }
+inline bool big_tile(long M, int N) { return big_tile_rows(M, N) && ceil_div(M, 128) * ceil_div(N, 128) >= 256; }
 
 template <typename T, int BM, int BN>
 int launch_fwd(const T* x, const T* w, const float* b, T* y, float* ps, float* pq, const Geom& g, hipStream_t st,
@@ -3951,7 +3955,7 @@ int conv_fwd_t(const void* x, const void* w, const float* b, void* y, float* ps,
       default: return launch_v3<false>((const bf16*)x, (const bf16*)w, b, (bf16*)y, ps, pq, 0, g, st, ep, pl);
     }
   }
-  if (big_tile(M, g.K))
+  if (ps != nullptr ? big_tile_rows(M, g.K) : big_tile(M, g.K))
     return launch_fwd<T, 128, 128>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
   return launch_fwd<T, 64, 64>((const T*)x, (const T*)w, b, (T*)y, ps, pq, g, st, ep);
 }
@@ -4345,7 +4349,7 @@ inline bool fp8_fwd_ok(int C, int K, long yps, const void* x8, const void* w8, c
          xbytes < (double)v3::kBufOob && wbytes < (double)v3::kBufOob;
 }
 
-DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile(M, K) ? 128 : 64); }
+DMY_API int dmy_conv_fwd_partial_rows(long M, int K) { return 2 * ceil_div(M, big_tile_rows(M, K) ? 128 : 64); }
 
 DMY_API long dmy_conv_fwd_bound_rows(long M, int K) {
   const long r = dmy_conv_fwd_partial_rows(M, K);

@@ -190,7 +190,12 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
         # per-parameter grad-norm vector is too heavy-tailed for a median bound at these sample sizes: over three runs
         # (round 6, profiles/r06/dma1536_distribution.log) the 15 emulation realizations spread 1.2e-2 .. 1.9e-1
         # (median 4.1e-2) and the product realizations 2.8e-2 .. 7.5e-2 (median 5.2e-2), and a run's 5-sample
-        # emulation median moved from 3.2e-2 to 6.0e-2; it keeps the sanity bound (median within the emulations' range)
+        # emulation median moved from 3.2e-2 to 6.0e-2; it keeps a sanity bound: median within 1.5x the largest
+        # emulation realization.  The emulation side is not run-to-run deterministic (torch's GPU weight-grad
+        # reductions), and the product's median (5.1e-2 at HEAD) sits at about the 85th percentile of the pooled
+        # emulation realizations (1.3e-2 .. 5.8e-2 over three runs, profiles/r06/dist_rerun.log), so 'within the 5
+        # realizations' max' failed one run in three; a broken kernel sits far outside (a BN partial-row count that did
+        # not follow the tile rule gave 2.1e-1 with outputs 3.4x the emulation's, profiles/r06/gpu_suite_bs2_bug.log)
         med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
         p_gn = [r[3][0] for r in perr]
         p_wg = [r[3][1] for r in perr]
@@ -203,7 +208,7 @@ def test_bench_shape_bf16_vs_oracle(yml, img, bs):
               f'                emulation    grad-norm vector {f(e_gnv)} whole {f(e_wg)} cos {f(e_cs)}')
         assert med(p_wg) <= 1.25 * med(e_wg), (p_wg, e_wg)
         assert med(p_cos) >= med(e_cs) - 0.05, (p_cos, e_cs)
-        assert med(p_gn) <= max(e_gnv), (p_gn, e_gnv)
+        assert med(p_gn) <= 1.5 * max(e_gnv), (p_gn, e_gnv)
         for r in perr:  # every product realization's outputs / loss inside the per-realization bounds too
             for a, e in zip(r[0], env_out):
                 assert a <= 1.1 * e + 2e-3, (r[0], env_out)
