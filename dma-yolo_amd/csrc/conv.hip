@@ -1279,13 +1279,15 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
       pix = ((long)bb * cls.HX + 2 * i2 + cls.a) * cls.WX + 2 * j2 + cls.b;
     }
     int nc = n;  // the output channel of column n
-    if (BUF == 4) {  // 2 x 2 class GEMM (conv_dgrad_q2): row (b, i, j), column cls * 64 + c -> dx pixel (2 i + a, 2 j + b)
+    if (BUF == 4 || BUF == 5) {  // 2 x 2 class GEMM (conv_dgrad_q2): row (b, i, j) -> dx pixel (2 i + a, 2 j + b) of
+      // column cls * 64 + c (BUF 4), of column b * 128 + c at the tile's row class cls.a (BUF 5)
       const int j = (int)(m % g.OW);
       const long t = m / g.OW;
-      const int i = (int)(t % g.OH), bb = (int)(t / g.OH), ca = n >> 7, cb = (n >> 6) & 1;
+      const int i = (int)(t % g.OH), bb = (int)(t / g.OH);
+      const int ca = BUF == 4 ? n >> 7 : cls.a, cb = BUF == 4 ? (n >> 6) & 1 : n >> 7;
       if (2 * i + ca >= cls.HX || 2 * j + cb >= cls.WX) continue;
       pix = ((long)bb * cls.HX + 2 * i + ca) * cls.WX + 2 * j + cb;
-      nc = n & 63;
+      nc = n & (BUF == 4 ? 63 : 127);
     }
     uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + nc);
     if (!DG && ep.on) {
@@ -1744,7 +1746,7 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
                                         gv, tm, m0, n0, cls, Epi{});
 }
 
-// ---------------------------------------------------------------- stride-2 data-grad of a 64-channel layer, one GEMM
+// ---------------------------------------------------------------- stride-2 data-grad of a 64 / 128-channel layer, one GEMM
 // dx of a 3x3 stride-2 pad-1 conv at the four output parities (a, b) of the 2 x 2 block (2i .. 2i + 1, 2j .. 2j + 1)
 // reads only dy[i .. i + 1][j .. j + 1] (class a = 0: tap kh = 1 from row i; a = 1: kh = 2 from row i, kh = 0 from row
 // i + 1; the same for columns).  So the whole data-grad is ONE GEMM over dy pixels: rows (b, i, j), K = the 2 x 2 dy
@@ -1753,7 +1755,12 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
 // B[cls * 64 + c][(dh, dw, co)] = W[c][a + 1 - 2 dh][b + 1 - 2 dw][co], zero where that tap does not exist.  It spends
 // 16 / 9 of the useful MFMA work on those zeros, against the four class GEMMs' 2..8-step K loops over 256 x 64 tiles:
 // 64 <- 128 @768^2 bs32 1936 -> 1711..1729 us, 64 <- 128 @160^2 bs64 170 -> 164 us (profiles/r06/q2_ab.log, cold caches).
+// CI = 128 (128 input channels): 4 classes x 128 = 512 columns do not fit one tile, so a tile holds ONE row class a
+// (columns = b x 128 + c) and walks only the dy rows that class reads: a = 0 the 1 x 2 window (K = 2 C_out, class
+// (0, 0) wastes half), a = 1 the 2 x 2 window (class (1, 0) wastes half) -- 12 / 9 of the useful work, not 16 / 9.
+template <int CI>
 struct LdsQ2 {
+  static_assert(CI == 64 || CI == 128, "one tile of 256 columns: 4 classes x 64 or 2 classes x 128");
   using C3_ = Cfg3<256, 256, 2, 128>;
   __amdgpu_buffer_rsrc_t rx, rw;
   int H, W, xps, Cout;
@@ -1763,7 +1770,7 @@ struct LdsQ2 {
   bool aval[C3_::APW];
   int wrow[C3_::BPW], ra[C3_::BPW], rb[C3_::BPW];  // B row: weight row base (c * 9 * Cout), the row's class (a, b)
   DEV LdsQ2(const bf16* dy, const bf16* wt, const Geom& g, long M, long m0, int wid, int lane, unsigned xbytes,
-            unsigned wbytes)
+            unsigned wbytes, int a)
       : H(g.H), W(g.W), xps((int)g.xps), Cout(g.C), dh(0), dw(0), ci0(0) {
     rx = make_rsrc(dy, xbytes);
     rw = make_rsrc(wt, wbytes);
@@ -1780,10 +1787,16 @@ struct LdsQ2 {
     }
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j) {
-      const int n = (wid * C3_::BPW + j) * 8 + (lane >> 3), cls = n >> 6;
-      wrow[j] = (n & 63) * 9 * Cout;
-      ra[j] = cls >> 1;
-      rb[j] = cls & 1;
+      const int n = (wid * C3_::BPW + j) * 8 + (lane >> 3);
+      if constexpr (CI == 64) {
+        wrow[j] = (n & 63) * 9 * Cout;
+        ra[j] = n >> 7;
+        rb[j] = (n >> 6) & 1;
+      } else {
+        wrow[j] = (n & 127) * 9 * Cout;
+        ra[j] = a;
+        rb[j] = n >> 7;
+      }
     }
   }
   DEV void issue(char* stage, int wid) {
@@ -1809,7 +1822,8 @@ struct LdsQ2 {
 };
 
 // gq = the GEMM view: (H, W, C, xps) = dy, (OH, OW) = dy's map (rows), K = 256, yps = dx's pixel stride; cls carries
-// dx's (HX, WX)
+// dx's (HX, WX).  CI = 128: 2 gm blocks, the a = 1 tiles (twice the K loop) first
+template <int CI>
 __global__ void __launch_bounds__(512) conv_dgrad_q2(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
                                                    bf16* __restrict__ dx, int accumulate, Geom gq, int gm,
                                                    unsigned xbytes, unsigned wbytes, S2Cls cls) {
@@ -1817,7 +1831,9 @@ __global__ void __launch_bounds__(512) conv_dgrad_q2(const bf16* __restrict__ dy
   using C3_ = Cfg3<256, 256, NS, WTR>;
   __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int tm = xcd_remap(blockIdx.x, gm);
+  const int half = CI == 128 && (int)blockIdx.x >= gm;
+  const int tm = xcd_remap((int)blockIdx.x - half * gm, gm);
+  cls.a = CI == 128 ? 1 - half : 0;
   const long M = (long)gq.N * gq.OH * gq.OW;
   const long m0 = (long)tm * 256;
   f32x4 acc[WTR / 16][4];
@@ -1825,11 +1841,11 @@ __global__ void __launch_bounds__(512) conv_dgrad_q2(const bf16* __restrict__ dy
   for (int i = 0; i < WTR / 16; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = 4 * gq.C / BK;
-  LdsQ2 ld(dy, wt, gq, M, m0, wid, lane, xbytes, wbytes);
+  const int nk = (CI == 64 || cls.a ? 4 : 2) * gq.C / BK;
+  LdsQ2<CI> ld(dy, wt, gq, M, m0, wid, lane, xbytes, wbytes, cls.a);
   mainloop_w<256, 256, NS, WTR>(ld, nk, smem, acc, wid, lane);
   __syncthreads();
-  v3_epilogue<256, 256, NS, true, 4, WTR>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr,
+  v3_epilogue<256, 256, NS, true, CI == 64 ? 4 : 5, WTR>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr,
                                           accumulate, gq, tm, m0, 0, cls, Epi{});
 }
 
@@ -3967,9 +3983,12 @@ inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const 
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
 }
-// the one-GEMM form (v3::conv_dgrad_q2) for 64 input channels, 3x3 stride 2 pad 1, a grid of >= one 256-row tile per CU
+// the one-GEMM form (v3::conv_dgrad_q2) for 64 / 128 input channels, 3x3 stride 2 pad 1, a grid of >= one 256-row tile
+// per CU.  128 channels, against the four 256 x 128 class launches (profiles/r06/q2h_ab.log): 128 <- 256 @384^2 bs32
+// 1318 -> 1207 us, @80^2 bs64 127 -> 103, @480^2 bs8 545 -> 460
 inline bool dgrad_q2_ok(const Geom& g) {
-  return g.C == 64 && g.KH == 3 && g.KW == 3 && g.P == 1 && g.S == 2 && g.K % 64 == 0 &&
+  if (g.C != 64 && g.C != 128) return false;
+  return g.KH == 3 && g.KW == 3 && g.P == 1 && g.S == 2 && g.K % 64 == 0 &&
          g.OH == (g.H + 1) / 2 && g.OW == (g.W + 1) / 2 && g.xps % 8 == 0 &&
          ceil_div((long)g.N * g.OH * g.OW, 256) >= num_cus();
 }
@@ -3979,7 +3998,11 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
   if (dgrad_q2_ok(g)) {
     const Geom gq = make_geom(g.N, g.OH, g.OW, g.K, g.yps, 256, 2, 2, 1, 0, g.OH, g.OW, g.xps);
     const int gm = (int)ceil_div((long)g.N * g.OH * g.OW, 256);
-    v3::conv_dgrad_q2<<<(unsigned)gm, 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes, v3::S2Cls{0, 0, g.H, g.W});
+    if (g.C == 64)
+      v3::conv_dgrad_q2<64><<<(unsigned)gm, 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes, v3::S2Cls{0, 0, g.H, g.W});
+    else
+      v3::conv_dgrad_q2<128><<<(unsigned)(2 * gm), 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes,
+                                                                 v3::S2Cls{0, 0, g.H, g.W});
     return (int)hipGetLastError();
   }
   // one launch for the four classes of <= 64-channel data-grads, one per class above.  Measured
