@@ -1758,6 +1758,7 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
 // CI = 128 (128 input channels): 4 classes x 128 = 512 columns do not fit one tile, so a tile holds ONE row class a
 // (columns = b x 128 + c) and walks only the dy rows that class reads: a = 0 the 1 x 2 window (K = 2 C_out, class
 // (0, 0) wastes half), a = 1 the 2 x 2 window (class (1, 0) wastes half) -- 12 / 9 of the useful work, not 16 / 9.
+// (The same split for 64 channels on 256 x 128 tiles measured slower at 768^2 / 960^2: profiles/r06/q2r_ab.log.)
 template <int CI>
 struct LdsQ2 {
   static_assert(CI == 64 || CI == 128, "one tile of 256 columns: 4 classes x 64 or 2 classes x 128");
