@@ -41,6 +41,12 @@ def test_bf16_training_trajectory(case):
         lh, oh = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp16')
         lb, ob = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'fp8' if fp8 else 'bf16')
         ls, os_ = tu.oracle_trajectory(cfg, nc, sd, batches, hyp, steps, 'bf16' if fp8 else 'bf16_sink')
+    # the shipped default mode as well (fp32 atomics in the split-K / fused 1x1 weight-grads, a run-dependent summation
+    # order): one more product realization of the same trajectory from the same initial state
+    ld = od = None
+    if not fp8:
+        md, _ = tu.product_model(cfg, nc)
+        ld, od = tu.product_trajectory(md, batches, hyp, steps)
     cp, ch, cb, cs = tu.curve_err(lp, lr_), tu.curve_err(lh, lr_), tu.curve_err(lb, lr_), tu.curve_err(ls, lr_)
     ep, eh, eb, es = tu.out_err(op, or_), tu.out_err(oh, or_), tu.out_err(ob, or_), tu.out_err(os_, or_)
     f = lambda v: ' '.join('%.3e' % e for e in v)  # noqa: E731
@@ -79,3 +85,13 @@ def test_bf16_training_trajectory(case):
     assert max(ep) <= 0.3 and all(a <= 1.5 * e + 0.01 for a, e in zip(ep, emu_out)), (ep, emu_out)
     # the final loss level (last eighth) within 8 % of the fp32 oracle's
     assert abs(float(lp[-q:].mean()) / float(lr_[-q:].mean()) - 1) <= 0.08
+    if ld is not None:
+        # the default-mode realization: a different chaotic realization of the same run, so a little more room than the
+        # deterministic one (which the bounds above were fixed on), the same kind of bound
+        cd, ed = tu.curve_err(ld, lr_), tu.out_err(od, or_)
+        print(f'  product default mode: curve err mean {cd[0]:.3e} last quarter {cd[1]:.3e}; outputs {f(ed)}; '
+              f'last-{q} mean {float(ld[-q:].mean()):.4f}')
+        assert torch.isfinite(ld).all() and float(ld[-q:].mean()) < learn * float(ld[0])
+        assert cd[0] <= 0.1 and cd[0] <= 2.5 * emu_curve, (cd, emu_curve)
+        assert max(ed) <= 0.35 and all(a <= 2.0 * e + 0.01 for a, e in zip(ed, emu_out)), (ed, emu_out)
+        assert abs(float(ld[-q:].mean()) / float(lr_[-q:].mean()) - 1) <= 0.1
