@@ -1,4 +1,5 @@
 #!/bin/bash
+# (EXTRA: more bench flags, e.g. --fp8 for the config-5 leg the default bench line nests)
 # Round-6 profiles of HEAD (tools/gpu/r4_prof.sh with the round-6 output dir): per-launch roofline table + layer report, rocprofv3 kernel stats, and the PMC passes
 # (FETCH_SIZE, WRITE_SIZE, MFMA-busy) on the FULL 3 + 2-step bench command.  The round-3 SIGSEGV under --pmc faulted in
 # librocprofiler-sdk reading one byte past a 1 MiB host mapping (the HIP kernel-argument pool) during a dispatch
@@ -11,7 +12,7 @@ mkdir -p $OUT
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 for cfg in ${CFGS:-dma-1536 v5s-640}; do
-  ARGS="--config $cfg --also none --steps ${STEPS:-3} --warmup ${WARM:-2} --no-cpu-baseline --no-detect"
+  ARGS="--config $cfg --also none --steps ${STEPS:-3} --warmup ${WARM:-2} --no-cpu-baseline --no-detect $EXTRA"
   if [ -z "$NOTABLE" ]; then
     timeout -k 10 400 python bench.py $ARGS --layer-report --launch-table $OUT/${cfg}_launches.csv > $OUT/${cfg}_bench.json 2> $OUT/${cfg}_layers.txt
     rc=$?; echo "bench $cfg rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/${cfg}_layers.txt; exit $rc; }
@@ -22,7 +23,7 @@ for cfg in ${CFGS:-dma-1536 v5s-640}; do
   fi
   [ -n "$NOPMC" ] && continue
   # the counter passes run 1 + 1 steps: the profiler's packet callback reads past its ring on longer runs
-  PARGS="--config $cfg --also none --steps ${PSTEPS:-1} --warmup ${PWARM:-1} --no-cpu-baseline --no-detect"
+  PARGS="--config $cfg --also none --steps ${PSTEPS:-1} --warmup ${PWARM:-1} --no-cpu-baseline --no-detect $EXTRA"
   for pass in ${PASSES:-fetch write mfma}; do
     case $pass in
       fetch) ctr="FETCH_SIZE";;
