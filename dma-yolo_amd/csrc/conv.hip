@@ -1284,10 +1284,10 @@ DEV void v3_epilogue(const f32x4 (&acc)[WTR / 16][4], bf16* ct, const float* __r
       const int j = (int)(m % g.OW);
       const long t = m / g.OW;
       const int i = (int)(t % g.OH), bb = (int)(t / g.OH);
-      const int ca = BUF == 4 ? n >> 7 : cls.a, cb = BUF == 4 ? (n >> 6) & 1 : n >> 7;
+      const int ca = BUF == 4 ? n / (BN / 2) : cls.a, cb = BUF == 4 ? (n / (BN / 4)) & 1 : n >> 7;
       if (2 * i + ca >= cls.HX || 2 * j + cb >= cls.WX) continue;
       pix = ((long)bb * cls.HX + 2 * i + ca) * cls.WX + 2 * j + cb;
-      nc = n & (BUF == 4 ? 63 : 127);
+      nc = BUF == 4 ? n % (BN / 4) : n & 127;
     }
     uint4* dst = reinterpret_cast<uint4*>(y + pix * g.yps + nc);
     if (!DG && ep.on) {
@@ -1746,7 +1746,7 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
                                         gv, tm, m0, n0, cls, Epi{});
 }
 
-// ---------------------------------------------------------------- stride-2 data-grad of a 64 / 128-channel layer, one GEMM
+// ---------------------------------------------------------------- stride-2 data-grad of a 32 / 64 / 128-channel layer, one GEMM
 // dx of a 3x3 stride-2 pad-1 conv at the four output parities (a, b) of the 2 x 2 block (2i .. 2i + 1, 2j .. 2j + 1)
 // reads only dy[i .. i + 1][j .. j + 1] (class a = 0: tap kh = 1 from row i; a = 1: kh = 2 from row i, kh = 0 from row
 // i + 1; the same for columns).  So the whole data-grad is ONE GEMM over dy pixels: rows (b, i, j), K = the 2 x 2 dy
@@ -1759,10 +1759,12 @@ __global__ void __launch_bounds__(512) conv_dgrad_s2_w(const bf16* __restrict__ 
 // (columns = b x 128 + c) and walks only the dy rows that class reads: a = 0 the 1 x 2 window (K = 2 C_out, class
 // (0, 0) wastes half), a = 1 the 2 x 2 window (class (1, 0) wastes half) -- 12 / 9 of the useful work, not 16 / 9.
 // (The same split for 64 channels on 256 x 128 tiles measured slower at 768^2 / 960^2: profiles/r06/q2r_ab.log.)
-template <int CI>
+// CI = 32: all four classes x 32 channels = 128 columns on 256 x 128 tiles (conv_fwd_v3's 3-stage loop, conv_dgrad_q2s).
+template <int CI, int BN = 256>
 struct LdsQ2 {
-  static_assert(CI == 64 || CI == 128, "one tile of 256 columns: 4 classes x 64 or 2 classes x 128");
-  using C3_ = Cfg3<256, 256, 2, 128>;
+  static constexpr bool ALL = 4 * CI == BN;  // all four classes in one tile, else one row class a per tile
+  static_assert((BN == 256 && (CI == 64 || CI == 128)) || (BN == 128 && CI == 32), "4 x 64 | 2 x 128 | 4 x 32 columns");
+  using C3_ = Cfg3<256, BN, BN == 256 ? 2 : 3, BN == 256 ? 128 : 64>;
   __amdgpu_buffer_rsrc_t rx, rw;
   int H, W, xps, Cout;
   int dh, dw, ci0;  // uniform cursor: dy window tap, channel base
@@ -1789,15 +1791,9 @@ struct LdsQ2 {
 #pragma unroll
     for (int j = 0; j < C3_::BPW; ++j) {
       const int n = (wid * C3_::BPW + j) * 8 + (lane >> 3);
-      if constexpr (CI == 64) {
-        wrow[j] = (n & 63) * 9 * Cout;
-        ra[j] = n >> 7;
-        rb[j] = (n >> 6) & 1;
-      } else {
-        wrow[j] = (n & 127) * 9 * Cout;
-        ra[j] = a;
-        rb[j] = n >> 7;
-      }
+      wrow[j] = (n % CI) * 9 * Cout;
+      ra[j] = ALL ? n / (2 * CI) : a;
+      rb[j] = (n / CI) & 1;
     }
   }
   DEV void issue(char* stage, int wid) {
@@ -1848,6 +1844,30 @@ __global__ void __launch_bounds__(512) conv_dgrad_q2(const bf16* __restrict__ dy
   __syncthreads();
   v3_epilogue<256, 256, NS, true, CI == 64 ? 4 : 5, WTR>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr,
                                           accumulate, gq, tm, m0, 0, cls, Epi{});
+}
+
+// CI = 32: the four classes x 32 channels = 128 columns, one 256 x 128 tile per 256 dy pixels (16 / 9 of the work)
+__global__ void __launch_bounds__(512) conv_dgrad_q2s(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
+                                                    bf16* __restrict__ dx, int accumulate, Geom gq, int gm,
+                                                    unsigned xbytes, unsigned wbytes, S2Cls cls) {
+  constexpr int BM = 256, BN = 128, NS = 3;
+  using C3_ = Cfg3<BM, BN, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3_::LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tm = xcd_remap((int)blockIdx.x, gm);
+  const long M = (long)gq.N * gq.OH * gq.OW;
+  const long m0 = (long)tm * BM;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = 4 * gq.C / BK;
+  LdsQ2<32, BN> ld(dy, wt, gq, M, m0, wid, lane, xbytes, wbytes, 0);
+  mainloop4<BM, BN, NS>(ld, nk, smem, acc, wid, lane);
+  __syncthreads();
+  v3_epilogue<BM, BN, NS, true, 4>(acc, reinterpret_cast<bf16*>(smem), nullptr, dx, nullptr, nullptr, accumulate, gq, tm,
+                                   m0, 0, cls, Epi{});
 }
 
 // ---------------------------------------------------------------- 256 x 256 half-tile pipeline (conv_fwd_8p, round 5)
@@ -3984,11 +4004,12 @@ inline bool dgrad_s2_v3_ok(const Geom& g, const void* dy, const void* wt, const 
   const double xb = 2.0 * ((double)g.N * g.OH * g.OW * g.yps), wb = 2.0 * g.C * g.KH * g.KW * g.K;
   return v3_ok(g.K, g.yps, g.C, g.xps, dy, wt, dx, Mmin) && xb < (double)v3::kBufOob && wb < (double)v3::kBufOob;
 }
-// the one-GEMM form (v3::conv_dgrad_q2) for 64 / 128 input channels, 3x3 stride 2 pad 1, a grid of >= one 256-row tile
-// per CU.  128 channels, against the four 256 x 128 class launches (profiles/r06/q2h_ab.log): 128 <- 256 @384^2 bs32
+// the one-GEMM form (v3::conv_dgrad_q2 / _q2s) for 32 / 64 / 128 input channels, 3x3 stride 2 pad 1, a grid of >= one
+// 256-row tile per CU.  32 channels, against the merged four-class launch (profiles/r06/q2s_ab.log): 32 <- 64 @320^2
+// bs64 (yolov5s) 462 -> 290 us, @384^2 bs32 318 -> 198, @640^2 bs16 436 -> 262; yolov5s step 16.60 -> 16.42 ms.  128 channels, against the four 256 x 128 class launches (profiles/r06/q2h_ab.log): 128 <- 256 @384^2 bs32
 // 1318 -> 1207 us, @80^2 bs64 127 -> 103, @480^2 bs8 545 -> 460
 inline bool dgrad_q2_ok(const Geom& g) {
-  if (g.C != 64 && g.C != 128) return false;
+  if (g.C != 32 && g.C != 64 && g.C != 128) return false;
   return g.KH == 3 && g.KW == 3 && g.P == 1 && g.S == 2 && g.K % 64 == 0 &&
          g.OH == (g.H + 1) / 2 && g.OW == (g.W + 1) / 2 && g.xps % 8 == 0 &&
          ceil_div((long)g.N * g.OH * g.OW, 256) >= num_cus();
@@ -3999,7 +4020,10 @@ inline int launch_dgrad_s2_v3(const bf16* dy, const bf16* wt, bf16* dx, int acc,
   if (dgrad_q2_ok(g)) {
     const Geom gq = make_geom(g.N, g.OH, g.OW, g.K, g.yps, 256, 2, 2, 1, 0, g.OH, g.OW, g.xps);
     const int gm = (int)ceil_div((long)g.N * g.OH * g.OW, 256);
-    if (g.C == 64)
+    if (g.C == 32) {
+      const Geom gs = make_geom(g.N, g.OH, g.OW, g.K, g.yps, 128, 2, 2, 1, 0, g.OH, g.OW, g.xps);
+      v3::conv_dgrad_q2s<<<(unsigned)gm, 512, 0, st>>>(dy, wt, dx, acc, gs, gm, xbytes, wbytes, v3::S2Cls{0, 0, g.H, g.W});
+    } else if (g.C == 64)
       v3::conv_dgrad_q2<64><<<(unsigned)gm, 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes, v3::S2Cls{0, 0, g.H, g.W});
     else
       v3::conv_dgrad_q2<128><<<(unsigned)(2 * gm), 512, 0, st>>>(dy, wt, dx, acc, gq, gm, xbytes, wbytes,

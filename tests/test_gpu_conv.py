@@ -94,12 +94,13 @@ def test_conv_dgrad_bf16_vs_torch(N, C, H, W, K, k, s, acc):
 
 @pytest.mark.parametrize('N,H,W,K', [(4, 256, 256, 128), (3, 383, 257, 64), (10, 192, 160, 192)])
 @pytest.mark.parametrize('acc', [0, 1])
-@pytest.mark.parametrize('C', [64, 128])
+@pytest.mark.parametrize('C', [32, 64, 128])
 def test_conv_dgrad_s2_one_gemm_vs_torch(N, H, W, K, acc, C):
-    """64- / 128-channel 3x3 stride-2 data-grad as one GEMM over dy pixels (conv_dgrad_q2: the 2 x 2 dy window
-    against the parity classes' weights, 256 columns = four classes x 64 channels, or one row class x two column
-    classes x 128 channels per tile), taken when the grid has >= one 256-row tile per CU: even and odd maps (the
-    a = 1 / b = 1 rows and columns past an odd edge are not stored), 64 / 128 / 192 dy channels, accumulate."""
+    """32- / 64- / 128-channel 3x3 stride-2 data-grad as one GEMM over dy pixels (conv_dgrad_q2 / _q2s: the 2 x 2 dy
+    window against the parity classes' weights; 128 columns = four classes x 32 channels, 256 = four classes x 64, or
+    one row class x two column classes x 128 channels per tile), taken when the grid has >= one 256-row tile per CU:
+    even and odd maps (the a = 1 / b = 1 rows and columns past an odd edge are not stored), 64 / 128 / 192 dy channels,
+    accumulate."""
     from dmayolo.functional import call, ptr, stream, prep_weight
     k, s, p = 3, 2, 1
     g = torch.Generator().manual_seed(N * 1000 + H + K)
