@@ -35,6 +35,7 @@ SETS = {
     'q2h': [(32, 128, 384, 384, 256, 3, 2), (64, 128, 80, 80, 256, 3, 2), (8, 128, 480, 480, 256, 3, 2)],
     'q2r': [(32, 64, 768, 768, 128, 3, 2), (64, 64, 160, 160, 128, 3, 2), (8, 64, 960, 960, 128, 3, 2)],
     'q2s': [(64, 32, 320, 320, 64, 3, 2), (32, 32, 384, 384, 64, 3, 2), (16, 32, 640, 640, 64, 3, 2)],
+    's2v5s': [(64, 256, 40, 40, 512, 3, 2), (64, 256, 40, 40, 256, 3, 2), (64, 128, 80, 80, 256, 3, 2), (64, 64, 160, 160, 128, 3, 2)],
     'stem': [(32, 16, 768, 768, 64, 3, 1), (64, 16, 320, 320, 32, 3, 1), (8, 16, 960, 960, 64, 3, 1)],
     # batch-1 1536 inference layers (dmy_conv_fwd_act path, 'infer' kind)
     'det': [(1, 256, 96, 96, 256, 1, 1), (1, 128, 192, 192, 128, 1, 1), (1, 128, 192, 192, 512, 1, 1),
